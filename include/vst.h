@@ -1,0 +1,78 @@
+/*
+ * vst.h — C ABI of libvst_hip.so, the MI355X (gfx950) kernels behind the AnimateDiff-XL +
+ * UnZipLoRA denoising path of tanmud/video_style_transfer.
+ *
+ * The reference is pure Python/PyTorch; its "FFI" for this path is the set of torch ops its
+ * plug-in classes call.  Each entry point below replaces one of those call sites (cited as
+ * reference file:line).  Conventions:
+ *   - all tensors are device pointers (bf16 unless stated), caller-owned; no allocation inside
+ *     except none at all — workspaces are caller-provided (see *_workspace_bytes);
+ *   - activations are token-major NHWC: row = (frame * H*W + pixel), C contiguous;
+ *   - `stream` is a hipStream_t; every call is asynchronous on it and graph-capturable;
+ *   - return 0 (VST_OK) on success, 1 for a bad argument, 2 for a launch failure.
+ */
+#ifndef VST_H
+#define VST_H
+#include <stddef.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Dense projection C = A.W^T (+bias) (+row_bias[m/div]) (+R), fp32 accumulate.
+ * A2 != NULL splits A along K: columns [0,K1) from A, [K1,K) from A2 (K1 % 64 == 0).
+ * With A2 = x.Acat^T and W = [W_base | s.(B (.) merger)] this is the fused base + UnZipLoRA
+ * projection: replaces LoRACompatibleLinear.forward (unziplora_unet/lora_linear.py:74-81) +
+ * UnZipLoRALinearLayerInfer.forward (unziplora_unet/unziplora_linear_layer.py:298-346), and
+ * TemporalLoRALinear.forward (animatediff/temporal_lora.py:29-32).
+ * epilogue 0: plain; 1: GEGLU (diffusers GEGLU feed-forward, unziplora_unet/unzip_attention.py
+ * ff path) with gate/hidden rows interleaved per 64-column block, output width N/2. */
+int vst_gemm(const void* A, int lda, const void* A2, int lda2, int K1, const void* W, int ldw, int M, int N, int K,
+             const float* bias, const float* row_bias, int row_bias_div, int ld_row_bias, const void* R, int ldr,
+             void* C, int ldc, int epilogue, void* stream);
+
+/* 3x3 conv, padding 1, NHWC, optional channel-concat second input, stride 1|2, fused nearest-2x
+ * upsample; Wt = [Cout][3][3][C1+C2].  Replaces the per-frame torch conv2d calls of diffusers
+ * ResnetBlock2D / Downsample2D / Upsample2D inside UNetMotionModel (called from
+ * inference_animatediff.py:110-121); temb add fused as row_bias[frame][Cout]. */
+int vst_conv3x3(const void* x1, int C1, const void* x2, int C2, int nimg, int H, int W, int stride, int upsample,
+                const void* Wt, int Cout, const float* bias, const float* row_bias, int row_bias_div, const void* R,
+                int ldr, void* out, int ldc, void* stream);
+
+/* Spatial SDPA, head_dim 64: replaces F.scaled_dot_product_attention in
+ * AnimateDiffAttnProcessor2_0.__call__ (animatediff/attention_processor.py:78-80).  K/V row
+ * batch = q batch / kv_div (replaces the repeat_interleave of text states, :63-66). */
+int vst_spatial_attention(const void* q, int ldq, const void* k, const void* v, int ldkv, void* o, int ldo,
+                          int nbatch, int heads, int Nq, int Nk, int kv_div, int head_dim, float scale, void* stream);
+
+/* Frame-axis attention (motion module / TemporalTransformerBlock, animatediff/temporal_transformer.py:66-68):
+ * token (clip b, frame f, pixel p) at row (b*F + f)*HW + p; F <= 32; head_dim in {8,16,32,40,64,80,160}. */
+int vst_temporal_attention(const void* q, const void* k, const void* v, int ldqkv, void* o, int ldo, int nclip,
+                           int F, int HW, int heads, int head_dim, float scale, void* stream);
+
+/* GroupNorm (+SiLU) over NHWC samples of rows_per_sample rows; optional 2-source channel concat. */
+size_t vst_groupnorm_workspace_bytes(int nsamples, int rows_per_sample, int groups);
+int vst_groupnorm(const void* x1, int ld1, int C1, const void* x2, int ld2, int C2, int nsamples,
+                  int rows_per_sample, int groups, float eps, const float* gamma, const float* beta, int silu_act,
+                  void* y, int ldy, void* workspace, void* stream);
+
+/* LayerNorm over C (+ sinusoidal PE row pe[(row/pe_div)%pe_mod], temporal_transformer.py:6-27). */
+int vst_layernorm(const void* x, int ldx, int C, int rows, const float* gamma, const float* beta, float eps,
+                  const float* pe, int pe_div, int pe_mod, void* y, int ldy, void* stream);
+
+/* Denoise-loop glue (inference_animatediff.py:104-131). */
+int vst_timestep_embedding(const float* t, const int* step_idx, int n, int dim, int flip_sin_to_cos,
+                           float downscale_freq_shift, void* out, int ld, int col0, int per_row, void* stream);
+int vst_pack_latents(const float* lat, int B, int Cl, int F, int HW, const float* sigmas, const int* step_idx,
+                     float fixed_scale, int ncopy, void* out, void* stream);
+int vst_euler_cfg_step(const void* noise, int ncopy, float guidance, float* lat, int B, int Cl, int F, int HW,
+                       const float* sigmas, const int* step_idx, void* stream);
+int vst_step_advance(int* step_idx, void* stream);
+int vst_silu(const void* x, void* y, size_t n, void* stream);
+int vst_add(const void* a, const void* b, void* y, size_t n, void* stream);
+int vst_copy2d(const void* x, int ldx, void* y, int ldy, int rows, int cols, void* stream);
+const char* vst_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VST_H */

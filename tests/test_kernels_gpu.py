@@ -1,0 +1,228 @@
+"""Kernel-level numerics: each HIP kernel vs a plain PyTorch fp32 reference of the same op.
+
+Tolerance: bf16 inputs are exact on both sides; kernels accumulate in fp32 and round the
+output once to bf16, so |err| <= ~1 bf16 ulp of the output (rel 2^-8) plus fp32 reassociation.
+We assert max|err| / max|ref| <= 1e-2 and rel-L2 <= 5e-3 per op.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def rnd(*shape, scale=1.0, gen=None):
+    return (torch.randn(*shape, generator=gen) * scale).to(torch.bfloat16)
+
+
+def check(out, ref, rel_l2=5e-3, rel_max=1e-2, name=""):
+    out = out.float().cpu()
+    ref = ref.float().cpu()
+    assert out.shape == ref.shape, (name, out.shape, ref.shape)
+    assert torch.isfinite(out).all(), name
+    err = (out - ref)
+    l2 = err.norm() / ref.norm().clamp_min(1e-12)
+    mx = err.abs().max() / ref.abs().max().clamp_min(1e-12)
+    assert l2 <= rel_l2 and mx <= rel_max, f"{name}: rel_l2={l2:.3e} rel_max={mx:.3e}"
+
+
+@pytest.fixture(scope="module")
+def K():
+    from video_style_transfer_amd import kernels
+    return kernels
+
+
+@pytest.mark.parametrize("M,N,Kd", [(300, 200, 192), (1024, 640, 640), (4096, 1920, 640), (77, 1280, 2048), (2, 1280, 320)])
+def test_gemm_bias_residual(cuda, K, M, N, Kd):
+    g = torch.Generator().manual_seed(M + N + Kd)
+    x, w = rnd(M, Kd, gen=g), rnd(N, Kd, scale=Kd ** -0.5, gen=g)
+    b = torch.randn(N, generator=g)
+    r = rnd(M, N, gen=g)
+    out = K.linear(x.to(cuda), w.to(cuda), b.to(cuda), residual=r.to(cuda))
+    ref = x.float() @ w.float().t() + b + r.float()
+    check(out, ref, name="gemm")
+
+
+def test_gemm_two_source_and_rowbias(cuda, K):
+    g = torch.Generator().manual_seed(7)
+    M, K1, K2, N = 640, 640, 32, 384
+    x, x2 = rnd(M, K1, gen=g), rnd(M, K2, gen=g)
+    w = rnd(N, K1 + K2, scale=0.04, gen=g)
+    rb = torch.randn(M // 64, N, generator=g)
+    out = K.linear(x.to(cuda), w.to(cuda), None, x2=x2.to(cuda), row_bias=rb.to(cuda), row_bias_div=64)
+    ref = torch.cat([x, x2], 1).float() @ w.float().t() + rb.repeat_interleave(64, 0)
+    check(out, ref, name="gemm2src")
+
+
+def test_gemm_strided_views(cuda, K):
+    g = torch.Generator().manual_seed(8)
+    big = rnd(512, 3 * 256, gen=g).to(cuda)
+    x = big[:, 256:512]  # column view, ld = 768
+    w = rnd(128, 256, scale=0.06, gen=g)
+    out = torch.zeros(512, 3 * 128, dtype=torch.bfloat16, device=cuda)
+    K.linear(x, w.to(cuda), None, out=out[:, 128:256])
+    ref = x.float().cpu() @ w.float().t()
+    check(out[:, 128:256], ref, name="gemm-views")
+    assert out[:, :128].abs().max() == 0 and out[:, 256:].abs().max() == 0
+
+
+def test_gemm_geglu(cuda, K):
+    g = torch.Generator().manual_seed(9)
+    M, C = 700, 128
+    inner = 4 * C
+    x = rnd(M, C, gen=g)
+    w = rnd(2 * inner, C, scale=C ** -0.5, gen=g)
+    b = torch.randn(2 * inner, generator=g) * 0.1
+    # interleave rows: per 64-output block j: hidden rows [64j,64j+64) then gate rows [inner+64j, ...)
+    idx = torch.cat([torch.cat([torch.arange(64 * j, 64 * j + 64), inner + torch.arange(64 * j, 64 * j + 64)])
+                     for j in range(inner // 64)])
+    out = K.linear(x.to(cuda), w[idx].contiguous().to(cuda), b[idx].contiguous().to(cuda), geglu=True)
+    y = x.float() @ w.float().t() + b
+    hdn, gate = y.chunk(2, dim=-1)
+    ref = hdn * F.gelu(gate)
+    check(out, ref, name="geglu")
+
+
+def conv_ref(x_nchw, w, b, stride=1, up=False):
+    if up:
+        x_nchw = F.interpolate(x_nchw, scale_factor=2.0, mode="nearest")
+    return F.conv2d(x_nchw, w, b, stride=stride, padding=1)
+
+
+def to_nhwc(x):  # (N,C,H,W) -> [N*H*W, C]
+    return x.permute(0, 2, 3, 1).reshape(-1, x.shape[1]).contiguous()
+
+
+def wflat(w):  # (Cout,Cin,3,3) -> [Cout, 9*Cin] (ky,kx,ci), K padded to 8
+    co, ci = w.shape[:2]
+    f = w.permute(0, 2, 3, 1).reshape(co, 9 * ci)
+    kp = (9 * ci + 7) & ~7
+    if kp != 9 * ci:
+        f = torch.cat([f, torch.zeros(co, kp - 9 * ci, dtype=f.dtype)], 1)
+    return f.contiguous()
+
+
+@pytest.mark.parametrize("n,Ci,Co,H,W,stride,up", [
+    (2, 64, 128, 16, 16, 1, False), (3, 320, 320, 8, 8, 2, False), (2, 128, 64, 8, 8, 1, True),
+    (2, 4, 320, 16, 16, 1, False), (2, 320, 4, 8, 8, 1, False), (1, 64, 64, 7, 5, 2, False)])
+def test_conv3x3(cuda, K, n, Ci, Co, H, W, stride, up):
+    g = torch.Generator().manual_seed(Ci * 7 + Co)
+    x = rnd(n, Ci, H, W, gen=g)
+    w = rnd(Co, Ci, 3, 3, scale=(9 * Ci) ** -0.5, gen=g)
+    b = torch.randn(Co, generator=g) * 0.1
+    out = K.conv3x3(to_nhwc(x).to(cuda), n, H, W, wflat(w).to(cuda), b.to(cuda), stride=stride, upsample=up)
+    ref = conv_ref(x.float(), w.float(), b, stride, up)
+    check(out, to_nhwc(ref), name="conv")
+
+
+def test_conv3x3_concat_temb_residual(cuda, K):
+    g = torch.Generator().manual_seed(11)
+    n, C1, C2, Co, H, W = 4, 128, 64, 128, 8, 8
+    x1, x2 = rnd(n, C1, H, W, gen=g), rnd(n, C2, H, W, gen=g)
+    w = rnd(Co, C1 + C2, 3, 3, scale=(9 * (C1 + C2)) ** -0.5, gen=g)
+    b = torch.randn(Co, generator=g) * 0.1
+    temb = torch.randn(n, Co, generator=g)
+    r = rnd(n, Co, H, W, gen=g)
+    out = K.conv3x3(to_nhwc(x1).to(cuda), n, H, W, wflat(w).to(cuda), b.to(cuda), x2=to_nhwc(x2).to(cuda),
+                    row_bias=temb.to(cuda), row_bias_div=H * W, residual=to_nhwc(r).to(cuda))
+    ref = conv_ref(torch.cat([x1, x2], 1).float(), w.float(), b) + temb[:, :, None, None] + r.float()
+    check(out, to_nhwc(ref), name="conv-cat")
+
+
+@pytest.mark.parametrize("nb,heads,Nq,Nk,kv_div", [(4, 2, 256, 256, 1), (2, 3, 1024, 1024, 1), (8, 2, 100, 77, 4),
+                                                   (2, 1, 64, 64, 1)])
+def test_spatial_attention(cuda, K, nb, heads, Nq, Nk, kv_div):
+    g = torch.Generator().manual_seed(Nq + Nk + heads)
+    C = heads * 64
+    q = rnd(nb * Nq, C, gen=g)
+    kv = rnd(nb // kv_div * Nk, 2 * C, gen=g)
+    qd, kvd = q.to(cuda), kv.to(cuda)
+    out = K.spatial_attention(qd, kvd[:, :C], kvd[:, C:], nb, heads, Nq, Nk, kv_div)
+    qh = q.float().view(nb, Nq, heads, 64).transpose(1, 2)
+    k = kv[:, :C].float().view(nb // kv_div, Nk, heads, 64).repeat_interleave(kv_div, 0).transpose(1, 2)
+    v = kv[:, C:].float().view(nb // kv_div, Nk, heads, 64).repeat_interleave(kv_div, 0).transpose(1, 2)
+    ref = torch.softmax(qh @ k.transpose(-1, -2) / 8.0, -1) @ v
+    check(out, ref.transpose(1, 2).reshape(nb * Nq, C), name="sdpa")
+
+
+@pytest.mark.parametrize("nclip,Fr,HW,C", [(2, 16, 64, 320), (1, 32, 16, 640), (1, 16, 8, 1280), (3, 5, 7, 64),
+                                           (2, 16, 1, 128)])
+def test_temporal_attention(cuda, K, nclip, Fr, HW, C):
+    g = torch.Generator().manual_seed(nclip * Fr + C)
+    heads, d = 8, C // 8
+    qkv = rnd(nclip * Fr * HW, 3 * C, gen=g)
+    qd = qkv.to(cuda)
+    out = K.temporal_attention(qd[:, :C], qd[:, C:2 * C], qd[:, 2 * C:], nclip, Fr, HW, heads, d)
+
+    def seq(t):  # rows (b*F+f)*HW+p -> (b*HW+p, heads, F, d)
+        return t.float().view(nclip, Fr, HW, heads, d).permute(0, 2, 3, 1, 4).reshape(nclip * HW, heads, Fr, d)
+
+    q, k, v = seq(qkv[:, :C]), seq(qkv[:, C:2 * C]), seq(qkv[:, 2 * C:])
+    o = torch.softmax(q @ k.transpose(-1, -2) / math.sqrt(d), -1) @ v
+    ref = o.view(nclip, HW, heads, Fr, d).permute(0, 3, 1, 2, 4).reshape(nclip * Fr * HW, C)
+    check(out, ref, name="temporal")
+
+
+@pytest.mark.parametrize("ns,rps,C1,C2,silu", [(4, 64, 320, 0, True), (2, 1000, 640, 0, False),
+                                               (3, 64, 128, 64, True), (1, 16 * 256, 1280, 0, False)])
+def test_group_norm(cuda, K, ns, rps, C1, C2, silu):
+    g = torch.Generator().manual_seed(ns * rps + C1)
+    x1 = rnd(ns * rps, C1, gen=g) + 0.5
+    x2 = rnd(ns * rps, C2, gen=g) if C2 else None
+    C = C1 + C2
+    gam, bet = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g) * 0.1
+    out = K.group_norm(x1.to(cuda), ns, rps, 32, 1e-5, gam.to(cuda), bet.to(cuda), silu=silu,
+                       x2=None if x2 is None else x2.to(cuda))
+    x = x1.float() if x2 is None else torch.cat([x1, x2], 1).float()
+    xs = x.view(ns, rps, C).permute(0, 2, 1)  # (N, C, L)
+    ref = F.group_norm(xs, 32, gam, bet, 1e-5).permute(0, 2, 1).reshape(ns * rps, C)
+    if silu:
+        ref = F.silu(ref)
+    check(out, ref, name="groupnorm")
+
+
+@pytest.mark.parametrize("rows,C,use_pe", [(300, 320, False), (64, 1280, True), (513, 640, True), (10, 64, False)])
+def test_layer_norm(cuda, K, rows, C, use_pe):
+    g = torch.Generator().manual_seed(rows + C)
+    x = rnd(rows, C, gen=g)
+    gam, bet = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g) * 0.1
+    pe = torch.randn(32, C, generator=g) if use_pe else None
+    HW, Fr = 4, 8
+    out = K.layer_norm(x.to(cuda), gam.to(cuda), bet.to(cuda), 1e-5, pe=None if pe is None else pe.to(cuda),
+                       pe_div=HW, pe_mod=Fr)
+    ref = F.layer_norm(x.float(), (C,), gam, bet, 1e-5)
+    if use_pe:
+        ref = ref + pe[(torch.arange(rows) // HW) % Fr]
+    check(out, ref, name="layernorm")
+
+
+def test_timestep_and_euler(cuda, K):
+    t = torch.tensor([981.0, 1.0, 500.0], device=cuda)
+    out = torch.zeros(3, 320, dtype=torch.bfloat16, device=cuda)
+    K.timestep_embedding(t, 3, 320, out)
+    half = 160
+    ex = torch.exp(-math.log(10000) * torch.arange(half, dtype=torch.float32) / half)
+    e = t.cpu()[:, None] * ex[None]
+    ref = torch.cat([torch.cos(e), torch.sin(e)], -1)
+    check(out, ref, rel_max=2e-2, name="temb")
+    # Euler + CFG
+    B, Cl, Fr, H, W = 1, 4, 3, 4, 4
+    lat = torch.randn(B, Cl, Fr, H, W)
+    sig = torch.tensor([14.6, 10.0, 0.0])
+    step = torch.zeros(1, dtype=torch.int32, device=cuda)
+    packed = torch.empty(2 * B * Fr * H * W, Cl, dtype=torch.bfloat16, device=cuda)
+    K.pack_latents(lat.to(cuda), packed, sigmas=sig.to(cuda), step_idx=step, ncopy=2)
+    ref_pack = (lat / math.sqrt(14.6 ** 2 + 1)).permute(0, 2, 3, 4, 1).reshape(-1, Cl)
+    check(packed[: B * Fr * H * W], ref_pack, name="pack")
+    check(packed[B * Fr * H * W:], ref_pack, name="pack2")
+    noise = rnd(2 * B * Fr * H * W, Cl)
+    latd = lat.to(cuda)
+    K.euler_cfg_step(noise.to(cuda), latd, sig.to(cuda), step, guidance=7.5, ncopy=2)
+    u = noise[: B * Fr * H * W].float().view(B, Fr, H, W, Cl).permute(0, 4, 1, 2, 3)
+    c = noise[B * Fr * H * W:].float().view(B, Fr, H, W, Cl).permute(0, 4, 1, 2, 3)
+    ref = lat + (0.0 - 0.0 + 10.0 - 14.6) * (u + 7.5 * (c - u))
+    check(latd, ref, rel_l2=1e-5, rel_max=1e-5, name="euler")
+    K.step_advance(step)
+    assert int(step.item()) == 1

@@ -1,0 +1,70 @@
+"""ctypes binding of libvst_hip.so (the C ABI declared in include/vst.h).
+
+This is the only place the shared library is touched.  There is deliberately no CPU or
+PyTorch fallback: if the library is missing, or a tensor is not on a HIP device, the call
+raises.  (The reference path is PyTorch eager; our kernels replace it, they do not wrap it.)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libvst_hip.so")
+
+# name -> (restype, argtypes)
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+_S = ctypes.c_size_t
+SIGNATURES = {
+    "vst_gemm": (_I, [_P, _I, _P, _I, _I, _P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _I, _P, _I, _I, _P]),
+    "vst_conv3x3": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P, _I, _P, _I, _P]),
+    "vst_spatial_attention": (_I, [_P, _I, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _F, _P]),
+    "vst_temporal_attention": (_I, [_P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _F, _P]),
+    "vst_groupnorm_workspace_bytes": (_S, [_I, _I, _I]),
+    "vst_groupnorm": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _F, _P, _P, _I, _P, _I, _P, _P]),
+    "vst_layernorm": (_I, [_P, _I, _I, _I, _P, _P, _F, _P, _I, _I, _P, _I, _P]),
+    "vst_timestep_embedding": (_I, [_P, _P, _I, _I, _I, _F, _P, _I, _I, _I, _P]),
+    "vst_pack_latents": (_I, [_P, _I, _I, _I, _I, _P, _P, _F, _I, _P, _P]),
+    "vst_euler_cfg_step": (_I, [_P, _I, _F, _P, _I, _I, _I, _I, _P, _P, _P]),
+    "vst_step_advance": (_I, [_P, _P]),
+    "vst_silu": (_I, [_P, _P, _S, _P]),
+    "vst_add": (_I, [_P, _P, _P, _S, _P]),
+    "vst_copy2d": (_I, [_P, _I, _P, _I, _I, _I, _P]),
+    "vst_version": (ctypes.c_char_p, []),
+}
+
+_lib = None
+
+
+class VstError(RuntimeError):
+    pass
+
+
+def load(path: str | None = None):
+    """Load the HIP library (idempotent).  Raises VstError when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or LIB_PATH
+    if not os.path.exists(path):
+        raise VstError(f"libvst_hip.so not found at {path}; build it with `make` (hipcc --offload-arch=gfx950)")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def exported_symbols() -> list[str]:
+    return list(SIGNATURES)
+
+
+def call(name: str, *args):
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        raise VstError(f"{name} failed with status {rc} ({'bad argument' if rc == 1 else 'launch failure'})")
+    return rc

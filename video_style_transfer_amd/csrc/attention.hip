@@ -1,0 +1,412 @@
+// Attention cores of the AnimateDiff-XL denoise path.
+//
+// 1) vst_spatial_attention: softmax(Q K^T / sqrt(64)) V per (frame, head), head_dim 64.
+//    Replaces F.scaled_dot_product_attention in AnimateDiffAttnProcessor2_0.__call__
+//    (animatediff/attention_processor.py:78-80).  Self-attention (Nk = Nq = H*W) and
+//    cross-attention over the text tokens.  The processor's repeat_interleave of the
+//    text states to B*F (:63-66) is replaced by indexing: K/V row batch = frame / kv_div,
+//    so the text K/V projection runs once per clip instead of once per frame.
+//    Flash-style: 4 waves x 32 queries; 64-key K/V tiles double-buffered in LDS;
+//    S^T = K.Q^T on v_mfma_f32_16x16x32_bf16 so each lane owns one query column and the
+//    softmax row state is lane-local (2 cross-lane shuffles per reduction);
+//    O^T = V^T.P^T with V^T fragments from ds_read_b64_tr_b16 transposed LDS reads and
+//    P^T fed straight from the S^T accumulators (no LDS round trip for P).
+//
+// 2) vst_temporal_attention: self-attention across the frame axis for every spatial
+//    position (the motion-module attention core: diffusers AnimateDiffTransformer3D /
+//    the reference's TemporalTransformerBlock, animatediff/temporal_transformer.py:66-68).
+//    Tokens stay in the spatial layout [(b*F + f)*HW + p, C]; the kernel reads the frame
+//    axis with stride HW rows, so no permute/contiguous copies are made on either side.
+//    One wave per (b, p, head); F <= 32; head_dim = C/8 (40/80/160 for SDXL).
+#include "vst_common.h"
+
+namespace vst {
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ s16x4 ds_read_tr(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4*)((__attribute__((address_space(3))) char*)(uintptr_t)(p)));
+}
+
+__device__ __forceinline__ bf16x8 cat_tr(s16x4 lo, s16x4 hi) {
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ bf16x8 pack_p8(float a0, float a1, float a2, float a3, float b0, float b1,
+                                          float b2, float b3) {
+  u32x4 u{pack2bf(a0, a1), pack2bf(a2, a3), pack2bf(b0, b1), pack2bf(b2, b3)};
+  return __builtin_bit_cast(bf16x8, u);
+}
+
+// K tile: [64 keys][64 d] bf16, 128-B rows, GEMM swizzle (ds_read_b128 row reads)
+__device__ __forceinline__ int k_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+// V tile: [64 keys][64 d], swizzle chosen for conflict-free ds_read_b64_tr_b16 over 8-row groups
+__device__ __forceinline__ int v_off(int row, int chunk) { return row * 128 + ((chunk ^ (((row >> 1) & 3) << 1)) << 4); }
+
+constexpr int SA_KT = 64;                         // keys per tile
+constexpr int SA_TILE = SA_KT * 64 * 2;           // 8 KiB
+constexpr int SA_LDS = 4 * SA_TILE;               // K,V double-buffered
+
+__global__ __launch_bounds__(256, 2) void spatial_attn_kernel(
+    const bf16_t* __restrict__ Q, int ldq, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V, int ldkv,
+    bf16_t* __restrict__ O, int ldo, int nbatch, int heads, int Nq, int Nk, int kv_div, float scale_log2,
+    uint32_t q_bytes, uint32_t kv_bytes) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nqb = (Nq + 127) / 128;
+  const int wg = xcd_remap(blockIdx.x, nqb * heads * nbatch);
+  const int qblk = wg % nqb;
+  const int bh = wg / nqb;
+  const int h = bh % heads, b = bh / heads;
+  const int bkv = b / kv_div;
+  const int fr = lane & 15, g = lane >> 4;
+
+  const auto rq = make_rsrc(Q, q_bytes);
+  const auto rk = make_rsrc(K, kv_bytes);
+  const auto rv = make_rsrc(V, kv_bytes);
+
+  // Q^T fragments (B operand of S^T = K.Q^T): lane (col q, group g) holds Q[q][32kk + 8g .. +7]
+  bf16x8 qf[2][2];
+  const int qbase = qblk * 128 + wid * 32;
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int q = qbase + qb * 16 + fr;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int off = q < Nq ? ((b * Nq + q) * ldq + h * 64 + kk * 32 + g * 8) * 2 : kOOB;
+      qf[qb][kk] = __builtin_bit_cast(bf16x8, buf_load16(rq, off));
+    }
+  }
+
+  // K/V staging: 64 rows x 8 chunks = 512 chunks per tile; 2 per thread per operand
+  const int sc = tid & 7, sr = tid >> 3;  // rows sr, sr+32
+  u32x4 kreg[2], vreg[2];
+  auto load_kv = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int key = t * SA_KT + sr + 32 * i;
+      const int off = key < Nk ? ((bkv * Nk + key) * ldkv + h * 64 + sc * 8) * 2 : kOOB;
+      kreg[i] = buf_load16(rk, off);
+      vreg[i] = buf_load16(rv, off);
+    }
+  };
+  auto store_kv = [&](int buf) {
+    char* Ks = smem + buf * 2 * SA_TILE;
+    char* Vs = Ks + SA_TILE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = sr + 32 * i;
+      *reinterpret_cast<u32x4*>(Ks + k_off(row, sc)) = kreg[i];
+      *reinterpret_cast<u32x4*>(Vs + v_off(row, sc)) = vreg[i];
+    }
+  };
+
+  f32x4 o[4][2];  // O^T accumulators [d-block][q-block]: lane col q, rows d = 16db + 4g + i
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) o[d][qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float mrun[2] = {-INFINITY, -INFINITY};
+  float lrun[2] = {0.f, 0.f};
+
+  const int nt = (Nk + SA_KT - 1) / SA_KT;
+  load_kv(0);
+  store_kv(0);
+  __syncthreads();
+
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nt) load_kv(t + 1);
+    const char* Ks = smem + cur * 2 * SA_TILE;
+    const char* Vs = Ks + SA_TILE;
+
+    // ---- S^T = K Q^T : s[kt][qb], lane col q, rows key = 16kt + 4g + i ----
+    f32x4 s[4][2];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      bf16x8 kf[2];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        kf[kk] = *reinterpret_cast<const bf16x8*>(Ks + k_off(kt * 16 + fr, kk * 4 + g));
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        f32x4 a{0.f, 0.f, 0.f, 0.f};
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[0], qf[qb][0], a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[1], qf[qb][1], a, 0, 0, 0);
+        s[kt][qb] = a;
+      }
+    }
+    // ---- mask keys beyond Nk (last tile) ----
+    if ((t + 1) * SA_KT > Nk) {
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key = t * SA_KT + kt * 16 + g * 4 + i;
+          if (key >= Nk) { s[kt][0][i] = -INFINITY; s[kt][1][i] = -INFINITY; }
+        }
+    }
+    // ---- online softmax (lane-local rows; reduce over the 4 g-lanes) ----
+    float alpha[2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mx = fmaxf(mx, s[kt][qb][i]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16));
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      const float mnew = fmaxf(mrun[qb], mx);
+      alpha[qb] = exp2f((mrun[qb] - mnew) * scale_log2);
+      mrun[qb] = mnew;
+      const float mb = mnew * scale_log2;
+      float ls = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float pv = exp2f(s[kt][qb][i] * scale_log2 - mb);
+          s[kt][qb][i] = pv;
+          ls += pv;
+        }
+      lrun[qb] = lrun[qb] * alpha[qb] + ls;
+    }
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) o[d][qb] *= alpha[qb];
+
+    // ---- O^T += V^T P^T ----
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {  // 32-key k-steps: tiles 2st (elements 0-3) and 2st+1 (4-7)
+      bf16x8 pf[2];
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+        pf[qb] = pack_p8(s[2 * st][qb][0], s[2 * st][qb][1], s[2 * st][qb][2], s[2 * st][qb][3],
+                         s[2 * st + 1][qb][0], s[2 * st + 1][qb][1], s[2 * st + 1][qb][2], s[2 * st + 1][qb][3]);
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        // lane 4q'+p' of group g: row (32st + 4g + q'), cols 16db + 4p'
+        const int li = lane & 15;
+        const int r0 = st * 32 + g * 4 + (li >> 2);
+        const int col = db * 16 + (li & 3) * 4;
+        const int ch = col >> 3, within = (col & 7) * 2;
+        const s16x4 lo = ds_read_tr(Vs + v_off(r0, ch) + within);
+        const s16x4 hi = ds_read_tr(Vs + v_off(r0 + 16, ch) + within);
+        const bf16x8 vf = cat_tr(lo, hi);
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+          o[db][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qb], o[db][qb], 0, 0, 0);
+      }
+    }
+    if (t + 1 < nt) store_kv(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- finalize: O[q][d] = O^T[d][q] / l ----
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    float l = lrun[qb];
+    l += __shfl_xor(l, 16);
+    l += __shfl_xor(l, 32);
+    const float inv = 1.0f / l;
+    const int q = qbase + qb * 16 + fr;
+    if (q >= Nq) continue;
+    bf16_t* orow = O + (size_t)(b * Nq + q) * ldo + h * 64;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const f32x4 v = o[db][qb] * inv;
+      u32x2 w{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+      *reinterpret_cast<u32x2*>(orow + db * 16 + g * 4) = w;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Temporal attention.  NT = number of 16-frame tiles (1: F<=16, 2: F<=32); D = head dim.
+template <int NT, int D>
+__global__ __launch_bounds__(256) void temporal_attn_kernel(
+    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V, int ldqkv,
+    bf16_t* __restrict__ O, int ldo, int nclip, int F, int HW, int heads, float scale_log2, uint32_t qkv_bytes) {
+  constexpr int KS = (D + 31) / 32;  // 32-deep k-steps for S
+  constexpr int DB = (D + 15) / 16;  // 16-wide d blocks for O
+  constexpr int NF = 16 * NT;
+  constexpr int VROW = DB * 32;      // bytes per V row in LDS
+  __shared__ __attribute__((aligned(16))) char vsm[4][NF * VROW];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int unit = blockIdx.x * 4 + wid;
+  const int nunits = nclip * HW * heads;
+  if (unit >= nunits) return;  // whole wave exits (unit is wave-uniform)
+  const int h = unit % heads;
+  const int bp = unit / heads;
+  const int b = bp / HW, p = bp - b * HW;
+  const int fr = lane & 15, g = lane >> 4;
+
+  const auto rq = make_rsrc(Q, qkv_bytes);
+  const auto rk = make_rsrc(K, qkv_bytes);
+  const auto rv = make_rsrc(V, qkv_bytes);
+  auto row_of = [&](int f) { return (b * F + f) * HW + p; };
+
+  // ---- stage V rows (zero rows >= F and columns >= D) ----
+  char* vs = vsm[wid];
+  constexpr int CPR = VROW / 16;  // 16-B chunks per LDS row
+  for (int idx = lane; idx < NF * CPR; idx += 64) {
+    const int f = idx / CPR, c = idx - f * CPR;
+    const int off = (f < F && c * 8 < D) ? (row_of(f) * ldqkv + h * D + c * 8) * 2 : kOOB;
+    *reinterpret_cast<u32x4*>(vs + f * VROW + c * 16) = buf_load16(rv, off);
+  }
+
+  // ---- S^T = K Q^T ----
+  f32x4 s[NT][NT];
+#pragma unroll
+  for (int a = 0; a < NT; ++a)
+#pragma unroll
+    for (int c = 0; c < NT; ++c) s[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    const int d0 = kk * 32 + g * 8;
+    bf16x8 kf[NT], qf[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+      const int f = tt * 16 + fr;
+      const int off = (f < F && d0 < D) ? (row_of(f) * ldqkv + h * D + d0) * 2 : kOOB;
+      kf[tt] = __builtin_bit_cast(bf16x8, buf_load16(rk, off));
+      qf[tt] = __builtin_bit_cast(bf16x8, buf_load16(rq, off));
+    }
+#pragma unroll
+    for (int a = 0; a < NT; ++a)
+#pragma unroll
+      for (int c = 0; c < NT; ++c) s[a][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[a], qf[c], s[a][c], 0, 0, 0);
+  }
+  // mask keys >= F
+#pragma unroll
+  for (int a = 0; a < NT; ++a)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (a * 16 + g * 4 + i >= F) {
+#pragma unroll
+        for (int c = 0; c < NT; ++c) s[a][c][i] = -INFINITY;
+      }
+  // softmax per query column
+  float inv[NT];
+#pragma unroll
+  for (int c = 0; c < NT; ++c) {
+    float mx = -INFINITY;
+#pragma unroll
+    for (int a = 0; a < NT; ++a)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) mx = fmaxf(mx, s[a][c][i]);
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float mb = mx * scale_log2;
+    float ls = 0.f;
+#pragma unroll
+    for (int a = 0; a < NT; ++a)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float pv = exp2f(s[a][c][i] * scale_log2 - mb);
+        s[a][c][i] = pv;
+        ls += pv;
+      }
+    ls += __shfl_xor(ls, 16);
+    ls += __shfl_xor(ls, 32);
+    inv[c] = 1.0f / ls;
+  }
+  // V staging stores (this wave only) complete before the transposed reads
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+
+  // ---- O^T = V^T P^T (one 32-key k-step; for NT=1 the upper 16 keys are zero) ----
+  bf16x8 pf[NT];
+#pragma unroll
+  for (int c = 0; c < NT; ++c) {
+    if (NT == 2)
+      pf[c] = pack_p8(s[0][c][0], s[0][c][1], s[0][c][2], s[0][c][3], s[NT - 1][c][0], s[NT - 1][c][1],
+                      s[NT - 1][c][2], s[NT - 1][c][3]);
+    else
+      pf[c] = pack_p8(s[0][c][0], s[0][c][1], s[0][c][2], s[0][c][3], 0.f, 0.f, 0.f, 0.f);
+  }
+  const int li = lane & 15;
+#pragma unroll
+  for (int db = 0; db < DB; ++db) {
+    const int r0 = g * 4 + (li >> 2);
+    const int colb = (db * 16 + (li & 3) * 4) * 2;
+    const s16x4 lo = ds_read_tr(vs + r0 * VROW + colb);
+    s16x4 hi = s16x4{0, 0, 0, 0};
+    if (NT == 2) hi = ds_read_tr(vs + (r0 + 16) * VROW + colb);
+    const bf16x8 vf = cat_tr(lo, hi);
+#pragma unroll
+    for (int c = 0; c < NT; ++c) {
+      f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[c], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      const int f = c * 16 + fr;
+      const int d = db * 16 + g * 4;
+      if (f < F && d < D) {
+        acc *= inv[c];
+        u32x2 w{pack2bf(acc[0], acc[1]), pack2bf(acc[2], acc[3])};
+        *reinterpret_cast<u32x2*>(O + (size_t)row_of(f) * ldo + h * D + d) = w;
+      }
+    }
+  }
+}
+
+static inline uint32_t clampb(size_t b) { return b > 0x7fffffffULL ? 0x7fffffffu : (uint32_t)b; }
+
+template <int NT, int D>
+static int launch_temporal(const bf16_t* Q, const bf16_t* K, const bf16_t* V, int ld, bf16_t* O, int ldo,
+                           int nclip, int F, int HW, int heads, float sl2, uint32_t bytes, hipStream_t s) {
+  const int units = nclip * HW * heads;
+  hipLaunchKernelGGL((temporal_attn_kernel<NT, D>), dim3((units + 3) / 4), dim3(256), 0, s, Q, K, V, ld, O, ldo,
+                     nclip, F, HW, heads, sl2, bytes);
+  return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+}
+
+}  // namespace vst
+
+using namespace vst;
+
+extern "C" int vst_spatial_attention(const void* q, int ldq, const void* k, const void* v, int ldkv, void* o,
+                                     int ldo, int nbatch, int heads, int Nq, int Nk, int kv_div, int head_dim,
+                                     float scale, void* stream) {
+  if (head_dim != 64 || !q || !k || !v || !o || nbatch <= 0 || heads <= 0 || Nq <= 0 || Nk <= 0 || kv_div <= 0)
+    return VST_ERR_ARG;
+  if ((ldq & 7) || (ldkv & 7) || (ldo & 7) || nbatch % kv_div) return VST_ERR_ARG;
+  const int nqb = (Nq + 127) / 128;
+  const int nkv = nbatch / kv_div;
+  const uint32_t qb = clampb(((size_t)(nbatch * Nq - 1) * ldq + heads * 64) * 2);
+  // K and V may be column views of one fused buffer; each rsrc is sized from its own base
+  const uint32_t kvb_v = clampb(((size_t)(nkv * Nk - 1) * ldkv + heads * 64) * 2);
+  hipLaunchKernelGGL(spatial_attn_kernel, dim3(nqb * heads * nbatch), dim3(256), SA_LDS, (hipStream_t)stream,
+                     (const bf16_t*)q, ldq, (const bf16_t*)k, (const bf16_t*)v, ldkv, (bf16_t*)o, ldo, nbatch, heads,
+                     Nq, Nk, kv_div, scale * 1.4426950408889634f, qb, kvb_v);
+  return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+}
+
+extern "C" int vst_temporal_attention(const void* q, const void* k, const void* v, int ldqkv, void* o, int ldo,
+                                      int nclip, int F, int HW, int heads, int head_dim, float scale, void* stream) {
+  if (!q || !k || !v || !o || nclip <= 0 || F <= 0 || F > 32 || HW <= 0 || heads <= 0) return VST_ERR_ARG;
+  if ((ldqkv & 7) || (ldo & 7) || (head_dim & 7)) return VST_ERR_ARG;
+  const uint32_t bytes = clampb(((size_t)(nclip * F * HW - 1) * ldqkv + heads * head_dim) * 2);
+  const float sl2 = scale * 1.4426950408889634f;
+  hipStream_t s = (hipStream_t)stream;
+  const bf16_t *Q = (const bf16_t*)q, *K = (const bf16_t*)k, *V = (const bf16_t*)v;
+  bf16_t* O = (bf16_t*)o;
+#define VST_TA(D)                                                                                    \
+  case D:                                                                                          \
+    return F <= 16 ? launch_temporal<1, D>(Q, K, V, ldqkv, O, ldo, nclip, F, HW, heads, sl2, bytes, s) \
+                   : launch_temporal<2, D>(Q, K, V, ldqkv, O, ldo, nclip, F, HW, heads, sl2, bytes, s);
+  switch (head_dim) {
+    VST_TA(8)
+    VST_TA(16)
+    VST_TA(32)
+    VST_TA(40)
+    VST_TA(64)
+    VST_TA(80)
+    VST_TA(160)
+    default:
+      return VST_ERR_ARG;
+  }
+#undef VST_TA
+}

@@ -1,0 +1,158 @@
+// Small element-wise kernels around the UNet: timestep embeddings, latent packing,
+// the fused CFG-combine + Euler step of the denoise loop, and glue (silu, add, copy).
+// Per-step scalars (timestep, sigma) are read from device tables indexed by a device
+// step counter, so one captured HIP graph of a denoise step replays for every step.
+#include "vst_common.h"
+
+namespace vst {
+
+// diffusers get_timestep_embedding (max_period 10000): value i -> row (i / per_row),
+// columns col0 + (i % per_row)*dim + [0, dim)
+__global__ void timestep_embed_kernel(const float* __restrict__ t, const int* __restrict__ step, int n, int dim,
+                                      int flip, float shift, bf16_t* __restrict__ out, int ld, int col0,
+                                      int per_row) {
+  const int half = dim / 2;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n * half) return;
+  const int i = idx / half, j = idx - i * half;
+  const float tv = step ? t[*step] : t[i];
+  const float freq = expf(-9.210340371976184f * (float)j / ((float)half - shift));  // ln(10000)
+  const float a = tv * freq;
+  const float s = sinf(a), c = cosf(a);
+  bf16_t* o = out + (size_t)(i / per_row) * ld + col0 + (i % per_row) * dim;
+  if (flip) { o[j] = f2bf(c); o[half + j] = f2bf(s); }
+  else { o[j] = f2bf(s); o[half + j] = f2bf(c); }
+}
+
+__global__ void silu_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    y[i] = f2bf(silu(bf2f(x[i])));
+}
+
+__global__ void add_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b, bf16_t* __restrict__ y,
+                           size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    y[i] = f2bf(bf2f(a[i]) + bf2f(b[i]));
+}
+
+__global__ void copy2d_kernel(const bf16_t* __restrict__ x, int ldx, bf16_t* __restrict__ y, int ldy, int rows,
+                              int cols) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= rows * cols) return;
+  const int r = idx / cols, c = idx - r * cols;
+  y[(size_t)r * ldy + c] = x[(size_t)r * ldx + c];
+}
+
+// latents fp32 (B, Cl, F, H, W) -> bf16 NHWC rows ((k*B + b)*F + f)*H*W + p, Cl channels,
+// scaled by 1/sqrt(sigma^2 + 1) (EulerDiscreteScheduler.scale_model_input), ncopy copies (CFG).
+__global__ void pack_latents_kernel(const float* __restrict__ lat, int B, int Cl, int F, int HW,
+                                    const float* __restrict__ sigmas, const int* __restrict__ step, float fixed_scale,
+                                    int ncopy, bf16_t* __restrict__ out) {
+  const size_t n = (size_t)B * Cl * F * HW;
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n) return;
+  const int p = (int)(idx % HW);
+  size_t r = idx / HW;
+  const int f = (int)(r % F); r /= F;
+  const int c = (int)(r % Cl);
+  const int b = (int)(r / Cl);
+  float scale = fixed_scale;
+  if (sigmas) { const float sg = sigmas[*step]; scale = rsqrtf(sg * sg + 1.0f); }
+  const uint16_t v = f2bf(lat[idx] * scale);
+  for (int k = 0; k < ncopy; ++k) out[((size_t)((k * B + b) * F + f) * HW + p) * Cl + c] = v;
+}
+
+// noise NHWC bf16 rows as above with ncopy=2 (k=0 uncond, k=1 cond) or 1 (no CFG).
+// latents += (sigma[step+1] - sigma[step]) * (u + g (c - u))   (Euler, epsilon prediction)
+__global__ void euler_cfg_kernel(const bf16_t* __restrict__ noise, int ncopy, float guidance, float* __restrict__ lat,
+                                 int B, int Cl, int F, int HW, const float* __restrict__ sigmas,
+                                 const int* __restrict__ step) {
+  const size_t n = (size_t)B * Cl * F * HW;
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n) return;
+  const int p = (int)(idx % HW);
+  size_t r = idx / HW;
+  const int f = (int)(r % F); r /= F;
+  const int c = (int)(r % Cl);
+  const int b = (int)(r / Cl);
+  float eps;
+  if (ncopy == 2) {
+    const float u = bf2f(noise[((size_t)(b * F + f) * HW + p) * Cl + c]);
+    const float cc = bf2f(noise[((size_t)((B + b) * F + f) * HW + p) * Cl + c]);
+    eps = u + guidance * (cc - u);
+  } else {
+    eps = bf2f(noise[((size_t)(b * F + f) * HW + p) * Cl + c]);
+  }
+  const int s = *step;
+  lat[idx] += (sigmas[s + 1] - sigmas[s]) * eps;
+}
+
+__global__ void step_advance_kernel(int* step) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) *step += 1;
+}
+
+}  // namespace vst
+
+using namespace vst;
+
+static inline int ok() { return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH; }
+
+extern "C" int vst_timestep_embedding(const float* t, const int* step_idx, int n, int dim, int flip_sin_to_cos,
+                                      float downscale_freq_shift, void* out, int ld, int col0, int per_row,
+                                      void* stream) {
+  if (!t || !out || n <= 0 || dim <= 0 || (dim & 1) || per_row <= 0) return VST_ERR_ARG;
+  const int tot = n * (dim / 2);
+  hipLaunchKernelGGL(timestep_embed_kernel, dim3((tot + 255) / 256), dim3(256), 0, (hipStream_t)stream, t, step_idx,
+                     n, dim, flip_sin_to_cos, downscale_freq_shift, (bf16_t*)out, ld, col0, per_row);
+  return ok();
+}
+
+extern "C" int vst_silu(const void* x, void* y, size_t n, void* stream) {
+  if (!x || !y) return VST_ERR_ARG;
+  const int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(silu_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, (bf16_t*)y, n);
+  return ok();
+}
+
+extern "C" int vst_add(const void* a, const void* b, void* y, size_t n, void* stream) {
+  if (!a || !b || !y) return VST_ERR_ARG;
+  const int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(add_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)a, (const bf16_t*)b,
+                     (bf16_t*)y, n);
+  return ok();
+}
+
+extern "C" int vst_copy2d(const void* x, int ldx, void* y, int ldy, int rows, int cols, void* stream) {
+  if (!x || !y || rows <= 0 || cols <= 0) return VST_ERR_ARG;
+  const int tot = rows * cols;
+  hipLaunchKernelGGL(copy2d_kernel, dim3((tot + 255) / 256), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                     ldx, (bf16_t*)y, ldy, rows, cols);
+  return ok();
+}
+
+extern "C" int vst_pack_latents(const float* lat, int B, int Cl, int F, int HW, const float* sigmas,
+                                const int* step_idx, float fixed_scale, int ncopy, void* out, void* stream) {
+  if (!lat || !out || B <= 0 || Cl <= 0 || F <= 0 || HW <= 0 || ncopy <= 0) return VST_ERR_ARG;
+  if (sigmas && !step_idx) return VST_ERR_ARG;
+  const size_t n = (size_t)B * Cl * F * HW;
+  hipLaunchKernelGGL(pack_latents_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, lat, B,
+                     Cl, F, HW, sigmas, step_idx, fixed_scale, ncopy, (bf16_t*)out);
+  return ok();
+}
+
+extern "C" int vst_euler_cfg_step(const void* noise, int ncopy, float guidance, float* lat, int B, int Cl, int F,
+                                  int HW, const float* sigmas, const int* step_idx, void* stream) {
+  if (!noise || !lat || !sigmas || !step_idx || (ncopy != 1 && ncopy != 2)) return VST_ERR_ARG;
+  const size_t n = (size_t)B * Cl * F * HW;
+  hipLaunchKernelGGL(euler_cfg_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)noise, ncopy, guidance, lat, B, Cl, F, HW, sigmas, step_idx);
+  return ok();
+}
+
+extern "C" int vst_step_advance(int* step_idx, void* stream) {
+  if (!step_idx) return VST_ERR_ARG;
+  hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, step_idx);
+  return ok();
+}
+
+extern "C" const char* vst_version(void) { return "vst-hip 0.1 gfx950"; }

@@ -1,0 +1,237 @@
+// Normalisations on NHWC / token-major activations ([rows, C], C contiguous).
+//
+// GroupNorm (32 groups) as used by the denoise path:
+//   * ResnetBlock2D norm1/norm2 (eps 1e-5, + SiLU), per frame;
+//   * Transformer2DModel.norm (eps 1e-6), per frame (unziplora_unet/transformer_2d.py:222-235);
+//   * motion-module norm (eps 1e-6) over the 5-D (B,C,F,H,W) tensor, i.e. statistics span
+//     every frame of a clip (diffusers AnimateDiffTransformer3D);
+//   * conv_norm_out (eps 1e-5, + SiLU).
+// A "sample" is `rows_per_sample` consecutive rows (H*W for per-frame, F*H*W per clip).
+// Three launches: partial (sum, sumsq) per (sample, chunk, group) -> merge to (mean, rstd)
+// with Chan's parallel-variance combine -> apply (+optional SiLU), bf16 out.  The input may
+// be two channel-concatenated sources (up-block skip concat), so the concat is never
+// materialised for the normalised branch.
+//
+// LayerNorm over C per row (BasicTransformerBlock norm1/2/3, eps 1e-5), optionally adding the
+// sinusoidal frame position table pe[(row / pe_div) % pe_mod] after the affine transform
+// (motion-module blocks add the PE to the normed input before attn1 and attn2).
+#include "vst_common.h"
+
+namespace vst {
+
+constexpr int GN_ROWS = 256;  // rows per stats chunk
+
+// x1: [rows, C1] (ld1), x2: [rows, C2] (ld2) ; channel c of the concat
+__device__ __forceinline__ const bf16_t* chan_ptr(const bf16_t* x1, int ld1, int C1, const bf16_t* x2, int ld2,
+                                                  size_t row, int c) {
+  return c < C1 ? x1 + row * ld1 + c : x2 + row * ld2 + (c - C1);
+}
+
+__global__ __launch_bounds__(256) void gn_stats_kernel(const bf16_t* __restrict__ x1, int ld1, int C1,
+                                                       const bf16_t* __restrict__ x2, int ld2, int C2,
+                                                       int rows_per_sample, int groups, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float gsm[];  // [rps][C] sums then sumsqs
+  const int C = C1 + C2;
+  const int CH = C / 8;
+  const int s = blockIdx.y, chunk = blockIdx.x;
+  const int nchunk = gridDim.x;
+  const int r_beg = chunk * GN_ROWS;
+  const int r_end = min(rows_per_sample, r_beg + GN_ROWS);
+  const size_t row0 = (size_t)s * rows_per_sample;
+  const int tid = threadIdx.x;
+  // layout: each thread owns channel chunks {cch, cch+256, ...} and a row phase
+  const int rps = CH >= 256 ? 1 : 256 / CH;  // rows per step
+  float* ssum = gsm;
+  float* ssq = gsm + rps * C;
+  for (int i = tid; i < 2 * rps * C; i += 256) gsm[i] = 0.f;
+  __syncthreads();
+  for (int cbase = 0; cbase < CH; cbase += 256) {
+    int cch, rph;
+    if (CH >= 256) { cch = cbase + tid; rph = 0; }
+    else { cch = tid % CH; rph = tid / CH; }
+    if (cch >= CH || rph >= rps) continue;
+    const int c = cch * 8;
+    float a[8], q[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { a[e] = 0.f; q[e] = 0.f; }
+    for (int r = r_beg + rph; r < r_end; r += rps) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(chan_ptr(x1, ld1, C1, x2, ld2, row0 + r, c));
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { a[e] += f[e]; q[e] += f[e] * f[e]; }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { ssum[rph * C + c + e] = a[e]; ssq[rph * C + c + e] = q[e]; }
+  }
+  __syncthreads();
+  const int Cg = C / groups;
+  for (int gi = tid; gi < groups; gi += 256) {
+    float a = 0.f, q = 0.f;
+    for (int rr = 0; rr < rps; ++rr)
+      for (int c = gi * Cg; c < (gi + 1) * Cg; ++c) { a += ssum[rr * C + c]; q += ssq[rr * C + c]; }
+    float* o = part + (((size_t)s * nchunk + chunk) * groups + gi) * 2;
+    o[0] = a;
+    o[1] = q;
+  }
+}
+
+// merge chunk partials -> mean, rstd per (sample, group)
+__global__ void gn_finalize_kernel(const float* __restrict__ part, int nchunk, int rows_per_sample, int groups,
+                                   int Cg, float eps, float* __restrict__ stats, int nsamples) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= nsamples * groups) return;
+  const int s = idx / groups, gi = idx - s * groups;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  for (int c = 0; c < nchunk; ++c) {
+    const float* p = part + (((size_t)s * nchunk + c) * groups + gi) * 2;
+    const int rows = min(GN_ROWS, rows_per_sample - c * GN_ROWS);
+    const double nb = (double)rows * Cg;
+    const double mb = p[0] / nb;
+    const double m2b = fmax((double)p[1] - (double)p[0] * mb, 0.0);
+    const double nn = n + nb;
+    const double d = mb - mean;
+    mean += d * nb / nn;
+    m2 += m2b + d * d * n * nb / nn;
+    n = nn;
+  }
+  const double var = m2 / n;
+  stats[idx * 2] = (float)mean;
+  stats[idx * 2 + 1] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+__global__ __launch_bounds__(256) void gn_apply_kernel(const bf16_t* __restrict__ x1, int ld1, int C1,
+                                                       const bf16_t* __restrict__ x2, int ld2, int C2,
+                                                       int rows_per_sample, int groups, const float* __restrict__ stats,
+                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                       int act, bf16_t* __restrict__ y, int ldy, size_t total_chunks) {
+  const int C = C1 + C2;
+  const int CH = C / 8;
+  const int Cg = C / groups;
+  for (size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x; idx < total_chunks; idx += (size_t)gridDim.x * 256) {
+    const size_t row = idx / CH;
+    const int c = (int)(idx - row * CH) * 8;
+    const int s = (int)(row / rows_per_sample);
+    float f[8];
+    unpack8(*reinterpret_cast<const u32x4*>(chan_ptr(x1, ld1, C1, x2, ld2, row, c)), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int ch = c + e;
+      const int gi = ch / Cg;
+      const float mean = stats[(s * groups + gi) * 2], rstd = stats[(s * groups + gi) * 2 + 1];
+      float v = (f[e] - mean) * rstd * gamma[ch] + beta[ch];
+      if (act) v = silu(v);
+      f[e] = v;
+    }
+    *reinterpret_cast<u32x4*>(y + row * ldy + c) = pack8(f);
+  }
+}
+
+// LayerNorm: one wave per row, up to MAXCH 8-channel chunks per lane.
+template <int MAXCH>
+__global__ __launch_bounds__(256) void layernorm_kernel(const bf16_t* __restrict__ x, int ldx, int C, int rows,
+                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                        float eps, const float* __restrict__ pe, int pe_div, int pe_mod,
+                                                        bf16_t* __restrict__ y, int ldy) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int CH = C / 8;
+  float v[MAXCH][8];
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int cc = lane + 64 * i;
+    if (cc < CH) {
+      unpack8(*reinterpret_cast<const u32x4*>(x + (size_t)row * ldx + cc * 8), v[i]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sum += v[i][e];
+    }
+  }
+  const float mean = wave_sum(sum) / C;
+  float sq = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int cc = lane + 64 * i;
+    if (cc < CH) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { const float d = v[i][e] - mean; sq += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(sq) / C + eps);
+  const float* pr = pe ? pe + (size_t)((row / pe_div) % pe_mod) * C : nullptr;
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int cc = lane + 64 * i;
+    if (cc < CH) {
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = cc * 8 + e;
+        float t = (v[i][e] - mean) * rstd * gamma[c] + beta[c];
+        if (pr) t += pr[c];
+        o[e] = t;
+      }
+      *reinterpret_cast<u32x4*>(y + (size_t)row * ldy + cc * 8) = pack8(o);
+    }
+  }
+}
+
+}  // namespace vst
+
+using namespace vst;
+
+extern "C" size_t vst_groupnorm_workspace_bytes(int nsamples, int rows_per_sample, int groups) {
+  const int nchunk = (rows_per_sample + GN_ROWS - 1) / GN_ROWS;
+  return ((size_t)nsamples * nchunk * groups * 2 + (size_t)nsamples * groups * 2) * sizeof(float);
+}
+
+extern "C" int vst_groupnorm(const void* x1, int ld1, int C1, const void* x2, int ld2, int C2, int nsamples,
+                             int rows_per_sample, int groups, float eps, const float* gamma, const float* beta,
+                             int silu_act, void* y, int ldy, void* workspace, void* stream) {
+  const int C = C1 + (x2 ? C2 : 0);
+  if (!x1 || !y || !workspace || !gamma || !beta || nsamples <= 0 || rows_per_sample <= 0 || groups <= 0)
+    return VST_ERR_ARG;
+  if (C % groups || C % 8 || C1 % 8 || (ld1 & 7) || (ldy & 7) || (x2 && (ld2 & 7))) return VST_ERR_ARG;
+  if (C > 4096) return VST_ERR_ARG;
+  if (!x2) C2 = 0;
+  hipStream_t s = (hipStream_t)stream;
+  const int nchunk = (rows_per_sample + GN_ROWS - 1) / GN_ROWS;
+  float* part = (float*)workspace;
+  float* stats = part + (size_t)nsamples * nchunk * groups * 2;
+  const int CH = C / 8;
+  const int rps = CH >= 256 ? 1 : 256 / CH;
+  const size_t lds = (size_t)2 * rps * C * sizeof(float);
+  if (lds > 64 * 1024) return VST_ERR_ARG;
+  hipLaunchKernelGGL(gn_stats_kernel, dim3(nchunk, nsamples), dim3(256), lds, s, (const bf16_t*)x1, ld1, C1,
+                     (const bf16_t*)x2, ld2, C2, rows_per_sample, groups, part);
+  const int ng = nsamples * groups;
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3((ng + 255) / 256), dim3(256), 0, s, part, nchunk, rows_per_sample,
+                     groups, C / groups, eps, stats, nsamples);
+  const size_t total = (size_t)nsamples * rows_per_sample * CH;
+  const int grid = (int)std::min<size_t>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(gn_apply_kernel, dim3(grid), dim3(256), 0, s, (const bf16_t*)x1, ld1, C1, (const bf16_t*)x2,
+                     ld2, C2, rows_per_sample, groups, stats, gamma, beta, silu_act, (bf16_t*)y, ldy, total);
+  return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+}
+
+extern "C" int vst_layernorm(const void* x, int ldx, int C, int rows, const float* gamma, const float* beta,
+                             float eps, const float* pe, int pe_div, int pe_mod, void* y, int ldy, void* stream) {
+  if (!x || !y || !gamma || !beta || rows <= 0 || C <= 0 || C % 8 || (ldx & 7) || (ldy & 7)) return VST_ERR_ARG;
+  if (pe && (pe_div <= 0 || pe_mod <= 0)) return VST_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int CH = C / 8;
+  const dim3 grid((rows + 3) / 4), blk(256);
+  if (CH <= 64)
+    hipLaunchKernelGGL(layernorm_kernel<1>, grid, blk, 0, s, (const bf16_t*)x, ldx, C, rows, gamma, beta, eps, pe,
+                       pe_div, pe_mod, (bf16_t*)y, ldy);
+  else if (CH <= 128)
+    hipLaunchKernelGGL(layernorm_kernel<2>, grid, blk, 0, s, (const bf16_t*)x, ldx, C, rows, gamma, beta, eps, pe,
+                       pe_div, pe_mod, (bf16_t*)y, ldy);
+  else if (CH <= 256)
+    hipLaunchKernelGGL(layernorm_kernel<4>, grid, blk, 0, s, (const bf16_t*)x, ldx, C, rows, gamma, beta, eps, pe,
+                       pe_div, pe_mod, (bf16_t*)y, ldy);
+  else
+    return VST_ERR_ARG;
+  return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+}

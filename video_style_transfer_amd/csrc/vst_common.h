@@ -1,0 +1,91 @@
+// Shared device helpers for the VST (video style transfer) HIP kernels.
+// gfx950 / CDNA4 only: 64-lane wavefronts, bf16 MFMA, raw buffer loads with
+// hardware range checking (out-of-range offsets read as zero, which is how
+// every kernel here implements zero padding and M/N/K tails without branches).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vst {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef uint16_t bf16_t;  // storage type of a bf16 in global memory
+
+// Offset that is always outside every buffer resource: buffer loads return 0.
+constexpr int kOOB = 0x7ffffff0;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+__device__ __forceinline__ u32x2 buf_load8(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+}
+__device__ __forceinline__ uint32_t buf_load4(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+}
+__device__ __forceinline__ uint16_t buf_load2(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+}
+
+__device__ __forceinline__ float bf2f(uint16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+// round-to-nearest-even f32 -> bf16 (NaN handled by the hardware cvt path)
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return *reinterpret_cast<uint16_t*>(&b);
+}
+__device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+__device__ __forceinline__ void unpack8(const u32x4& v, float* f) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(v[i] << 16);
+    f[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ u32x4 pack8(const float* f) {
+  u32x4 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = pack2bf(f[2 * i], f[2 * i + 1]);
+  return r;
+}
+
+__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// Bijective XCD-aware block remap (blocks b and b+8 share an XCD under
+// round-robin dispatch): consecutive logical tiles land on one XCD's L2.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (orig >> 3);
+}
+
+}  // namespace vst
+
+// C-ABI status codes (see include/vst.h)
+#define VST_OK 0
+#define VST_ERR_ARG 1
+#define VST_ERR_LAUNCH 2

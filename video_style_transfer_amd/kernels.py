@@ -1,0 +1,216 @@
+"""Tensor-level wrappers over the C ABI (libvst_hip.so).
+
+Every function takes device tensors (bf16 activations/weights, fp32 bias/norm params), checks
+shapes, and launches on torch's current HIP stream.  Activations are token-major 2-D views
+[rows, C] (row stride may exceed C, e.g. a column slice of a fused QKV buffer).
+No CPU fallback exists: a CPU tensor or a missing library raises.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _dev(t: torch.Tensor, dtype, name):
+    if not t.is_cuda:
+        raise _lib.VstError(f"{name}: tensor is on {t.device}; the HIP path has no CPU fallback")
+    if t.dtype != dtype:
+        raise _lib.VstError(f"{name}: expected {dtype}, got {t.dtype}")
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise _lib.VstError(f"{name}: expected a 2-D row-major view, got shape {tuple(t.shape)} stride {t.stride()}")
+    return t
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _ld(t):
+    return t.stride(0) if t.shape[0] > 1 else t.shape[1]
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *, x2: torch.Tensor | None = None,
+           residual: torch.Tensor | None = None, row_bias: torch.Tensor | None = None, row_bias_div: int = 1,
+           out: torch.Tensor | None = None, geglu: bool = False) -> torch.Tensor:
+    """out[M, N'] = epilogue([x | x2] @ w^T + bias + row_bias[m // div] + residual); N' = N or N/2 (GEGLU)."""
+    _dev(x, BF16, "x")
+    _dev(w, BF16, "w")
+    M, K1 = x.shape
+    N, K = w.shape
+    if x2 is not None:
+        _dev(x2, BF16, "x2")
+        if x2.shape[0] != M or K1 + x2.shape[1] != K:
+            raise _lib.VstError(f"linear: x {tuple(x.shape)} + x2 {tuple(x2.shape)} vs w {tuple(w.shape)}")
+    elif K1 != K:
+        raise _lib.VstError(f"linear: x {tuple(x.shape)} vs w {tuple(w.shape)}")
+    n_out = N // 2 if geglu else N
+    if out is None:
+        out = torch.empty((M, n_out), dtype=BF16, device=x.device)
+    _dev(out, BF16, "out")
+    if out.shape != (M, n_out):
+        raise _lib.VstError(f"linear: out shape {tuple(out.shape)} != {(M, n_out)}")
+    if bias is not None and (bias.dtype != F32 or bias.numel() != N or not bias.is_cuda):
+        raise _lib.VstError("linear: bias must be fp32 [N] on device")
+    if residual is not None:
+        _dev(residual, BF16, "residual")
+        if residual.shape != (M, n_out):
+            raise _lib.VstError("linear: residual shape mismatch")
+    if row_bias is not None:
+        if row_bias.dtype != F32 or not row_bias.is_cuda or row_bias.shape[-1] != N:
+            raise _lib.VstError("linear: row_bias must be fp32 [M/div, N]")
+    _lib.call("vst_gemm", _p(x), _ld(x), _p(x2), 0 if x2 is None else _ld(x2), K1, _p(w), _ld(w), M, N, K, _p(bias),
+              _p(row_bias), row_bias_div, N if row_bias is not None else 0, _p(residual),
+              0 if residual is None else _ld(residual), _p(out), _ld(out), 1 if geglu else 0, _stream())
+    return out
+
+
+def conv3x3(x1: torch.Tensor, nimg: int, H: int, W: int, w: torch.Tensor, bias: torch.Tensor | None, *,
+            x2: torch.Tensor | None = None, stride: int = 1, upsample: bool = False,
+            row_bias: torch.Tensor | None = None, row_bias_div: int = 1, residual: torch.Tensor | None = None,
+            out: torch.Tensor | None = None) -> torch.Tensor:
+    """NHWC 3x3 conv (pad 1).  x1: [nimg*H*W, C1] (+ x2: [nimg*H*W, C2] concatenated on channels).
+    w: [Cout, 9*(C1+C2)] laid out (ky, kx, ci).  Returns [nimg*OH*OW, Cout]."""
+    _dev(x1, BF16, "x1")
+    C1 = x1.shape[1]
+    C2 = 0
+    if x2 is not None:
+        _dev(x2, BF16, "x2")
+        C2 = x2.shape[1]
+    for t, c in ((x1, C1), (x2, C2)):
+        if t is not None and (not t.is_contiguous() or t.shape[0] != nimg * H * W):
+            raise _lib.VstError("conv3x3: inputs must be contiguous [nimg*H*W, C]")
+    _dev(w, BF16, "w")
+    Cout = w.shape[0]
+    kreal = 9 * (C1 + C2)
+    if w.shape[1] != ((kreal + 7) & ~7) and w.shape[1] != kreal:
+        raise _lib.VstError(f"conv3x3: weight {tuple(w.shape)} vs K={kreal}")
+    if upsample:
+        OH, OW = 2 * H, 2 * W
+    elif stride == 2:
+        OH, OW = (H + 1) // 2, (W + 1) // 2
+    else:
+        OH, OW = H, W
+    M = nimg * OH * OW
+    if out is None:
+        out = torch.empty((M, Cout), dtype=BF16, device=x1.device)
+    if bias is not None and (bias.dtype != F32 or bias.numel() != Cout):
+        raise _lib.VstError("conv3x3: bias must be fp32 [Cout]")
+    if residual is not None:
+        _dev(residual, BF16, "residual")
+    _lib.call("vst_conv3x3", _p(x1), C1, _p(x2), C2, nimg, H, W, stride, 1 if upsample else 0, _p(w), Cout,
+              _p(bias), _p(row_bias), row_bias_div, _p(residual), 0 if residual is None else _ld(residual), _p(out),
+              _ld(out) if Cout >= 8 else Cout, _stream())
+    return out
+
+
+def spatial_attention(q, k, v, nbatch, heads, Nq, Nk, kv_div=1, out=None, scale=None):
+    """q: [nbatch*Nq, >=heads*64] view; k/v: [nbatch/kv_div*Nk, >=heads*64] views."""
+    for n, t in (("q", q), ("k", k), ("v", v)):
+        _dev(t, BF16, n)
+    if q.shape[0] != nbatch * Nq or k.shape[0] != (nbatch // kv_div) * Nk or v.shape[0] != k.shape[0]:
+        raise _lib.VstError("spatial_attention: row counts do not match batch/Nq/Nk")
+    if k.stride(0) != v.stride(0):
+        raise _lib.VstError("spatial_attention: k and v must share a row stride")
+    if out is None:
+        out = torch.empty((nbatch * Nq, heads * 64), dtype=BF16, device=q.device)
+    _dev(out, BF16, "out")
+    scale = 0.125 if scale is None else scale
+    _lib.call("vst_spatial_attention", _p(q), _ld(q), _p(k), _p(v), k.stride(0), _p(out), _ld(out), nbatch, heads,
+              Nq, Nk, kv_div, 64, float(scale), _stream())
+    return out
+
+
+def temporal_attention(q, k, v, nclip, F, HW, heads, head_dim, out=None, scale=None):
+    """Frame-axis attention; rows (b*F + f)*HW + p.  q/k/v views share one row stride."""
+    for n, t in (("q", q), ("k", k), ("v", v)):
+        _dev(t, BF16, n)
+    if not (q.stride(0) == k.stride(0) == v.stride(0)):
+        raise _lib.VstError("temporal_attention: q/k/v must share a row stride")
+    if q.shape[0] != nclip * F * HW:
+        raise _lib.VstError("temporal_attention: rows != nclip*F*HW")
+    if out is None:
+        out = torch.empty((q.shape[0], heads * head_dim), dtype=BF16, device=q.device)
+    scale = head_dim ** -0.5 if scale is None else scale
+    _lib.call("vst_temporal_attention", _p(q), _p(k), _p(v), q.stride(0), _p(out), _ld(out), nclip, F, HW, heads,
+              head_dim, float(scale), _stream())
+    return out
+
+
+def group_norm(x1, nsamples, rows_per_sample, groups, eps, gamma, beta, *, silu=False, x2=None, out=None):
+    _dev(x1, BF16, "x1")
+    C = x1.shape[1] + (0 if x2 is None else x2.shape[1])
+    if x2 is not None:
+        _dev(x2, BF16, "x2")
+    if x1.shape[0] != nsamples * rows_per_sample:
+        raise _lib.VstError("group_norm: rows != nsamples*rows_per_sample")
+    if out is None:
+        out = torch.empty((x1.shape[0], C), dtype=BF16, device=x1.device)
+    ws_bytes = _lib.load().vst_groupnorm_workspace_bytes(nsamples, rows_per_sample, groups)
+    ws = torch.empty((ws_bytes + 3) // 4, dtype=F32, device=x1.device)
+    _lib.call("vst_groupnorm", _p(x1), _ld(x1), x1.shape[1], _p(x2), 0 if x2 is None else _ld(x2),
+              0 if x2 is None else x2.shape[1], nsamples, rows_per_sample, groups, float(eps), _p(gamma), _p(beta),
+              1 if silu else 0, _p(out), _ld(out), _p(ws), _stream())
+    return out
+
+
+def layer_norm(x, gamma, beta, eps=1e-5, *, pe=None, pe_div=1, pe_mod=1, out=None):
+    _dev(x, BF16, "x")
+    rows, C = x.shape
+    if out is None:
+        out = torch.empty((rows, C), dtype=BF16, device=x.device)
+    _lib.call("vst_layernorm", _p(x), _ld(x), C, rows, _p(gamma), _p(beta), float(eps), _p(pe), pe_div, pe_mod,
+              _p(out), _ld(out), _stream())
+    return out
+
+
+def timestep_embedding(t, n, dim, out, *, col0=0, per_row=1, step_idx=None, flip=True, shift=0.0):
+    """diffusers Timesteps(dim, flip_sin_to_cos, shift): value i -> out[i // per_row, col0 + (i % per_row)*dim]."""
+    if t.dtype != F32 or not t.is_cuda:
+        raise _lib.VstError("timestep_embedding: t must be fp32 on device")
+    _lib.call("vst_timestep_embedding", _p(t), _p(step_idx), n, dim, 1 if flip else 0, float(shift), _p(out),
+              _ld(out), col0, per_row, _stream())
+    return out
+
+
+def silu(x, out=None):
+    out = torch.empty_like(x) if out is None else out
+    _lib.call("vst_silu", _p(x), _p(out), x.numel(), _stream())
+    return out
+
+
+def add(a, b, out=None):
+    out = torch.empty_like(a) if out is None else out
+    _lib.call("vst_add", _p(a), _p(b), _p(out), a.numel(), _stream())
+    return out
+
+
+def copy2d(x, out):
+    _lib.call("vst_copy2d", _p(x), _ld(x), _p(out), _ld(out), x.shape[0], x.shape[1], _stream())
+    return out
+
+
+def pack_latents(lat, out, *, sigmas=None, step_idx=None, fixed_scale=1.0, ncopy=1):
+    B, Cl, F, H, W = lat.shape
+    if lat.dtype != F32 or not lat.is_contiguous():
+        raise _lib.VstError("pack_latents: latents must be contiguous fp32 (B,C,F,H,W)")
+    _lib.call("vst_pack_latents", _p(lat), B, Cl, F, H * W, _p(sigmas), _p(step_idx), float(fixed_scale), ncopy,
+              _p(out), _stream())
+    return out
+
+
+def euler_cfg_step(noise, lat, sigmas, step_idx, *, guidance=7.5, ncopy=2):
+    B, Cl, F, H, W = lat.shape
+    _lib.call("vst_euler_cfg_step", _p(noise), ncopy, float(guidance), _p(lat), B, Cl, F, H * W, _p(sigmas),
+              _p(step_idx), _stream())
+
+
+def step_advance(step_idx):
+    _lib.call("vst_step_advance", _p(step_idx), _stream())

@@ -1,0 +1,179 @@
+"""Parameter inventory (diffusers key names) and seeded synthetic weights.
+
+The state-dict layout is exactly what the reference's UNet carries after
+`load_unet_with_motion` (animatediff/utils.py:13-45) + `insert_unziplora_to_unet`
+(unziplora_unet/utils.py:388-484): diffusers UNetMotionModel names, plus for every spatial
+attention projection `...{to_q,to_k,to_v,to_out.0}.lora_layer.lora_matrix_dic.{content,style}_{down,up}.weight`
+and `...lora_layer.merge_{content,style}`.  No real checkpoints exist offline, so benchmarks and
+parity tests use seeded synthetic weights of this exact architecture.
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+
+import torch
+
+from .config import UNetMotionConfig
+
+
+def sinusoid_table(dim: int, max_len: int = 32) -> torch.Tensor:
+    """diffusers SinusoidalPositionalEmbedding table == reference PositionalEncoding
+    (animatediff/temporal_transformer.py:11-21).  Shape (1, max_len, dim)."""
+    position = torch.arange(max_len).unsqueeze(1)
+    div_term = torch.exp(torch.arange(0, dim, 2) * (-math.log(10000.0) / dim))
+    pe = torch.zeros(1, max_len, dim)
+    pe[0, :, 0::2] = torch.sin(position * div_term)
+    pe[0, :, 1::2] = torch.cos(position * div_term)
+    return pe
+
+
+def _linear(S, name, out_f, in_f, bias=True, kind="w"):
+    S[name + ".weight"] = ((out_f, in_f), kind)
+    if bias:
+        S[name + ".bias"] = ((out_f,), "b")
+
+
+def _norm(S, name, C):
+    S[name + ".weight"] = ((C,), "g")
+    S[name + ".bias"] = ((C,), "b")
+
+
+def _conv(S, name, cout, cin, k=3, kind="w"):
+    S[name + ".weight"] = ((cout, cin, k, k), kind)
+    S[name + ".bias"] = ((cout,), "b")
+
+
+def _lora(S, name, in_f, out_f, rank):
+    for key in ("content", "style"):
+        S[f"{name}.lora_layer.lora_matrix_dic.{key}_down.weight"] = ((rank, in_f), "lora")
+        S[f"{name}.lora_layer.lora_matrix_dic.{key}_up.weight"] = ((out_f, rank), "lora")
+        S[f"{name}.lora_layer.merge_{key}"] = ((out_f,), "merger")
+
+
+def _attention(S, name, q_dim, kv_dim, lora_rank=None):
+    _linear(S, name + ".to_q", q_dim, q_dim, bias=False)
+    _linear(S, name + ".to_k", q_dim, kv_dim, bias=False)
+    _linear(S, name + ".to_v", q_dim, kv_dim, bias=False)
+    _linear(S, name + ".to_out.0", q_dim, q_dim, bias=True, kind="wo")
+    if lora_rank:
+        _lora(S, name + ".to_q", q_dim, q_dim, lora_rank)
+        _lora(S, name + ".to_k", kv_dim, q_dim, lora_rank)
+        _lora(S, name + ".to_v", kv_dim, q_dim, lora_rank)
+        _lora(S, name + ".to_out.0", q_dim, q_dim, lora_rank)
+
+
+def _basic_block(S, name, C, cross_dim, lora_rank=None, temporal=False):
+    _norm(S, name + ".norm1", C)
+    _attention(S, name + ".attn1", C, C, lora_rank)
+    _norm(S, name + ".norm2", C)
+    _attention(S, name + ".attn2", C, C if temporal else cross_dim, lora_rank)
+    _norm(S, name + ".norm3", C)
+    _linear(S, name + ".ff.net.0.proj", 8 * C, C)
+    _linear(S, name + ".ff.net.2", C, 4 * C, kind="wo")
+    if temporal:
+        S[name + ".pos_embed.pe"] = ((1, 32, C), "pe")
+
+
+def _transformer2d(S, name, C, layers, cross_dim, lora_rank):
+    _norm(S, name + ".norm", C)
+    _linear(S, name + ".proj_in", C, C)
+    for i in range(layers):
+        _basic_block(S, f"{name}.transformer_blocks.{i}", C, cross_dim, lora_rank)
+    _linear(S, name + ".proj_out", C, C, kind="wo")
+
+
+def _motion(S, name, C):
+    _norm(S, name + ".norm", C)
+    _linear(S, name + ".proj_in", C, C)
+    _basic_block(S, name + ".transformer_blocks.0", C, None, None, temporal=True)
+    _linear(S, name + ".proj_out", C, C, kind="wo")
+
+
+def _resnet(S, name, cin, cout, temb):
+    _norm(S, name + ".norm1", cin)
+    _conv(S, name + ".conv1", cout, cin)
+    _linear(S, name + ".time_emb_proj", cout, temb)
+    _norm(S, name + ".norm2", cout)
+    _conv(S, name + ".conv2", cout, cout, kind="wo")
+    if cin != cout:
+        _conv(S, name + ".conv_shortcut", cout, cin, k=1)
+
+
+def param_shapes(cfg: UNetMotionConfig, lora_rank: int | None = 8) -> "OrderedDict[str, tuple]":
+    """name -> (shape, init kind) for every parameter/buffer of the LoRA-injected UNetMotionModel."""
+    S: "OrderedDict[str, tuple]" = OrderedDict()
+    ch = cfg.block_out_channels
+    T = cfg.time_embed_dim
+    _conv(S, "conv_in", ch[0], cfg.in_channels)
+    _linear(S, "time_embedding.linear_1", T, ch[0])
+    _linear(S, "time_embedding.linear_2", T, T)
+    _linear(S, "add_embedding.linear_1", T, cfg.projection_class_embeddings_input_dim)
+    _linear(S, "add_embedding.linear_2", T, T)
+    out_c = ch[0]
+    for i, bt in enumerate(cfg.down_block_types):
+        in_c, out_c = out_c, ch[i]
+        for j in range(cfg.layers_per_block):
+            _resnet(S, f"down_blocks.{i}.resnets.{j}", in_c if j == 0 else out_c, out_c, T)
+            if bt.startswith("CrossAttn"):
+                _transformer2d(S, f"down_blocks.{i}.attentions.{j}", out_c, cfg.transformer_layers_per_block[i],
+                               cfg.cross_attention_dim, lora_rank)
+            _motion(S, f"down_blocks.{i}.motion_modules.{j}", out_c)
+        if i < len(ch) - 1:
+            _conv(S, f"down_blocks.{i}.downsamplers.0.conv", out_c, out_c)
+    C = ch[-1]
+    _resnet(S, "mid_block.resnets.0", C, C, T)
+    _transformer2d(S, "mid_block.attentions.0", C, cfg.transformer_layers_per_block[-1], cfg.cross_attention_dim,
+                   lora_rank)
+    if cfg.use_motion_mid_block:
+        _motion(S, "mid_block.motion_modules.0", C)
+    _resnet(S, "mid_block.resnets.1", C, C, T)
+    rch = list(reversed(ch))
+    rtl = list(reversed(cfg.transformer_layers_per_block))
+    out_c = rch[0]
+    for i, bt in enumerate(cfg.up_block_types):
+        prev_c, out_c = out_c, rch[i]
+        in_c = rch[min(i + 1, len(ch) - 1)]
+        n = cfg.layers_per_block + 1
+        for j in range(n):
+            skip = in_c if j == n - 1 else out_c
+            rin = prev_c if j == 0 else out_c
+            _resnet(S, f"up_blocks.{i}.resnets.{j}", rin + skip, out_c, T)
+            if bt.startswith("CrossAttn"):
+                _transformer2d(S, f"up_blocks.{i}.attentions.{j}", out_c, rtl[i], cfg.cross_attention_dim, lora_rank)
+            _motion(S, f"up_blocks.{i}.motion_modules.{j}", out_c)
+        if i < len(ch) - 1:
+            _conv(S, f"up_blocks.{i}.upsamplers.0.conv", out_c, out_c)
+    _norm(S, "conv_norm_out", ch[0])
+    _conv(S, "conv_out", cfg.out_channels, ch[0], kind="wo")
+    return S
+
+
+def synthetic_state_dict(cfg: UNetMotionConfig, seed: int = 0, lora_rank: int | None = 8,
+                         dtype: torch.dtype = torch.float32) -> "OrderedDict[str, torch.Tensor]":
+    """Seeded synthetic weights: linear/conv ~ N(0,1)/sqrt(fan_in) (0.5x on the
+    residual-branch outputs), biases N(0, 0.02), norm gamma 1+N(0,0.05) / beta N(0,0.02),
+    UnZipLoRA A,B ~ N(0, 1/r) (unziplora_linear_layer.py:281-282), mergers ~ U(0,1).
+    Values are generated in fp32 on CPU, then rounded to `dtype` (bf16 for the device path; the
+    oracle consumes the same bf16-rounded values in fp32)."""
+    g = torch.Generator().manual_seed(seed)
+    out = OrderedDict()
+    for name, (shape, kind) in param_shapes(cfg, lora_rank).items():
+        if kind in ("w", "wo"):
+            fan_in = int(torch.tensor(shape[1:]).prod())
+            t = torch.randn(shape, generator=g) * ((0.5 if kind == "wo" else 1.0) / math.sqrt(fan_in))
+        elif kind == "b":
+            t = torch.randn(shape, generator=g) * 0.02
+        elif kind == "g":
+            t = 1.0 + torch.randn(shape, generator=g) * 0.05
+        elif kind == "lora":
+            r = shape[0] if "_down" in name else shape[1]
+            t = torch.randn(shape, generator=g) / r
+        elif kind == "merger":
+            t = torch.rand(shape, generator=g)
+        elif kind == "pe":
+            t = sinusoid_table(shape[-1], shape[1])
+        else:
+            raise ValueError(kind)
+        out[name] = t.to(dtype)
+    return out
