@@ -1,0 +1,143 @@
+"""CPU tests: C-ABI library loads and exports every declared symbol, architecture inventory,
+scheduler tables vs the oracle, host-side LoRA/temporal-LoRA bookkeeping."""
+import os
+import re
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_header_symbols():
+    from video_style_transfer_amd import _lib
+    lib = _lib.load()
+    hdr = open(os.path.join(ROOT, "include", "vst.h")).read()
+    declared = set(re.findall(r"\b(vst_[a-z0-9_]+)\s*\(", hdr))
+    assert declared, "no declarations parsed"
+    assert declared == set(_lib.SIGNATURES), declared ^ set(_lib.SIGNATURES)
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.vst_version().startswith(b"vst-hip")
+
+
+def test_calls_fail_loudly_on_cpu_tensors():
+    from video_style_transfer_amd import _lib, kernels as K
+    x = torch.zeros(4, 64, dtype=torch.bfloat16)
+    with pytest.raises(_lib.VstError):
+        K.linear(x, x)
+
+
+def test_bad_arguments_rejected_without_gpu():
+    from video_style_transfer_amd import _lib
+    lib = _lib.load()
+    # K not a multiple of 8 -> VST_ERR_ARG before any launch
+    assert lib.vst_gemm(1, 8, None, 0, 0, 1, 8, 4, 4, 6, None, None, 1, 0, None, 0, 1, 8, 0, None) == 1
+    assert lib.vst_temporal_attention(1, 1, 1, 8, 1, 8, 1, 64, 1, 8, 8, 1.0, None) == 1  # F > 32
+    assert lib.vst_spatial_attention(1, 64, 1, 1, 64, 1, 64, 1, 1, 8, 8, 1, 40, 1.0, None) == 1  # head_dim != 64
+
+
+@pytest.mark.parametrize("cfgname", ["tiny", "sdxl"])
+def test_param_inventory_matches_module_tree(cfgname):
+    from video_style_transfer_amd.config import UNetMotionConfig
+    from video_style_transfer_amd.unet_motion import UNetMotionModel
+    from video_style_transfer_amd.utils import attach_unziplora_layers
+    from video_style_transfer_amd.weights import param_shapes
+    cfg = getattr(UNetMotionConfig, cfgname)()
+    with torch.device("meta"):
+        unet = UNetMotionModel(cfg)
+        attach_unziplora_layers(unet, 8)
+    sd = unet.state_dict()
+    inv = param_shapes(cfg, 8)
+    assert set(sd) == set(inv), sorted(set(sd) ^ set(inv))[:10]
+    for k, (shape, _) in inv.items():
+        assert tuple(sd[k].shape) == tuple(shape), k
+    # SDXL topology facts from SURVEY.md §3.A: 70 spatial transformer blocks (140 attention
+    # modules, 560 LoRA-wrapped projections), 15 motion modules, 17 resnets
+    blocks = {k.split(".attn1.")[0] for k in sd if ".attn1.to_q.weight" in k and "motion" not in k}
+    motion = {k.split(".motion_modules.")[0] + k.split(".motion_modules.")[1][:2] for k in sd if ".motion_modules." in k}
+    resnets = {k.rsplit(".conv1.", 1)[0] for k in sd if k.endswith("conv1.weight")}
+    loras = [k for k in sd if k.endswith("lora_layer.merge_content")]
+    if cfgname == "sdxl":
+        assert len(blocks) == 70 and len(loras) == 560 and len(motion) == 15 and len(resnets) == 17
+
+
+def test_attn_processor_surface():
+    from video_style_transfer_amd.attention_processor import AnimateDiffAttnProcessor2_0, AttnProcessor2_0
+    from video_style_transfer_amd.config import UNetMotionConfig
+    from video_style_transfer_amd.unet_motion import UNetMotionModel
+    with torch.device("meta"):
+        unet = UNetMotionModel(UNetMotionConfig.tiny())
+    procs = unet.attn_processors
+    spatial = [k for k in procs if "motion_modules" not in k]
+    motion = [k for k in procs if "motion_modules" in k]
+    assert all(isinstance(procs[k], AnimateDiffAttnProcessor2_0) for k in spatial)
+    assert all(isinstance(procs[k], AttnProcessor2_0) for k in motion)
+    # the reference's processor swap (inference_animatediff.py:209-215) round-trips
+    new = {n: (p if "motion_modules" in n else AnimateDiffAttnProcessor2_0()) for n, p in procs.items()}
+    unet.set_attn_processor(new)
+    assert unet.attn_processors.keys() == procs.keys()
+
+
+def test_scheduler_matches_oracle():
+    from oracle.unet import euler_schedule
+    from video_style_transfer_amd.scheduler import EulerDiscreteScheduler
+    s = EulerDiscreteScheduler()
+    s.set_timesteps(50)
+    ts, sig, init = euler_schedule(50)
+    assert torch.equal(s.timesteps.float(), ts.float())
+    assert torch.allclose(s.sigmas, sig, rtol=1e-6, atol=1e-7)
+    assert abs(s.init_noise_sigma - init) < 1e-5
+    assert s.timesteps[0] == 981 and s.timesteps[-1] == 1
+
+
+def test_temporal_lora_bookkeeping_cpu():
+    from video_style_transfer_amd.config import UNetMotionConfig
+    from video_style_transfer_amd.temporal_lora import (TemporalLoRALinear, build_spatial_lora_index,
+                                                        get_merged_motion_state_dict, inject_temporal_lora)
+    from video_style_transfer_amd.unet_motion import UNetMotionModel
+    from video_style_transfer_amd.utils import attach_unziplora_layers, freeze_spatial_layers
+    unet = UNetMotionModel(UNetMotionConfig.tiny())
+    attach_unziplora_layers(unet, 8)
+    n = inject_temporal_lora(unet, rank=32, alpha=1.0)
+    assert n == 15 * 2 * 4  # 15 motion modules x (attn1, attn2) x (q, k, v, out)
+    assert inject_temporal_lora(unet) == 0  # idempotent
+    idx = build_spatial_lora_index(unet)
+    # motion module i of a cross-attn block pairs with attentions.i of the same block
+    assert idx and all(".motion_modules." in k for k in idx)
+    assert "down_blocks.1.motion_modules.0.transformer_blocks.0.attn1.to_q" in idx
+    freeze_spatial_layers(unet)
+    trainable = {n for n, p in unet.named_parameters() if p.requires_grad}
+    assert all("motion_modules" in n for n in trainable)
+    assert not any(".base." in n for n in trainable)
+    merged = get_merged_motion_state_dict(unet)
+    assert not any(".base." in k or "lora_A" in k for k in merged)
+    assert "down_blocks.0.motion_modules.0.transformer_blocks.0.attn1.to_q.weight" in merged
+    assert isinstance(unet.down_blocks[0].motion_modules[0].transformer_blocks[0].attn1.to_q, TemporalLoRALinear)
+
+
+def test_orth_loss_lowrank_matches_dense():
+    """compute_orth_loss evaluated low-rank equals the reference's dense formula."""
+    from oracle.ref_ops import orth_loss
+    from video_style_transfer_amd.config import UNetMotionConfig
+    from video_style_transfer_amd.temporal_lora import build_spatial_lora_index, compute_orth_loss, inject_temporal_lora
+    from video_style_transfer_amd.unet_motion import UNetMotionModel
+    from video_style_transfer_amd.utils import attach_unziplora_layers
+    torch.manual_seed(0)
+    unet = UNetMotionModel(UNetMotionConfig.tiny())
+    attach_unziplora_layers(unet, 8)
+    inject_temporal_lora(unet, rank=32, alpha=1.0)
+    for n, p in unet.named_parameters():
+        if "lora_B" in n:
+            p.data.normal_(0, 0.01)
+    idx = build_spatial_lora_index(unet)
+    got = compute_orth_loss(unet, idx, 0.1)
+    pairs = []
+    mods = dict(unet.named_modules())
+    for name, lora in idx.items():
+        m = mods[name]
+        d = lora.lora_matrix_dic
+        pairs.append((m.get_delta().detach(), d["content_down"].weight, d["content_up"].weight,
+                      d["style_down"].weight, d["style_up"].weight))
+    ref = orth_loss(pairs, 0.1)
+    assert torch.allclose(got.detach(), ref, rtol=1e-4), (got, ref)

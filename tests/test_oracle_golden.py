@@ -1,0 +1,132 @@
+"""Pin the oracle: oracle/ref_ops.py vs outputs of the REFERENCE's own modules (tests/golden).
+
+The fixtures were produced by tests/golden/make_golden.py importing /root/reference's torch-only
+modules.  Oracle and reference are both fp32 CPU, so the tolerance is fp32 reassociation only.
+"""
+import json
+import os
+import sys
+
+import pytest
+import torch
+from safetensors import safe_open
+from safetensors.torch import load_file
+
+from oracle import ref_ops as R
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+sys.path.insert(0, GOLD)
+import structured as S  # noqa: E402
+
+
+def load(name):
+    t = load_file(os.path.join(GOLD, name + ".safetensors"))
+    with safe_open(os.path.join(GOLD, name + ".safetensors"), "pt") as f:
+        meta = json.loads(f.metadata()["meta"])
+    return {k: v.float() for k, v in t.items()}, meta
+
+
+def close(a, b, tol=2e-5):
+    err = (a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-12)
+    assert err < tol, f"rel max err {err:.3e}"
+
+
+def test_unziplora_modes():
+    T, meta = load("unziplora")
+    for in_f, out_f, r in meta["cases"]:
+        t = f"i{in_f}_o{out_f}_r{r}."
+        args = [T[t + k] for k in ("A_c", "B_c", "m_c", "A_s", "B_s", "m_s")]
+        for mode in ("both", "content", "style"):
+            close(R.unziplora_delta(T[t + "x"], *args, forward_type=mode), T[t + f"out_{mode}"])
+        close(R.unziplora_delta(T[t + "x"], *args, "both", x_style=T[t + "xs"]), T[t + "out_both_xs"])
+        close(R.unziplora_delta(T[t + "x"], *args, "both", masked_s=True), T[t + "out_both_masked_style"])
+
+
+def test_lora_compatible_linear():
+    T, meta = load("lora_linear")
+    W = S.rebuild(S.load("W", T), meta["out"], meta["in"])
+    args = [T["lora." + k] for k in ("A_c", "B_c", "m_c", "A_s", "B_s", "m_s")]
+    for mode in ("both", "content", "style"):
+        d = R.unziplora_delta(T["x"], *args, forward_type=mode)
+        close(R.lora_compatible_linear(T["x"], W, T["b"], d, 1.0), T[f"out_{mode}_s1"])
+        close(R.lora_compatible_linear(T["x"], W, T["b"], d, 0.7), T[f"out_{mode}_s07"])
+    close(R.lora_compatible_linear(T["x"], W, T["b"]), T["out_nolora"])
+
+
+def _proj_fn(T, prefix, mode="both", scale=1.0, lora=True):
+    def proj(name, x):
+        key = "to_out.0" if name == "to_out" else name
+        W = T[f"{prefix}{key}.W.U"] @ T[f"{prefix}{key}.W.V"].t()
+        n = T[f"{prefix}{key}.W.d"].numel()
+        W[torch.arange(n), torch.arange(n)] += T[f"{prefix}{key}.W.d"]
+        b = T.get(f"{prefix}{key}.b")
+        d = None
+        if lora and f"{prefix}{key}.lora.A_c" in T:
+            args = [T[f"{prefix}{key}.lora.{k}"] for k in ("A_c", "B_c", "m_c", "A_s", "B_s", "m_s")]
+            d = R.unziplora_delta(x, *args, forward_type=mode)
+        return R.lora_compatible_linear(x, W, b, d, scale)
+    return proj
+
+
+def test_attention_processor_self_and_cross():
+    T, meta = load("processor")
+    for mode in ("both", "content", "style"):
+        out = R.attn_processor(T["self.x"], None, meta["self"]["heads"], _proj_fn(T, "self.", mode))
+        close(out, T[f"self.out_{mode}"])
+        out = R.attn_processor(T["self.x"], None, meta["self"]["heads"], _proj_fn(T, "self.", mode, 0.5))
+        close(out, T[f"self.out_{mode}_s05"])
+    out = R.attn_processor(T["cross.x"], T["cross.enc"], meta["cross"]["heads"], _proj_fn(T, "cross."))
+    close(out, T["cross.out_both"])
+    # bf16 autocast run of the reference: the fp32 oracle is within bf16 rounding of it
+    ref16 = T["self.out_both_autocast_bf16"]
+    out = R.attn_processor(T["self.x"], None, meta["self"]["heads"], _proj_fn(T, "self."))
+    err = (out - ref16).norm() / out.norm()
+    assert err < 2e-2, err
+
+
+def test_temporal_core():
+    T, meta = load("temporal_core")
+    for C, Fr, nseq in meta["cases"]:
+        tag = f"C{C}_F{Fr}."
+        out = R.attn_processor(T[tag + "x"], None, 8, _proj_fn(T, tag, lora=False))
+        close(out, T[tag + "out"])
+
+
+def test_positional_encoding_and_temporal_transformer():
+    T, meta = load("temporal_transformer")
+    close(R.positional_encoding(meta["C"], 32)[None], T["pe"], 1e-6)
+    close(R.positional_encoding(80, 32)[None], T["pe_d80"], 1e-6)
+    P = {}
+    for k in T:
+        if k.endswith(".d"):
+            base = k[:-2]
+            shp = {"attn.in_proj_weight": (3 * meta["C"], meta["C"]), "attn.out_proj.weight": (meta["C"], meta["C"]),
+                   "ffn.0.weight": (4 * meta["C"], meta["C"]), "ffn.3.weight": (meta["C"], 4 * meta["C"])}
+            of, inf = next(v for s, v in shp.items() if base.endswith(s))
+            P[base] = S.rebuild(S.load(base, T), of, inf)
+        elif not (k.endswith(".U") or k.endswith(".V")):
+            P[k] = T[k]
+    P["pos_encoding.pe"] = T["pe"]
+    out = R.temporal_transformer(T["x"], P, meta["layers"], meta["heads"])
+    close(out, T["out"], 5e-5)
+
+
+def test_temporal_lora_fwd_delta_orth():
+    T, meta = load("temporal_lora")
+    mod = meta["fwd_module"]
+    sd = {k[3:]: v for k, v in T.items() if k.startswith("sd.")}
+    W, b = sd[mod + ".base.weight"], sd[mod + ".base.bias"]
+    A, Bm = sd[mod + ".lora_A"], sd[mod + ".lora_B"]
+    close(R.temporal_lora_forward(T["x"], W, b, A, Bm, meta["alpha"], meta["rank"]), T["fwd"])
+    close(R.temporal_lora_delta(A, Bm, meta["alpha"], meta["rank"]), T["delta"])
+    close(W + R.temporal_lora_delta(A, Bm, meta["alpha"], meta["rank"]), T["merged"])
+    pairs = []
+    for tname in meta["index"]:
+        parts = tname.split(".")
+        mm = parts.index("motion_modules")
+        spatial = ".".join(parts[:mm]) + ".attentions." + parts[mm + 1] + "." + ".".join(parts[mm + 2:])
+        pre = spatial + ".lora_layer.lora_matrix_dic."
+        dt = R.temporal_lora_delta(sd[tname + ".lora_A"], sd[tname + ".lora_B"], meta["alpha"], meta["rank"])
+        pairs.append((dt, sd[pre + "content_down.weight"], sd[pre + "content_up.weight"],
+                      sd[pre + "style_down.weight"], sd[pre + "style_up.weight"]))
+    close(R.orth_loss(pairs, meta["lambda"]).reshape(1), T["orth_loss"], 1e-4)

@@ -1,0 +1,120 @@
+"""The denoise loop of `generate_video` (inference_animatediff.py:53-151), MI355X-native.
+
+Per step the reference does: scale_model_input -> unet(uncond) -> unet(cond) -> CFG combine ->
+Euler step (two B=1 UNet calls, :109-121).  Here one step is:
+  vst_pack_latents (scale_model_input, both CFG branches, NHWC bf16)
+  -> embed (timestep read from the device schedule table)
+  -> ONE UNet forward over the CFG-batched B=2 clip (results identical to two B=1 calls: no op mixes
+     batch elements)
+  -> vst_euler_cfg_step (CFG combine + Euler update of the fp32 latents)
+  -> vst_step_advance (device step counter).
+Because every per-step scalar lives in device tables indexed by the device counter, the whole step
+is captured once into a HIP graph and replayed for all 50 steps (no per-launch host overhead).
+Latents stay fp32 on the device (the reference keeps them in the UNet dtype between steps).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import kernels as K
+from .scheduler import EulerDiscreteScheduler
+from .unet_motion import UNetMotionModel
+
+BF16 = torch.bfloat16
+
+
+class AnimateDiffDenoiser:
+    def __init__(self, unet: UNetMotionModel, num_frames: int, height: int, width: int, *,
+                 num_inference_steps: int = 50, guidance_scale: float = 7.5, device=None,
+                 scheduler: Optional[EulerDiscreteScheduler] = None, use_graph: bool = True):
+        self.unet = unet
+        self.F = num_frames
+        self.h, self.w = height // 8, width // 8
+        self.height, self.width = height, width
+        self.guidance = guidance_scale
+        self.cfg = guidance_scale > 1.0
+        self.ncopy = 2 if self.cfg else 1
+        self.device = torch.device(device or "cuda")
+        self.scheduler = scheduler or EulerDiscreteScheduler()
+        self.scheduler.set_timesteps(num_inference_steps, device=self.device)
+        self.num_steps = num_inference_steps
+        self.use_graph = use_graph
+        cfg = unet.config
+        dev = self.device
+        self.lat = torch.zeros(1, cfg.in_channels, self.F, self.h, self.w, dtype=torch.float32, device=dev)
+        self.x = torch.empty(self.ncopy * self.F * self.h * self.w, cfg.in_channels, dtype=BF16, device=dev)
+        self.step_idx = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.timesteps = self.scheduler.timesteps.to(dev, torch.float32).contiguous()
+        self.sigmas = self.scheduler.sigmas.to(dev, torch.float32).contiguous()
+        self.enc = None
+        self.graph = None
+
+    def set_prompt_embeds(self, cond_embeds, cond_pooled, uncond_embeds=None, uncond_pooled=None):
+        """(1, L, D) text states and (1, P) pooled embeds per branch (encode_prompt output)."""
+        dev = self.device
+        if self.cfg:
+            enc = torch.cat([uncond_embeds, cond_embeds], 0)
+            pooled = torch.cat([uncond_pooled, cond_pooled], 0)
+        else:
+            enc, pooled = cond_embeds, cond_pooled
+        self.enc = enc.to(dev, BF16).contiguous()
+        self.pooled = pooled.to(dev, BF16).contiguous()
+        # SDXL time ids (inference_animatediff.py:81-85)
+        tid = torch.tensor([self.height, self.width, 0, 0, self.height, self.width], dtype=torch.float32)
+        self.time_ids = tid.unsqueeze(0).repeat(self.ncopy, 1).to(dev).contiguous()
+        self.graph = None
+
+    def _step(self):
+        B = self.ncopy
+        K.pack_latents(self.lat, self.x, sigmas=self.sigmas, step_idx=self.step_idx, ncopy=B)
+        emb = self.unet.embed(self.timesteps, self.pooled, self.time_ids, B, step_idx=self.step_idx)
+        noise = self.unet.forward_tokens(self.x, B, self.F, self.h, self.w, emb, self.enc)
+        K.euler_cfg_step(noise, self.lat, self.sigmas, self.step_idx, guidance=self.guidance, ncopy=B)
+        K.step_advance(self.step_idx)
+
+    def capture(self):
+        """Warm up (fills every derived-weight cache), then capture one step into a HIP graph."""
+        saved = self.lat.clone()
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            self.step_idx.zero_()
+            self._step()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._step()
+        self.graph = g
+        self.lat.copy_(saved)
+        self.step_idx.zero_()
+
+    def set_latents(self, latents):
+        self.lat.copy_(latents.to(self.device, torch.float32).reshape(self.lat.shape))
+        self.step_idx.zero_()
+
+    def init_latents(self, seed: int = 42):
+        """randn((1,4,F,h,w), generator=seed) * init_noise_sigma (inference_animatediff.py:88-95)."""
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        lat = torch.randn(self.lat.shape, generator=g) * self.scheduler.init_noise_sigma
+        self.set_latents(lat)
+        return lat
+
+    def run_steps(self, n: Optional[int] = None):
+        n = self.num_steps if n is None else n
+        if self.use_graph and self.graph is None:
+            self.capture()
+        for _ in range(n):
+            if self.graph is not None:
+                self.graph.replay()
+            else:
+                self._step()
+        return self.lat
+
+    def __call__(self, latents=None, seed: int = 42):
+        if latents is None:
+            self.init_latents(seed)
+        else:
+            self.set_latents(latents)
+        return self.run_steps()

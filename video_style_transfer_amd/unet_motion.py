@@ -1,0 +1,471 @@
+"""UNetMotionModel (SDXL + AnimateDiff motion modules), MI355X-native.
+
+Module tree and parameter names follow diffusers' UNetMotionModel, which the reference builds with
+`UNetMotionModel.from_unet2d` (animatediff/utils.py:13-45) and then patches with UnZipLoRA
+(unziplora_unet/utils.py:388-484) and AnimateDiffAttnProcessor2_0 (inference_animatediff.py:209-215).
+So `load_state_dict` of a reference/diffusers checkpoint (plus Stage-1 LoRA keys) drops in.
+
+Execution is MI355X-first: activations never leave the token-major NHWC layout
+[(b*F + f)*H*W + p, C] (bf16); every conv is an implicit GEMM, every projection a fused MFMA
+GEMM with bias / residual / GEGLU / temb epilogues, GroupNorm+SiLU and LayerNorm(+PE) are single
+passes, the skip concatenation of the up path is read from two sources instead of copied, and the
+motion modules read the frame axis in place (no permutes).  The public forward keeps the
+reference signature and 5-D (B, C, F, h, w) in/out.
+
+Block semantics (diffusers ~0.30, restated in oracle/unet.py with citations):
+  ResnetBlock2D:        GN+SiLU -> conv3x3 (+ time_emb_proj(SiLU(emb))) -> GN+SiLU -> conv3x3 (+ shortcut)
+  Transformer2DModel:   GN(eps 1e-6) -> proj_in -> BasicTransformerBlock* -> proj_out -> + residual
+  BasicTransformerBlock: LN -> attn1 -> +res ; LN -> attn2(text) -> +res ; LN -> GEGLU FF -> +res
+  motion module:        GN over (C-group, F, H, W) -> proj_in -> block(self, self, PE before each attn)
+                        -> proj_out -> + residual
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+from torch import nn
+
+from . import kernels as K
+from .attention_processor import Attention
+from .config import UNetMotionConfig
+from .lora_linear import LoRACompatibleLinear, build_ops, run_ops
+from .weights import sinusoid_table
+
+BF16 = torch.bfloat16
+
+
+class _F32Cache:
+    """fp32 device copies of bf16 params (norm affine, conv/linear bias) keyed by tensor version."""
+
+    @staticmethod
+    def get(p: torch.Tensor) -> torch.Tensor:
+        key = (p.data_ptr(), p._version)
+        c = p.__dict__.get("_vst_f32")
+        if c is None or c[0] != key:
+            c = (key, p.detach().float().contiguous())
+            p.__dict__["_vst_f32"] = c
+        return c[1]
+
+
+f32 = _F32Cache.get
+
+
+class GroupNorm(nn.GroupNorm):
+    def run(self, x1, nsamples, rows_per_sample, *, silu=False, x2=None, out=None):
+        return K.group_norm(x1, nsamples, rows_per_sample, self.num_groups, self.eps, f32(self.weight), f32(self.bias),
+                            silu=silu, x2=x2, out=out)
+
+
+class LayerNorm(nn.LayerNorm):
+    def run(self, x, *, pe=None, pe_div=1, pe_mod=1, out=None):
+        return K.layer_norm(x, f32(self.weight), f32(self.bias), self.eps, pe=pe, pe_div=pe_div, pe_mod=pe_mod,
+                            out=out)
+
+
+class Conv3x3(nn.Conv2d):
+    """nn.Conv2d(k=3, pad=1) whose device weight is re-laid out once to [Cout, (ky,kx,ci)]."""
+
+    def __init__(self, cin, cout, stride=1):
+        super().__init__(cin, cout, 3, stride=stride, padding=1)
+
+    def kernel_weight(self):
+        key = (self.weight.data_ptr(), self.weight._version)
+        c = self.__dict__.get("_vst_w")
+        if c is None or c[0] != key:
+            co, ci = self.weight.shape[:2]
+            w = self.weight.detach().permute(0, 2, 3, 1).reshape(co, 9 * ci)
+            kp = (9 * ci + 7) & ~7
+            if kp != 9 * ci:
+                w = torch.cat([w, w.new_zeros(co, kp - 9 * ci)], 1)
+            c = (key, w.to(BF16).contiguous())
+            self.__dict__["_vst_w"] = c
+        return c[1]
+
+    def run(self, x1, nimg, H, W, *, x2=None, upsample=False, row_bias=None, row_bias_div=1, residual=None):
+        return K.conv3x3(x1, nimg, H, W, self.kernel_weight(), f32(self.bias), x2=x2, stride=self.stride[0],
+                         upsample=upsample, row_bias=row_bias, row_bias_div=row_bias_div, residual=residual)
+
+
+class Conv1x1(nn.Conv2d):
+    def __init__(self, cin, cout):
+        super().__init__(cin, cout, 1)
+
+    def kernel_weight(self):
+        key = (self.weight.data_ptr(), self.weight._version)
+        c = self.__dict__.get("_vst_w")
+        if c is None or c[0] != key:
+            c = (key, self.weight.detach().reshape(self.weight.shape[0], -1).to(BF16).contiguous())
+            self.__dict__["_vst_w"] = c
+        return c[1]
+
+    def run(self, x1, x2=None):
+        return K.linear(x1, self.kernel_weight(), f32(self.bias), x2=x2)
+
+
+class Linear(LoRACompatibleLinear):
+    """Plain projection (proj_in/out, FF, embeddings) — LoRACompatibleLinear without a lora layer."""
+
+    def run(self, x, *, residual=None, out=None):
+        return run_ops(x, build_ops([self], 1.0), residual=residual, out=out)
+
+
+@dataclass
+class FwdCtx:
+    B: int                 # clips in the batch (CFG-batched: 2x)
+    F: int                 # frames per clip
+    emb_silu: torch.Tensor  # [B, T] bf16, SiLU(time + add embedding)
+    enc: Optional[torch.Tensor]  # [B, L, D] bf16 text states
+    cross_kwargs: dict
+
+
+# --------------------------------------------------------------------------------------- blocks
+class GEGLU(nn.Module):
+    def __init__(self, dim_in, dim_out):
+        super().__init__()
+        self.proj = Linear(dim_in, dim_out * 2)
+
+    def geglu_ops(self):
+        """proj weight with hidden/gate rows interleaved per 64-output block (GEMM GEGLU epilogue)."""
+        w, b = self.proj.weight, self.proj.bias
+        key = (w.data_ptr(), w._version, b.data_ptr(), b._version)
+        c = self.__dict__.get("_vst_geglu")
+        if c is None or c[0] != key:
+            inner = w.shape[0] // 2
+            idx = torch.arange(inner, device=w.device).view(-1, 64)
+            idx = torch.cat([idx, idx + inner], 1).reshape(-1)
+            c = (key, (w.detach()[idx].to(BF16).contiguous(), b.detach()[idx].float().contiguous()))
+            self.__dict__["_vst_geglu"] = c
+        return c[1]
+
+
+class FeedForward(nn.Module):
+    """diffusers FeedForward(activation_fn="geglu"): net = [GEGLU, Dropout, Linear]."""
+
+    def __init__(self, dim, mult=4):
+        super().__init__()
+        inner = dim * mult
+        self.net = nn.ModuleList([GEGLU(dim, inner), nn.Dropout(0.0), Linear(inner, dim)])
+
+    def run(self, x, residual):
+        w, b = self.net[0].geglu_ops()
+        h = K.linear(x, w, b, geglu=True)
+        return self.net[2].run(h, residual=residual)
+
+
+class BasicTransformerBlock(nn.Module):
+    """unziplora_unet/unzip_attention.py:13-239 / diffusers BasicTransformerBlock (norm_type layer_norm)."""
+
+    def __init__(self, dim, heads, head_dim, cross_attention_dim=None, temporal=False, max_seq_length=32):
+        super().__init__()
+        self.temporal = temporal
+        self.norm1 = LayerNorm(dim)
+        self.attn1 = Attention(dim, None, heads, head_dim, temporal=temporal)
+        self.norm2 = LayerNorm(dim)
+        self.attn2 = Attention(dim, None if temporal else cross_attention_dim, heads, head_dim, temporal=temporal)
+        self.norm3 = LayerNorm(dim)
+        self.ff = FeedForward(dim)
+        if temporal:
+            self.pos_embed = _SinusoidalPE(dim, max_seq_length)
+
+    def run(self, x, nimg, N, ctx: FwdCtx):
+        """x: [nimg*N, C] -> same."""
+        C = x.shape[1]
+        if self.temporal:
+            pe = f32(self.pos_embed.pe).view(-1, C)
+            kw = dict(pe=pe, pe_div=N, pe_mod=ctx.F)
+            n = self.norm1.run(x, **kw)
+            x = self.attn1(n.view(nimg, N, C), num_frames=ctx.F, _vst_residual=x).view(-1, C)
+            n = self.norm2.run(x, **kw)
+            x = self.attn2(n.view(nimg, N, C), num_frames=ctx.F, _vst_residual=x).view(-1, C)
+        else:
+            n = self.norm1.run(x)
+            x = self.attn1(n.view(nimg, N, C), _vst_residual=x, **ctx.cross_kwargs).view(-1, C)
+            n = self.norm2.run(x)
+            x = self.attn2(n.view(nimg, N, C), encoder_hidden_states=ctx.enc, _vst_residual=x,
+                           **ctx.cross_kwargs).view(-1, C)
+        n = self.norm3.run(x)
+        return self.ff.run(n, residual=x)
+
+
+class _SinusoidalPE(nn.Module):
+    def __init__(self, dim, max_len=32):
+        super().__init__()
+        self.register_buffer("pe", sinusoid_table(dim, max_len))
+
+
+class Transformer2DModel(nn.Module):
+    """unziplora_unet/transformer_2d.py:137-352 (continuous input, use_linear_projection=True)."""
+
+    def __init__(self, heads, head_dim, C, layers, cross_attention_dim, groups=32):
+        super().__init__()
+        self.norm = GroupNorm(groups, C, eps=1e-6)
+        self.proj_in = Linear(C, C)
+        self.transformer_blocks = nn.ModuleList(
+            [BasicTransformerBlock(C, heads, head_dim, cross_attention_dim) for _ in range(layers)])
+        self.proj_out = Linear(C, C)
+
+    def run(self, x, nimg, H, W, ctx):
+        h = self.norm.run(x, nimg, H * W)
+        h = self.proj_in.run(h)
+        for blk in self.transformer_blocks:
+            h = blk.run(h, nimg, H * W, ctx)
+        return self.proj_out.run(h, residual=x)
+
+
+class MotionModule(nn.Module):
+    """diffusers AnimateDiffTransformer3D (motion module built by UNetMotionModel.from_unet2d)."""
+
+    def __init__(self, C, heads=8, groups=32, max_seq_length=32):
+        super().__init__()
+        self.norm = GroupNorm(groups, C, eps=1e-6)
+        self.proj_in = Linear(C, C)
+        self.transformer_blocks = nn.ModuleList(
+            [BasicTransformerBlock(C, heads, C // heads, None, temporal=True, max_seq_length=max_seq_length)])
+        self.proj_out = Linear(C, C)
+
+    def run(self, x, nimg, H, W, ctx):
+        HW = H * W
+        h = self.norm.run(x, nimg // ctx.F, ctx.F * HW)  # statistics over every frame of a clip
+        h = self.proj_in.run(h)
+        for blk in self.transformer_blocks:
+            h = blk.run(h, nimg, HW, ctx)
+        return self.proj_out.run(h, residual=x)
+
+
+class ResnetBlock2D(nn.Module):
+    def __init__(self, cin, cout, temb, groups=32, eps=1e-5):
+        super().__init__()
+        self.in_channels, self.out_channels = cin, cout
+        self.norm1 = GroupNorm(groups, cin, eps=eps)
+        self.conv1 = Conv3x3(cin, cout)
+        self.time_emb_proj = Linear(temb, cout)
+        self.norm2 = GroupNorm(groups, cout, eps=eps)
+        self.dropout = nn.Dropout(0.0)
+        self.conv2 = Conv3x3(cout, cout)
+        self.conv_shortcut = Conv1x1(cin, cout) if cin != cout else None
+
+    def run(self, x1, nimg, H, W, ctx, x2=None):
+        HW = H * W
+        h = self.norm1.run(x1, nimg, HW, silu=True, x2=x2)
+        temb = self.time_emb_proj.run(ctx.emb_silu).float()  # [B, cout]; bf16-rounded like the reference
+        h = self.conv1.run(h, nimg, H, W, row_bias=temb, row_bias_div=ctx.F * HW)
+        h = self.norm2.run(h, nimg, HW, silu=True)
+        sc = self.conv_shortcut.run(x1, x2) if self.conv_shortcut is not None else x1
+        return self.conv2.run(h, nimg, H, W, residual=sc)
+
+
+class Downsample2D(nn.Module):
+    def __init__(self, C):
+        super().__init__()
+        self.conv = Conv3x3(C, C, stride=2)
+
+    def run(self, x, nimg, H, W):
+        return self.conv.run(x, nimg, H, W), (H + 1) // 2, (W + 1) // 2
+
+
+class Upsample2D(nn.Module):
+    def __init__(self, C):
+        super().__init__()
+        self.conv = Conv3x3(C, C)
+
+    def run(self, x, nimg, H, W):
+        return self.conv.run(x, nimg, H, W, upsample=True), 2 * H, 2 * W
+
+
+class DownBlock(nn.Module):
+    """DownBlockMotion / CrossAttnDownBlockMotion."""
+
+    def __init__(self, cin, cout, temb, layers, cross, t_layers, heads, cross_dim, add_down, motion_heads):
+        super().__init__()
+        self.resnets = nn.ModuleList([ResnetBlock2D(cin if j == 0 else cout, cout, temb) for j in range(layers)])
+        self.attentions = nn.ModuleList(
+            [Transformer2DModel(heads, cout // heads, cout, t_layers, cross_dim) for _ in range(layers)]) if cross else None
+        self.motion_modules = nn.ModuleList([MotionModule(cout, motion_heads) for _ in range(layers)])
+        self.downsamplers = nn.ModuleList([Downsample2D(cout)]) if add_down else None
+
+    def run(self, x, nimg, H, W, ctx):
+        outs = []
+        for j, res in enumerate(self.resnets):
+            x = res.run(x, nimg, H, W, ctx)
+            if self.attentions is not None:
+                x = self.attentions[j].run(x, nimg, H, W, ctx)
+            x = self.motion_modules[j].run(x, nimg, H, W, ctx)
+            outs.append((x, H, W))
+        if self.downsamplers is not None:
+            x, H, W = self.downsamplers[0].run(x, nimg, H, W)
+            outs.append((x, H, W))
+        return x, H, W, outs
+
+
+class UpBlock(nn.Module):
+    """UpBlockMotion / CrossAttnUpBlockMotion."""
+
+    def __init__(self, prev_c, cout, skip_in, temb, layers, cross, t_layers, heads, cross_dim, add_up, motion_heads):
+        super().__init__()
+        n = layers + 1
+        self.resnets = nn.ModuleList([
+            ResnetBlock2D((prev_c if j == 0 else cout) + (skip_in if j == n - 1 else cout), cout, temb)
+            for j in range(n)])
+        self.attentions = nn.ModuleList(
+            [Transformer2DModel(heads, cout // heads, cout, t_layers, cross_dim) for _ in range(n)]) if cross else None
+        self.motion_modules = nn.ModuleList([MotionModule(cout, motion_heads) for _ in range(n)])
+        self.upsamplers = nn.ModuleList([Upsample2D(cout)]) if add_up else None
+
+    def run(self, x, nimg, H, W, ctx, skips):
+        for j, res in enumerate(self.resnets):
+            s, sh, sw = skips.pop()
+            assert (sh, sw) == (H, W)
+            x = res.run(x, nimg, H, W, ctx, x2=s)  # channel concat [x, skip] read from two sources
+            if self.attentions is not None:
+                x = self.attentions[j].run(x, nimg, H, W, ctx)
+            x = self.motion_modules[j].run(x, nimg, H, W, ctx)
+        if self.upsamplers is not None:
+            x, H, W = self.upsamplers[0].run(x, nimg, H, W)
+        return x, H, W
+
+
+class MidBlock(nn.Module):
+    """UNetMidBlockCrossAttnMotion (no motion module for the SDXL-beta adapter)."""
+
+    def __init__(self, C, temb, t_layers, heads, cross_dim, motion, motion_heads):
+        super().__init__()
+        self.resnets = nn.ModuleList([ResnetBlock2D(C, C, temb), ResnetBlock2D(C, C, temb)])
+        self.attentions = nn.ModuleList([Transformer2DModel(heads, C // heads, C, t_layers, cross_dim)])
+        self.motion_modules = nn.ModuleList([MotionModule(C, motion_heads)]) if motion else None
+
+    def run(self, x, nimg, H, W, ctx):
+        x = self.resnets[0].run(x, nimg, H, W, ctx)
+        x = self.attentions[0].run(x, nimg, H, W, ctx)
+        if self.motion_modules is not None:
+            x = self.motion_modules[0].run(x, nimg, H, W, ctx)
+        return self.resnets[1].run(x, nimg, H, W, ctx)
+
+
+class TimestepEmbedding(nn.Module):
+    def __init__(self, cin, T):
+        super().__init__()
+        self.linear_1 = Linear(cin, T)
+        self.linear_2 = Linear(T, T)
+
+    def run(self, x, residual=None):
+        h = self.linear_1.run(x)
+        h = K.silu(h)
+        return self.linear_2.run(h, residual=residual)
+
+
+@dataclass
+class UNetMotionOutput:
+    sample: torch.Tensor
+
+
+class UNetMotionModel(nn.Module):
+    def __init__(self, config: Optional[UNetMotionConfig] = None):
+        super().__init__()
+        cfg = config or UNetMotionConfig.sdxl()
+        self.config = cfg
+        ch = cfg.block_out_channels
+        T = cfg.time_embed_dim
+        self.conv_in = Conv3x3(cfg.in_channels, ch[0])
+        self.time_embedding = TimestepEmbedding(ch[0], T)
+        self.add_embedding = TimestepEmbedding(cfg.projection_class_embeddings_input_dim, T)
+        self.down_blocks = nn.ModuleList()
+        out_c = ch[0]
+        for i, bt in enumerate(cfg.down_block_types):
+            in_c, out_c = out_c, ch[i]
+            self.down_blocks.append(DownBlock(in_c, out_c, T, cfg.layers_per_block, bt.startswith("CrossAttn"),
+                                              cfg.transformer_layers_per_block[i], cfg.num_attention_heads[i],
+                                              cfg.cross_attention_dim, i < len(ch) - 1, cfg.motion_num_attention_heads))
+        self.mid_block = MidBlock(ch[-1], T, cfg.transformer_layers_per_block[-1], cfg.num_attention_heads[-1],
+                                  cfg.cross_attention_dim, cfg.use_motion_mid_block, cfg.motion_num_attention_heads)
+        rch = list(reversed(ch))
+        rtl = list(reversed(cfg.transformer_layers_per_block))
+        rheads = list(reversed(cfg.num_attention_heads))
+        self.up_blocks = nn.ModuleList()
+        out_c = rch[0]
+        for i, bt in enumerate(cfg.up_block_types):
+            prev_c, out_c = out_c, rch[i]
+            skip_in = rch[min(i + 1, len(ch) - 1)]
+            self.up_blocks.append(UpBlock(prev_c, out_c, skip_in, T, cfg.layers_per_block, bt.startswith("CrossAttn"),
+                                          rtl[i], rheads[i], cfg.cross_attention_dim, i < len(ch) - 1,
+                                          cfg.motion_num_attention_heads))
+        self.conv_norm_out = GroupNorm(cfg.norm_num_groups, ch[0], eps=cfg.norm_eps)
+        self.conv_out = Conv3x3(ch[0], cfg.out_channels)
+
+    # ---- diffusers surface ----------------------------------------------------------------
+    @property
+    def dtype(self):
+        return self.conv_in.weight.dtype
+
+    @property
+    def attn_processors(self):
+        return {f"{n}.processor": m.processor for n, m in self.named_modules() if isinstance(m, Attention)}
+
+    def set_attn_processor(self, processor):
+        mods = {f"{n}.processor": m for n, m in self.named_modules() if isinstance(m, Attention)}
+        if isinstance(processor, dict):
+            if set(processor) != set(mods):
+                raise ValueError("processor dict keys must match attn_processors")
+            for k, p in processor.items():
+                mods[k].set_processor(p)
+        else:
+            for m in mods.values():
+                m.set_processor(processor)
+
+    # ---- embeddings -----------------------------------------------------------------------
+    def embed(self, timestep, text_embeds, time_ids, B, step_idx=None, out=None):
+        """SiLU(time_embedding(Timesteps(t)) + add_embedding([text_embeds, Timesteps(time_ids)])) -> [B, T].
+        `timestep`: fp32 device tensor [B] (or a schedule table with step_idx)."""
+        cfg = self.config
+        ch0 = cfg.block_out_channels[0]
+        dev = text_embeds.device
+        t_in = torch.empty(B, ch0, dtype=BF16, device=dev)
+        K.timestep_embedding(timestep, B, ch0, t_in, step_idx=step_idx)
+        add_in = torch.empty(B, cfg.projection_class_embeddings_input_dim, dtype=BF16, device=dev)
+        K.copy2d(text_embeds, add_in[:, : cfg.text_embed_dim])
+        tid = time_ids.float().reshape(-1).contiguous()
+        K.timestep_embedding(tid, B * cfg.num_time_ids, cfg.addition_time_embed_dim, add_in,
+                             col0=cfg.text_embed_dim, per_row=cfg.num_time_ids)
+        temb = self.time_embedding.run(t_in)
+        emb = self.add_embedding.run(add_in, residual=temb)  # emb = temb + aug_emb
+        return K.silu(emb, out=out)
+
+    # ---- core (NHWC tokens) -----------------------------------------------------------------
+    def forward_tokens(self, x, B, F, h, w, emb_silu, enc, cross_kwargs=None):
+        """x: [B*F*h*w, in_channels] bf16 -> noise prediction [B*F*h*w, out_channels] bf16."""
+        ctx = FwdCtx(B, F, emb_silu, enc, cross_kwargs or {})
+        nimg = B * F
+        H, W = h, w
+        x = self.conv_in.run(x, nimg, H, W)
+        skips = [(x, H, W)]
+        for blk in self.down_blocks:
+            x, H, W, outs = blk.run(x, nimg, H, W, ctx)
+            skips.extend(outs)
+        x = self.mid_block.run(x, nimg, H, W, ctx)
+        for blk in self.up_blocks:
+            x, H, W = blk.run(x, nimg, H, W, ctx, skips)
+        x = self.conv_norm_out.run(x, nimg, H * W, silu=True)
+        return self.conv_out.run(x, nimg, H, W)
+
+    def forward(self, sample, timestep, encoder_hidden_states, timestep_cond=None, attention_mask=None,
+                cross_attention_kwargs=None, added_cond_kwargs=None, return_dict=True, **kwargs):
+        """diffusers UNetMotionModel.forward signature (inference_animatediff.py:110-121)."""
+        if not sample.is_cuda:
+            raise K._lib.VstError("UNetMotionModel: sample is on CPU; the HIP path has no CPU fallback")
+        B, Cin, F, h, w = sample.shape
+        dev = sample.device
+        t = timestep if torch.is_tensor(timestep) else torch.tensor([timestep])
+        t = t.to(device=dev, dtype=torch.float32).reshape(-1)
+        if t.numel() == 1:
+            t = t.expand(B)
+        t = t.contiguous()
+        text_embeds = added_cond_kwargs["text_embeds"].to(dev, BF16).reshape(B, -1).contiguous()
+        time_ids = added_cond_kwargs["time_ids"].to(dev).reshape(B, -1)
+        emb_silu = self.embed(t, text_embeds, time_ids, B)
+        enc = encoder_hidden_states.to(dev, BF16).contiguous()
+        x = torch.empty(B * F * h * w, Cin, dtype=BF16, device=dev)
+        K.pack_latents(sample.float().contiguous(), x)
+        y = self.forward_tokens(x, B, F, h, w, emb_silu, enc, cross_attention_kwargs)
+        out = y.view(B, F, h, w, -1).permute(0, 4, 1, 2, 3).contiguous().to(sample.dtype)
+        return UNetMotionOutput(out) if return_dict else (out,)
