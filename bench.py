@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""Denoised frames/s of the AnimateDiff-XL (+UnZipLoRA r=8) 50-step CFG denoise loop on MI355X.
+
+Metric (BASELINE.json): denoised frames/sec, 16x512x512 clip, 50-step AnimateDiff-XL.
+A "step" = one denoise step of the loop (inference_animatediff.py:105-131): scale_model_input ->
+UNet forward of the CFG pair (batched, B=2) -> CFG combine -> Euler update; captured once as a HIP
+graph and replayed.  value = frames / (50 steps x mean step time) — the rate at which whole clips
+are produced; weights are seeded synthetic SDXL + AnimateDiff-SDXL motion + UnZipLoRA r=8 (no
+checkpoints offline), text embeddings synthetic N(0,1).
+
+  python bench.py [--gpus N --steps K --warmup W] [--frames 16 --size 512 --lora-rank 8 --lora-mode fused]
+N>1 (torch.distributed.run, one rank per GPU): see --parallel.  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table; no sparsity)
+PEAK_HBM_GBS = 8000.0
+
+KERNEL_OF_KIND = {
+    "gemm": "gemm_kernel<0,0> (dense projection)",
+    "gemm_lora": "gemm_kernel<0,0> (dense projection)",
+    "gemm_lora_down": "gemm_kernel<0,0> (dense projection)",
+    "gemm_geglu": "gemm_kernel<0,1> (GEGLU FF)",
+    "conv3x3": "gemm_kernel<1,0> (implicit-GEMM conv3x3)",
+    "conv3x3_small_cin": "gemm_kernel<2,0> (conv_in)",
+    "spatial_attention": "spatial_attn_kernel",
+    "temporal_attention": "temporal_attn_kernel",
+    "groupnorm": "gn_stats/gn_finalize/gn_apply",
+    "layernorm": "layernorm_kernel",
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=16)
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--lora-rank", type=int, default=8)
+    ap.add_argument("--lora-mode", default="fused", choices=["fused", "folded"])
+    ap.add_argument("--num-inference-steps", type=int, default=50)
+    ap.add_argument("--guidance", type=float, default=7.5)
+    ap.add_argument("--parallel", default="replicas", choices=["replicas"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--cpu-sample-frames", type=int, default=2)
+    ap.add_argument("--seed", type=int, default=0)
+    return ap.parse_args()
+
+
+def roofline(den):
+    """One instrumented eager step: HIP events around every launch on its stream."""
+    from video_style_transfer_amd import kernels as K
+    den.step_idx.zero_()
+    torch.cuda.synchronize()
+    K.profile_launches(True)
+    den._step()
+    rec = K.collect_launches()
+    K.profile_launches(False)
+    den.step_idx.zero_()
+    by = {}
+    for kind, fl, nb, ms in rec:
+        sym = KERNEL_OF_KIND.get(kind, kind)
+        d = by.setdefault(sym, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
+        d["launches"] += 1
+        d["ms"] += ms
+        d["flops"] += fl
+        d["bytes"] += nb
+    total_ms = sum(d["ms"] for d in by.values())
+    dom_sym, dom = max(by.items(), key=lambda kv: kv[1]["ms"])
+    mfma = dom["flops"] > 0
+    if mfma:
+        achieved = dom["flops"] / (dom["ms"] * 1e-3) / 1e12
+        peak, unit = PEAK_BF16_TFLOPS, "TFLOP/s"
+    else:
+        achieved = dom["bytes"] / (dom["ms"] * 1e-3) / 1e9
+        peak, unit = PEAK_HBM_GBS, "GB/s"
+    table = {}
+    for sym, d in sorted(by.items(), key=lambda kv: -kv[1]["ms"]):
+        table[sym] = {"launches": d["launches"], "ms_per_step": round(d["ms"], 3),
+                      "share": round(d["ms"] / total_ms, 4),
+                      "tflops": round(d["flops"] / (d["ms"] * 1e-3) / 1e12, 1) if d["flops"] else None,
+                      "gbs": round(d["bytes"] / (d["ms"] * 1e-3) / 1e9, 1)}
+    return {
+        "bound": "mfma" if mfma else "hbm", "kernel": dom_sym, "achieved": round(achieved, 1), "peak": peak,
+        "unit": unit, "frac": round(achieved / peak, 4), "traffic": None,
+        "avg_launch_ms": round(dom["ms"] / dom["launches"], 4),
+        "flops_per_launch": dom["flops"] / dom["launches"],
+        "kernel_time_ms_per_step": round(total_ms, 3),
+    }, table
+
+
+def cpu_baseline(args, cfg):
+    """Oracle (fp32 CPU restatement) timed on a bounded sample: one UNet forward (one CFG branch)
+    of a `cpu_sample_frames`-frame clip at the bench resolution; extrapolated to frames/s of the
+    50-step CFG loop = frames / (2 * steps * t_forward)."""
+    from oracle.unet import unet_forward
+    from video_style_transfer_amd.weights import synthetic_state_dict
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    sd = synthetic_state_dict(cfg, args.seed, args.lora_rank or None)
+    fr, h = args.cpu_sample_frames, args.size // 8
+    g = torch.Generator().manual_seed(1)
+    lat = torch.randn(1, 4, fr, h, h, generator=g)
+    enc = torch.randn(1, 77, cfg.cross_attention_dim, generator=g)
+    pooled = torch.randn(1, cfg.text_embed_dim, generator=g)
+    tids = torch.tensor([[args.size, args.size, 0, 0, args.size, args.size]], dtype=torch.float32)
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        unet_forward(sd, cfg.to_dict(), lat, torch.tensor([981.0]), enc, pooled, tids)
+        dt = time.perf_counter() - t0
+    del sd
+    fps = fr / (2 * args.num_inference_steps * dt)
+    return {"value": fps, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"1 UNet forward (one CFG branch) of a {fr}-frame {args.size}x{args.size} clip, fp32, "
+                      f"{dt:.2f}s, extrapolated x{2 * args.num_inference_steps} forwards"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from video_style_transfer_amd.config import UNetMotionConfig
+    from video_style_transfer_amd.lora_linear import set_lora_mode
+    from video_style_transfer_amd.pipeline import AnimateDiffDenoiser
+    from video_style_transfer_amd.utils import build_unet
+
+    cfg = UNetMotionConfig.sdxl()
+    set_lora_mode(args.lora_mode)
+    t_build = time.perf_counter()
+    unet = build_unet(cfg, seed=args.seed, lora_rank=args.lora_rank or None, device=dev)
+    den = AnimateDiffDenoiser(unet, args.frames, args.size, args.size, num_inference_steps=args.num_inference_steps,
+                              guidance_scale=args.guidance, device=dev)
+    g = torch.Generator().manual_seed(7 + rank)
+    enc = torch.randn(2, 77, cfg.cross_attention_dim, generator=g)
+    pooled = torch.randn(2, cfg.text_embed_dim, generator=g)
+    den.set_prompt_embeds(enc[1:], pooled[1:], enc[:1], pooled[:1])
+    den.init_latents(seed=42 + rank)
+    den.capture()
+    t_build = time.perf_counter() - t_build
+    for _ in range(args.warmup):
+        den.graph.replay()
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        den.graph.replay()
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        tt = torch.tensor([dt], device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    ms_step = dt / args.steps * 1e3
+    frames_total = args.frames * world  # replicas: every rank denoises its own clip
+    value = frames_total / (args.num_inference_steps * ms_step * 1e-3)
+    ok = bool(torch.isfinite(den.lat).all().item())
+
+    rl, table = (None, None) if args.no_roofline else roofline(den)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        del den, unet
+        torch.cuda.empty_cache()
+        cpu = cpu_baseline(args, cfg)
+    if rank == 0:
+        out = {
+            "metric": f"denoised frames/sec, {args.frames}x{args.size}x{args.size} clip, "
+                      f"{args.num_inference_steps}-step AnimateDiff-XL",
+            "value": round(value, 4), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "config": {"workload": f"BASELINE configs[2]: {args.frames}x{args.size}x{args.size} clip + UnZipLoRA "
+                                   f"rank-{args.lora_rank} ({args.lora_mode}) on all 560 spatial q/k/v/out, "
+                                   f"{args.num_inference_steps}-step Euler, CFG {args.guidance} batched (B=2)",
+                       "model": "SDXL UNet + AnimateDiff-SDXL motion modules (synthetic weights)",
+                       "global_batch": world, "frames": args.frames, "resolution": args.size,
+                       "parallelism": f"{args.parallel}x{world}" if world > 1 else "single"},
+            "roofline": rl, "cpu_baseline": cpu, "kernels": table, "finite": ok,
+            "setup_s": round(t_build, 1),
+        }
+        print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

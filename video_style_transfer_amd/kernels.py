@@ -19,6 +19,42 @@ def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
+# ---- launch profiler (bench.py roofline): HIP events around every launch of an instrumented op
+_PROF = None  # list of (kind, flops, bytes, ev_start, ev_end) while active
+
+
+def profile_launches(active: bool):
+    global _PROF
+    _PROF = [] if active else None
+
+
+def collect_launches():
+    """[(kind, flops, bytes, ms)] for the launches recorded since profile_launches(True)."""
+    torch.cuda.synchronize()
+    out = [(k, f, b, s.elapsed_time(e)) for k, f, b, s, e in (_PROF or [])]
+    return out
+
+
+class _Rec:
+    __slots__ = ("kind", "flops", "nbytes", "s")
+
+    def __init__(self, kind, flops, nbytes):
+        self.kind, self.flops, self.nbytes = kind, flops, nbytes
+        self.s = None
+
+    def __enter__(self):
+        if _PROF is not None:
+            self.s = torch.cuda.Event(enable_timing=True)
+            self.s.record()
+        return self
+
+    def __exit__(self, *a):
+        if _PROF is not None and self.s is not None:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            _PROF.append((self.kind, self.flops, self.nbytes, self.s, e))
+
+
 def _dev(t: torch.Tensor, dtype, name):
     if not t.is_cuda:
         raise _lib.VstError(f"{name}: tensor is on {t.device}; the HIP path has no CPU fallback")
@@ -39,7 +75,8 @@ def _ld(t):
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *, x2: torch.Tensor | None = None,
            residual: torch.Tensor | None = None, row_bias: torch.Tensor | None = None, row_bias_div: int = 1,
-           out: torch.Tensor | None = None, geglu: bool = False) -> torch.Tensor:
+           out: torch.Tensor | None = None, geglu: bool = False, alg_k2: int | None = None,
+           kind: str | None = None, alg_n: int | None = None) -> torch.Tensor:
     """out[M, N'] = epilogue([x | x2] @ w^T + bias + row_bias[m // div] + residual); N' = N or N/2 (GEGLU)."""
     _dev(x, BF16, "x")
     _dev(w, BF16, "w")
@@ -66,9 +103,14 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
     if row_bias is not None:
         if row_bias.dtype != F32 or not row_bias.is_cuda or row_bias.shape[-1] != N:
             raise _lib.VstError("linear: row_bias must be fp32 [M/div, N]")
-    _lib.call("vst_gemm", _p(x), _ld(x), _p(x2), 0 if x2 is None else _ld(x2), K1, _p(w), _ld(w), M, N, K, _p(bias),
-              _p(row_bias), row_bias_div, N if row_bias is not None else 0, _p(residual),
-              0 if residual is None else _ld(residual), _p(out), _ld(out), 1 if geglu else 0, _stream())
+    # algorithmic work: the LoRA columns count only their real rank (alg_k2), not the zero padding
+    k_alg = K1 + (0 if x2 is None else (x2.shape[1] if alg_k2 is None else alg_k2))
+    kind = kind or ("gemm_geglu" if geglu else ("gemm_lora" if x2 is not None and alg_k2 is not None else "gemm"))
+    n_alg = N if alg_n is None else alg_n
+    with _Rec(kind, 2.0 * M * n_alg * k_alg, 2.0 * (M * k_alg + N * k_alg + M * n_out * (2 if residual is not None else 1))):
+        _lib.call("vst_gemm", _p(x), _ld(x), _p(x2), 0 if x2 is None else _ld(x2), K1, _p(w), _ld(w), M, N, K,
+                  _p(bias), _p(row_bias), row_bias_div, N if row_bias is not None else 0, _p(residual),
+                  0 if residual is None else _ld(residual), _p(out), _ld(out), 1 if geglu else 0, _stream())
     return out
 
 
@@ -105,9 +147,11 @@ def conv3x3(x1: torch.Tensor, nimg: int, H: int, W: int, w: torch.Tensor, bias: 
         raise _lib.VstError("conv3x3: bias must be fp32 [Cout]")
     if residual is not None:
         _dev(residual, BF16, "residual")
-    _lib.call("vst_conv3x3", _p(x1), C1, _p(x2), C2, nimg, H, W, stride, 1 if upsample else 0, _p(w), Cout,
-              _p(bias), _p(row_bias), row_bias_div, _p(residual), 0 if residual is None else _ld(residual), _p(out),
-              _ld(out) if Cout >= 8 else Cout, _stream())
+    kind = "conv3x3" if (C1 + C2) % 64 == 0 else "conv3x3_small_cin"
+    with _Rec(kind, 2.0 * M * Cout * kreal, 2.0 * (nimg * H * W * (C1 + C2) + Cout * kreal + M * Cout)):
+        _lib.call("vst_conv3x3", _p(x1), C1, _p(x2), C2, nimg, H, W, stride, 1 if upsample else 0, _p(w), Cout,
+                  _p(bias), _p(row_bias), row_bias_div, _p(residual), 0 if residual is None else _ld(residual),
+                  _p(out), _ld(out) if Cout >= 8 else Cout, _stream())
     return out
 
 
@@ -123,8 +167,10 @@ def spatial_attention(q, k, v, nbatch, heads, Nq, Nk, kv_div=1, out=None, scale=
         out = torch.empty((nbatch * Nq, heads * 64), dtype=BF16, device=q.device)
     _dev(out, BF16, "out")
     scale = 0.125 if scale is None else scale
-    _lib.call("vst_spatial_attention", _p(q), _ld(q), _p(k), _p(v), k.stride(0), _p(out), _ld(out), nbatch, heads,
-              Nq, Nk, kv_div, 64, float(scale), _stream())
+    with _Rec("spatial_attention", 4.0 * nbatch * heads * Nq * Nk * 64,
+              2.0 * 64 * heads * (2 * nbatch * Nq + 2 * (nbatch // kv_div) * Nk)):
+        _lib.call("vst_spatial_attention", _p(q), _ld(q), _p(k), _p(v), k.stride(0), _p(out), _ld(out), nbatch,
+                  heads, Nq, Nk, kv_div, 64, float(scale), _stream())
     return out
 
 
@@ -139,8 +185,10 @@ def temporal_attention(q, k, v, nclip, F, HW, heads, head_dim, out=None, scale=N
     if out is None:
         out = torch.empty((q.shape[0], heads * head_dim), dtype=BF16, device=q.device)
     scale = head_dim ** -0.5 if scale is None else scale
-    _lib.call("vst_temporal_attention", _p(q), _p(k), _p(v), q.stride(0), _p(out), _ld(out), nclip, F, HW, heads,
-              head_dim, float(scale), _stream())
+    T = nclip * F * HW
+    with _Rec("temporal_attention", 4.0 * T * F * heads * head_dim, 2.0 * 4 * T * heads * head_dim):
+        _lib.call("vst_temporal_attention", _p(q), _p(k), _p(v), q.stride(0), _p(out), _ld(out), nclip, F, HW, heads,
+                  head_dim, float(scale), _stream())
     return out
 
 
@@ -155,9 +203,10 @@ def group_norm(x1, nsamples, rows_per_sample, groups, eps, gamma, beta, *, silu=
         out = torch.empty((x1.shape[0], C), dtype=BF16, device=x1.device)
     ws_bytes = _lib.load().vst_groupnorm_workspace_bytes(nsamples, rows_per_sample, groups)
     ws = torch.empty((ws_bytes + 3) // 4, dtype=F32, device=x1.device)
-    _lib.call("vst_groupnorm", _p(x1), _ld(x1), x1.shape[1], _p(x2), 0 if x2 is None else _ld(x2),
-              0 if x2 is None else x2.shape[1], nsamples, rows_per_sample, groups, float(eps), _p(gamma), _p(beta),
-              1 if silu else 0, _p(out), _ld(out), _p(ws), _stream())
+    with _Rec("groupnorm", 0.0, 2.0 * 3 * x1.shape[0] * C):  # two reads + one write
+        _lib.call("vst_groupnorm", _p(x1), _ld(x1), x1.shape[1], _p(x2), 0 if x2 is None else _ld(x2),
+                  0 if x2 is None else x2.shape[1], nsamples, rows_per_sample, groups, float(eps), _p(gamma),
+                  _p(beta), 1 if silu else 0, _p(out), _ld(out), _p(ws), _stream())
     return out
 
 
@@ -166,8 +215,9 @@ def layer_norm(x, gamma, beta, eps=1e-5, *, pe=None, pe_div=1, pe_mod=1, out=Non
     rows, C = x.shape
     if out is None:
         out = torch.empty((rows, C), dtype=BF16, device=x.device)
-    _lib.call("vst_layernorm", _p(x), _ld(x), C, rows, _p(gamma), _p(beta), float(eps), _p(pe), pe_div, pe_mod,
-              _p(out), _ld(out), _stream())
+    with _Rec("layernorm", 0.0, 2.0 * 2 * rows * C):
+        _lib.call("vst_layernorm", _p(x), _ld(x), C, rows, _p(gamma), _p(beta), float(eps), _p(pe), pe_div, pe_mod,
+                  _p(out), _ld(out), _stream())
     return out
 
 

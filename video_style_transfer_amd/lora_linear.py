@@ -97,6 +97,7 @@ class ProjOps:
     bias: Optional[torch.Tensor]     # fp32 [N] or None
     k1: int
     n: int
+    r: int = 0                       # real (unpadded) low-rank width
 
 
 def _linear_parts(lin):
@@ -167,7 +168,7 @@ def build_ops(lins: Sequence[nn.Module], scale: float = 1.0, mode: Optional[str]
         if any(b is not None for b in bs):
             bias = torch.cat([b if b is not None else torch.zeros(w.shape[0], device=dev) for w, b in zip(Ws, bs)])
             bias = bias.contiguous()
-        ops = ProjOps(W_all.to(torch.bfloat16).contiguous(), a_bf, bias, K1, N)
+        ops = ProjOps(W_all.to(torch.bfloat16).contiguous(), a_bf, bias, K1, N, R if a_bf is not None else 0)
     cache[key] = (skey, ops)
     return ops
 
@@ -175,8 +176,8 @@ def build_ops(lins: Sequence[nn.Module], scale: float = 1.0, mode: Optional[str]
 def run_ops(x2d: torch.Tensor, ops: ProjOps, residual=None, out=None, geglu=False) -> torch.Tensor:
     if ops.a is None:
         return K.linear(x2d, ops.w, ops.bias, residual=residual, out=out, geglu=geglu)
-    u = K.linear(x2d, ops.a)
-    return K.linear(x2d, ops.w, ops.bias, x2=u, residual=residual, out=out, geglu=geglu)
+    u = K.linear(x2d, ops.a, kind="gemm_lora_down", alg_n=ops.r)
+    return K.linear(x2d, ops.w, ops.bias, x2=u, residual=residual, out=out, geglu=geglu, alg_k2=ops.r)
 
 
 class LoRACompatibleLinear(nn.Linear):

@@ -17,7 +17,7 @@ from .config import UNetMotionConfig
 from .lora_linear import LoRACompatibleLinear
 from .unet_motion import UNetMotionModel
 from .unziplora_linear_layer import UnZipLoRALinearLayerInfer
-from .weights import synthetic_state_dict
+from .weights import init_synthetic_, synthetic_state_dict  # noqa: F401
 
 LORA_WEIGHT_NAME_SAFE = "pytorch_lora_weights.safetensors"
 PARTS = ("to_q", "to_k", "to_v", "to_out.0")
@@ -140,11 +140,20 @@ def build_unet(cfg: Optional[UNetMotionConfig] = None, *, state_dict=None, seed:
     cfg = cfg or UNetMotionConfig.sdxl()
     with torch.device("meta"):
         unet = UNetMotionModel(cfg)
+    if state_dict is None:
+        # seeded synthetic weights generated directly on the target device
+        unet = unet.to_empty(device=device)
+        if lora_rank:
+            attach_unziplora_layers(unet, lora_rank)
+        for name, p in unet.named_parameters():
+            if "lora_layer" not in name:
+                p.data = p.data.to(dtype)
+        init_synthetic_(unet, cfg, seed, lora_rank)
+        return unet.requires_grad_(False)
     unet = unet.to_empty(device="cpu")
     if lora_rank:
         attach_unziplora_layers(unet, lora_rank)
-    sd = state_dict if state_dict is not None else synthetic_state_dict(cfg, seed, lora_rank)
-    unet.load_state_dict(sd, strict=True)
+    unet.load_state_dict(state_dict, strict=True)
     unet.requires_grad_(False)
     # UNet weights in the compute dtype; UnZipLoRA params stay fp32 like the reference (dtype=None)
     for name, p in unet.named_parameters():

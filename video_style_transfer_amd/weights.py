@@ -149,6 +149,37 @@ def param_shapes(cfg: UNetMotionConfig, lora_rank: int | None = 8) -> "OrderedDi
     return S
 
 
+def _init_value(name, shape, kind, g, device):
+    if kind in ("w", "wo"):
+        fan_in = int(math.prod(shape[1:]))
+        return torch.randn(shape, generator=g, device=device) * ((0.5 if kind == "wo" else 1.0) / math.sqrt(fan_in))
+    if kind == "b":
+        return torch.randn(shape, generator=g, device=device) * 0.02
+    if kind == "g":
+        return 1.0 + torch.randn(shape, generator=g, device=device) * 0.05
+    if kind == "lora":
+        r = shape[0] if "_down" in name else shape[1]
+        return torch.randn(shape, generator=g, device=device) / r
+    if kind == "merger":
+        return torch.rand(shape, generator=g, device=device)
+    if kind == "pe":
+        return sinusoid_table(shape[-1], shape[1]).to(device)
+    raise ValueError(kind)
+
+
+@torch.no_grad()
+def init_synthetic_(module, cfg: UNetMotionConfig, seed: int = 0, lora_rank: int | None = 8):
+    """Fill an existing (e.g. to_empty'd) module in place, on its own device, with the same
+    distributions as synthetic_state_dict (device RNG: values differ from the CPU stream)."""
+    sd = module.state_dict()
+    dev = next(iter(sd.values())).device
+    g = torch.Generator(device=dev).manual_seed(seed)
+    for name, (shape, kind) in param_shapes(cfg, lora_rank).items():
+        t = sd[name]
+        t.copy_(_init_value(name, shape, kind, g, dev).to(t.dtype))
+    return module
+
+
 def synthetic_state_dict(cfg: UNetMotionConfig, seed: int = 0, lora_rank: int | None = 8,
                          dtype: torch.dtype = torch.float32) -> "OrderedDict[str, torch.Tensor]":
     """Seeded synthetic weights: linear/conv ~ N(0,1)/sqrt(fan_in) (0.5x on the
@@ -159,21 +190,5 @@ def synthetic_state_dict(cfg: UNetMotionConfig, seed: int = 0, lora_rank: int | 
     g = torch.Generator().manual_seed(seed)
     out = OrderedDict()
     for name, (shape, kind) in param_shapes(cfg, lora_rank).items():
-        if kind in ("w", "wo"):
-            fan_in = int(torch.tensor(shape[1:]).prod())
-            t = torch.randn(shape, generator=g) * ((0.5 if kind == "wo" else 1.0) / math.sqrt(fan_in))
-        elif kind == "b":
-            t = torch.randn(shape, generator=g) * 0.02
-        elif kind == "g":
-            t = 1.0 + torch.randn(shape, generator=g) * 0.05
-        elif kind == "lora":
-            r = shape[0] if "_down" in name else shape[1]
-            t = torch.randn(shape, generator=g) / r
-        elif kind == "merger":
-            t = torch.rand(shape, generator=g)
-        elif kind == "pe":
-            t = sinusoid_table(shape[-1], shape[1])
-        else:
-            raise ValueError(kind)
-        out[name] = t.to(dtype)
+        out[name] = _init_value(name, shape, kind, g, "cpu").to(dtype)
     return out
