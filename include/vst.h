@@ -29,6 +29,13 @@ extern "C" {
 int vst_gemm(const void* A, int lda, const void* A2, int lda2, int K1, const void* W, int ldw, int M, int N, int K,
              const float* bias, const float* row_bias, int row_bias_div, int ld_row_bias, const void* R, int ldr,
              void* C, int ldc, int epilogue, void* stream);
+/* Same, with the tile (0 auto, 1 = 128x128, 2 = 128x64) and split-K (0 auto, >= 1 forced) choice and a
+ * caller-owned fp32 workspace for split-K slabs (NULL / too small disables split-K). */
+int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int K1, const void* W, int ldw, int M, int N, int K,
+                const float* bias, const float* row_bias, int row_bias_div, int ld_row_bias, const void* R, int ldr,
+                void* C, int ldc, int epilogue, int tile, int splits, void* workspace, size_t ws_bytes,
+                void* stream);
+size_t vst_gemm_workspace_bytes(int M, int N, int K);
 
 /* 3x3 conv, padding 1, NHWC, optional channel-concat second input, stride 1|2, fused nearest-2x
  * upsample; Wt = [Cout][3][3][C1+C2].  Replaces the per-frame torch conv2d calls of diffusers
@@ -37,6 +44,10 @@ int vst_gemm(const void* A, int lda, const void* A2, int lda2, int K1, const voi
 int vst_conv3x3(const void* x1, int C1, const void* x2, int C2, int nimg, int H, int W, int stride, int upsample,
                 const void* Wt, int Cout, const float* bias, const float* row_bias, int row_bias_div, const void* R,
                 int ldr, void* out, int ldc, void* stream);
+int vst_conv3x3_ex(const void* x1, int C1, const void* x2, int C2, int nimg, int H, int W, int stride, int upsample,
+                   const void* Wt, int Cout, const float* bias, const float* row_bias, int row_bias_div,
+                   const void* R, int ldr, void* out, int ldc, int tile, int splits, void* workspace,
+                   size_t ws_bytes, void* stream);
 
 /* Spatial SDPA, head_dim 64: replaces F.scaled_dot_product_attention in
  * AnimateDiffAttnProcessor2_0.__call__ (animatediff/attention_processor.py:78-80).  K/V row
@@ -50,7 +61,7 @@ int vst_temporal_attention(const void* q, const void* k, const void* v, int ldqk
                            int F, int HW, int heads, int head_dim, float scale, void* stream);
 
 /* GroupNorm (+SiLU) over NHWC samples of rows_per_sample rows; optional 2-source channel concat. */
-size_t vst_groupnorm_workspace_bytes(int nsamples, int rows_per_sample, int groups);
+size_t vst_groupnorm_workspace_bytes(int nsamples, int rows_per_sample, int groups, int C);
 int vst_groupnorm(const void* x1, int ld1, int C1, const void* x2, int ld2, int C2, int nsamples,
                   int rows_per_sample, int groups, float eps, const float* gamma, const float* beta, int silu_act,
                   void* y, int ldy, void* workspace, void* stream);

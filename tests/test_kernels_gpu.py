@@ -45,6 +45,53 @@ def test_gemm_bias_residual(cuda, K, M, N, Kd):
     check(out, ref, name="gemm")
 
 
+@pytest.mark.parametrize("tile,splits", [(1, 1), (2, 1), (1, 3), (2, 5), (0, 0), (3, 1), (4, 1)])
+@pytest.mark.parametrize("geglu", [False, True])
+def test_gemm_tile_and_splitk_variants(cuda, K, tile, splits, geglu):
+    g = torch.Generator().manual_seed(tile * 10 + splits)
+    M, N, Kd, K2 = 300, 384, 640, 32
+    x, x2 = rnd(M, Kd, gen=g), rnd(M, K2, gen=g)
+    w = rnd(N, Kd + K2, scale=0.04, gen=g)
+    b = torch.randn(N, generator=g)
+    rb = torch.randn(M // 100, N, generator=g)
+    r = rnd(M, N // 2 if geglu else N, gen=g)
+    K.GEMM_POLICY.update(tile=tile, splits=splits)
+    try:
+        if geglu:
+            out = K.linear(x.to(cuda), w.to(cuda), b.to(cuda), x2=x2.to(cuda), geglu=True)
+        else:
+            out = K.linear(x.to(cuda), w.to(cuda), b.to(cuda), x2=x2.to(cuda), row_bias=rb.to(cuda),
+                           row_bias_div=100, residual=r.to(cuda))
+    finally:
+        K.GEMM_POLICY.update(tile=0, splits=0)
+    y = torch.cat([x, x2], 1).float() @ w.float().t() + b
+    if geglu:
+        idx = torch.arange(N).view(-1, 128)
+        h, gt = y[:, idx[:, :64].reshape(-1)], y[:, idx[:, 64:].reshape(-1)]
+        ref = h * F.gelu(gt)
+    else:
+        ref = y + rb.repeat_interleave(100, 0) + r.float()
+    check(out, ref, name=f"gemm t{tile} s{splits} geglu={geglu}")
+
+
+@pytest.mark.parametrize("tile,splits", [(2, 1), (1, 4), (2, 3), (3, 1), (4, 1)])
+def test_conv_tile_and_splitk_variants(cuda, K, tile, splits):
+    g = torch.Generator().manual_seed(31 + splits)
+    n, C1, C2, Co, H, W = 2, 128, 64, 192, 8, 8
+    x1, x2 = rnd(n, C1, H, W, gen=g), rnd(n, C2, H, W, gen=g)
+    w = rnd(Co, C1 + C2, 3, 3, scale=(9 * (C1 + C2)) ** -0.5, gen=g)
+    b = torch.randn(Co, generator=g) * 0.1
+    r = rnd(n, Co, H, W, gen=g)
+    K.GEMM_POLICY.update(tile=tile, splits=splits)
+    try:
+        out = K.conv3x3(to_nhwc(x1).to(cuda), n, H, W, wflat(w).to(cuda), b.to(cuda), x2=to_nhwc(x2).to(cuda),
+                        residual=to_nhwc(r).to(cuda))
+    finally:
+        K.GEMM_POLICY.update(tile=0, splits=0)
+    ref = conv_ref(torch.cat([x1, x2], 1).float(), w.float(), b) + r.float()
+    check(out, to_nhwc(ref), name=f"conv t{tile} s{splits}")
+
+
 def test_gemm_two_source_and_rowbias(cuda, K):
     g = torch.Generator().manual_seed(7)
     M, K1, K2, N = 640, 640, 32, 384

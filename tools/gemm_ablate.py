@@ -1,0 +1,51 @@
+"""Ablation of the ring GEMM main loop (run once per VST_GEMM_ABLATE value: 0 full,
+1 no loop DMA, 2 no MFMA, 3 neither).  Prints TF/s-equivalent per (shape, tile)."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from video_style_transfer_amd import kernels as K  # noqa: E402
+
+BF = torch.bfloat16
+SHAPES = [("qkv1280", 8192, 3840, 1344), ("ff2_1280", 8192, 1280, 5120), ("ff2_640", 32768, 640, 2560),
+          ("big4k", 4096, 4096, 4096)]
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    dev = torch.device("cuda")
+    ab = os.environ.get("VST_GEMM_ABLATE", "0")
+    for name, M, N, Kd in SHAPES:
+        x = torch.randn(M, Kd, device=dev).to(BF)
+        w = (torch.randn(N, Kd, device=dev) / Kd ** 0.5).to(BF)
+        out = torch.empty(M, N, device=dev, dtype=BF)
+        fl = 2.0 * M * N * Kd
+        row = {"ablate": ab, "shape": name}
+        for t in (1, 3, 4):
+            K.GEMM_POLICY.update(tile=t, splits=1)
+            ms = timeit(lambda: K.linear(x, w, None, out=out))
+            row[f"t{t}_tf"] = round(fl / ms / 1e9, 1)
+            row[f"t{t}_us"] = round(ms * 1e3, 1)
+        if ab == "0":
+            ms = timeit(lambda: torch.nn.functional.linear(x, w))
+            row["hipblaslt_tf"] = round(fl / ms / 1e9, 1)
+        print(json.dumps(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -19,10 +19,15 @@ _F = ctypes.c_float
 _S = ctypes.c_size_t
 SIGNATURES = {
     "vst_gemm": (_I, [_P, _I, _P, _I, _I, _P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _I, _P, _I, _I, _P]),
+    "vst_gemm_ex": (_I, [_P, _I, _P, _I, _I, _P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _I, _P, _I, _I, _I, _I, _P, _S,
+                         _P]),
+    "vst_gemm_workspace_bytes": (_S, [_I, _I, _I]),
     "vst_conv3x3": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P, _I, _P, _I, _P]),
+    "vst_conv3x3_ex": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P, _I, _P, _I, _I, _I, _P, _S,
+                            _P]),
     "vst_spatial_attention": (_I, [_P, _I, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _F, _P]),
     "vst_temporal_attention": (_I, [_P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _F, _P]),
-    "vst_groupnorm_workspace_bytes": (_S, [_I, _I, _I]),
+    "vst_groupnorm_workspace_bytes": (_S, [_I, _I, _I, _I]),
     "vst_groupnorm": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _F, _P, _P, _I, _P, _I, _P, _P]),
     "vst_layernorm": (_I, [_P, _I, _I, _I, _P, _P, _F, _P, _I, _I, _P, _I, _P]),
     "vst_timestep_embedding": (_I, [_P, _P, _I, _I, _I, _F, _P, _I, _I, _I, _P]),

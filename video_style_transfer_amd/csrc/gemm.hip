@@ -13,43 +13,37 @@
 //      out-of-range buffer loads, stride 1/2, fused nearest-2x upsample, two-source
 //      channel concat (up-block skip connections).
 //   2  same conv with a scalar gather (tiny Cin, e.g. conv_in with 4 channels).
-// Epilogues (template EPI): 0 = +bias[n] +row_bias[m/div][n] +residual[m,n];
+// Epilogues (template EPI): 0 = +bias[n] +row_bias[m/div][n] +residual[m,n] -> bf16;
 //   1 = GEGLU (tile columns [0,64) hidden, [64,128) gate of the same 64 outputs;
-//   the host interleaves the weight rows accordingly).
+//   the host interleaves the weight rows accordingly); 2 = fp32 split-K partial slab
+//   (the epilogue then runs in gemm_splitk_reduce_kernel).
 //
-// Tile 128x128x64, 256 threads = 4 waves (2x2), each wave 64x64 via 4x4
-// v_mfma_f32_16x16x32_bf16.  Register-staged double-buffered LDS with the
-// load-early / write-late split; XOR-swizzled 128-byte LDS rows (conflict-free
-// ds_read_b128 fragment reads); XCD-aware tile order; fp32 LDS-staged epilogue
-// with 16-byte coalesced stores.
-#include "vst_common.h"
+// Tile BM=128 x BN (128 or 64) x BK=64, 256 threads = 4 waves (2x2), each wave 64 x BN/2 via
+// v_mfma_f32_16x16x32_bf16.  Register-staged double-buffered LDS with the load-early /
+// write-late split; XOR-swizzled 128-byte LDS rows (conflict-free ds_read_b128 fragment
+// reads); XCD-aware tile order; fp32 LDS-staged epilogue with 16-byte coalesced stores.
+// Host-side heuristic (vst_gemm): BN=64 when the 128x128 grid would run in few waves on
+// 256 CUs (tail effect), split-K (blockIdx.z) when even that grid cannot fill the chip.
+#include <cstdlib>
+
+#include "gemm_common.h"
 
 namespace vst {
 
-constexpr int BM = 128, BN = 128, BK = 64;
-constexpr int TILE_BYTES = BM * BK * 2;  // 16 KiB per operand tile
-constexpr int GEMM_LDS = 4 * TILE_BYTES;  // 2 buffers x (A,B) = 64 KiB (= fp32 C tile)
+constexpr int BM = 128, BK = 64;
+constexpr int A_TILE = BM * BK * 2;  // 16 KiB
 
-struct GemmArgs {
-  const bf16_t* A1; const bf16_t* A2;
-  int lda1, lda2, K1;
-  // conv geometry (AMODE 1/2): input NHWC [nimg, H, W, C1 (+C2)] -> output [nimg, OH, OW, N]
-  int H, W, C1, C2, OH, OW, stride, up;
-  const bf16_t* Wt; int ldw;
-  int M, N, K;
-  const float* bias;
-  const float* rbias; int rbias_div, ldrb;
-  const bf16_t* R; int ldr;
-  bf16_t* C; int ldc;
-  uint32_t a1_bytes, a2_bytes, w_bytes, r_bytes;
-};
-
-__device__ __forceinline__ int swz(int row, int chunk) {
-  return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
+template <int BN>
+constexpr int gemm_lds_bytes() {
+  return (2 * (A_TILE + BN * BK * 2)) > (BM * BN * 4) ? 2 * (A_TILE + BN * BK * 2) : BM * BN * 4;
 }
 
-template <int AMODE, int EPI>
+template <int AMODE, int EPI, int BN>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
+  constexpr int B_TILE = BN * BK * 2;
+  constexpr int STAGE = A_TILE + B_TILE;
+  constexpr int NT = BN / 32;      // 16-wide n tiles per wave
+  constexpr int BCH = BN / 32;     // B staging chunks per thread
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
@@ -83,15 +77,21 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
       }
     }
   }
-  int rowB[4];
+  int rowB[BCH];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < BCH; ++i) {
     const int n = n0 + sr + 32 * i;
     rowB[i] = n < p.N ? n : -1;
   }
 
-  u32x4 va[4], vb[4];
-  const int nk = (p.K + BK - 1) / BK;
+  u32x4 va[4], vb[BCH];
+  const int nk_all = (p.K + BK - 1) / BK;
+  int kt_beg = 0, kt_end = nk_all;
+  if (EPI == 2) {
+    const int z = blockIdx.z;
+    kt_beg = (int)((long long)nk_all * z / p.splits);
+    kt_end = (int)((long long)nk_all * (z + 1) / p.splits);
+  }
   const int Ctot = p.C1 + p.C2;
 
   auto load_tile = [&](int kt) {
@@ -99,7 +99,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
     const int k = k0 + sc * 8;
     // ---- B (weights) ----
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < BCH; ++i) {
       const int off = (rowB[i] >= 0 && k < p.K) ? (rowB[i] * p.ldw + k) * 2 : kOOB;
       vb[i] = buf_load16(rw, off);
     }
@@ -171,54 +171,49 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
   };
 
   auto store_tile = [&](int buf) {
-    char* As = smem + buf * 2 * TILE_BYTES;
-    char* Bs = As + TILE_BYTES;
+    char* As = smem + buf * STAGE;
+    char* Bs = As + A_TILE;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = sr + 32 * i;
-      *reinterpret_cast<u32x4*>(As + swz(row, sc)) = va[i];
-      *reinterpret_cast<u32x4*>(Bs + swz(row, sc)) = vb[i];
-    }
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(As + swz(sr + 32 * i, sc)) = va[i];
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) *reinterpret_cast<u32x4*>(Bs + swz(sr + 32 * i, sc)) = vb[i];
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[4][NT];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) load_tile(kt + 1);
-    const char* As = smem + cur * 2 * TILE_BYTES;
-    const char* Bs = As + TILE_BYTES;
+  if (kt_beg < kt_end) {
+    load_tile(kt_beg);
+    store_tile(0);
+  }
+  __syncthreads();
+
+  for (int kt = kt_beg; kt < kt_end; ++kt) {
+    const int cur = (kt - kt_beg) & 1;
+    if (kt + 1 < kt_end) load_tile(kt + 1);
+    const char* As = smem + cur * STAGE;
+    const char* Bs = As + A_TILE;
     // skip the second 32-deep half when it lies wholly beyond K (LoRA tail tile)
     const int nkk = (kt * BK + 32 < p.K) ? 2 : 1;
     for (int kk = 0; kk < nkk; ++kk) {
-      bf16x8 af[4], bfr[4];
+      bf16x8 af[4], bfr[NT];
       const int chunk = kk * 4 + fq;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = wr * 64 + i * 16 + fr;
-        af[i] = *reinterpret_cast<const bf16x8*>(As + swz(row, chunk));
-      }
+      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const bf16x8*>(As + swz(wr * 64 + i * 16 + fr, chunk));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = wc * 64 + j * 16 + fr;
-        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + swz(row, chunk));
-      }
+      for (int j = 0; j < NT; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + swz(wc * (BN / 2) + j * 16 + fr, chunk));
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < NT; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) store_tile(cur ^ 1);
+    if (kt + 1 < kt_end) store_tile(cur ^ 1);
     __syncthreads();
   }
 
@@ -227,21 +222,42 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < NT; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = wr * 64 + i * 16 + fq * 4 + r;
-        const int col = wc * 64 + j * 16 + fr;
+        const int col = wc * (BN / 2) + j * 16 + fr;
         Cs[row * BN + col] = acc[i][j][r];
       }
   __syncthreads();
 
+  constexpr int CPR = BN / 8;  // 8-column chunks per tile row
+  if (EPI == 2) {
+    float* slab = p.ws + (size_t)blockIdx.z * p.M * p.N;
+#pragma unroll 2
+    for (int it = 0; it < BM * CPR / 256; ++it) {
+      const int idx = tid + 256 * it;
+      const int row = idx / CPR, cc = idx - row * CPR;
+      const int m = m0 + row, n = n0 + cc * 8;
+      if (m >= p.M || n >= p.N) continue;
+      const f32x4 c0 = *reinterpret_cast<const f32x4*>(Cs + row * BN + cc * 8);
+      const f32x4 c1 = *reinterpret_cast<const f32x4*>(Cs + row * BN + cc * 8 + 4);
+      float* dst = slab + (size_t)m * p.N + n;
+      if (n + 8 <= p.N) {
+        *reinterpret_cast<f32x4*>(dst) = c0;
+        *reinterpret_cast<f32x4*>(dst + 4) = c1;
+      } else {
+        for (int e = 0; e < p.N - n; ++e) dst[e] = e < 4 ? c0[e] : c1[e - 4];
+      }
+    }
+    return;
+  }
   const auto rr = make_rsrc(p.R ? p.R : p.Wt, p.R ? p.r_bytes : 0u);
   if (EPI == 0) {
 #pragma unroll 2
-    for (int it = 0; it < 8; ++it) {
+    for (int it = 0; it < BM * CPR / 256; ++it) {
       const int idx = tid + 256 * it;
-      const int row = idx >> 4, cc = idx & 15;
+      const int row = idx / CPR, cc = idx - row * CPR;
       const int m = m0 + row, n = n0 + cc * 8;
       if (m >= p.M || n >= p.N) continue;
       float v[8];
@@ -275,7 +291,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
         }
       }
     }
-  } else {  // GEGLU: out[m, n0/2 + c] = (h + bh) * gelu(g + bg)
+  } else {  // GEGLU (BN == 128): out[m, n0/2 + c] = (h + bh) * gelu(g + bg)
 #pragma unroll 2
     for (int it = 0; it < 4; ++it) {
       const int idx = tid + 256 * it;
@@ -295,23 +311,155 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
   }
 }
 
-template <int AMODE, int EPI>
-static int launch(const GemmArgs& a, hipStream_t s) {
+// sum the split-K slabs and apply the epilogue.  geglu: slab columns are the interleaved
+// [h(64) | g(64)] blocks; each thread produces 8 output columns.
+__global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(GemmArgs p, int geglu) {
+  const int Nout = geglu ? p.N / 2 : p.N;
+  const int CPR = (Nout + 7) / 8;
+  const size_t total = (size_t)p.M * CPR;
+  const size_t slab = (size_t)p.M * p.N;
+  for (size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (size_t)gridDim.x * 256) {
+    const int m = (int)(idx / CPR);
+    const int n = (int)(idx - (size_t)m * CPR) * 8;
+    const int nv = min(8, Nout - n);
+    float v[8];
+    if (!geglu) {
+      const float* src = p.ws + (size_t)m * p.N + n;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 0.f;
+      for (int z = 0; z < p.splits; ++z) {
+        const float* s = src + z * slab;
+        if (nv == 8) {
+          const f32x4 a = *reinterpret_cast<const f32x4*>(s), b = *reinterpret_cast<const f32x4*>(s + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { v[e] += a[e]; v[e + 4] += b[e]; }
+        } else {
+          for (int e = 0; e < nv; ++e) v[e] += s[e];
+        }
+      }
+      for (int e = 0; e < nv; ++e) {
+        if (p.bias) v[e] += p.bias[n + e];
+        if (p.rbias) v[e] += p.rbias[(size_t)(m / p.rbias_div) * p.ldrb + n + e];
+        if (p.R) v[e] += bf2f(p.R[(size_t)m * p.ldr + n + e]);
+      }
+    } else {
+      const int blk = n / 64, c = n - blk * 64;
+      const int hc = blk * 128 + c, gc = hc + 64;
+      float h[8], g[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { h[e] = 0.f; g[e] = 0.f; }
+      for (int z = 0; z < p.splits; ++z) {
+        const float* s = p.ws + z * slab + (size_t)m * p.N;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { h[e] += s[hc + e]; g[e] += s[gc + e]; }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if (p.bias) { h[e] += p.bias[hc + e]; g[e] += p.bias[gc + e]; }
+        v[e] = h[e] * gelu_erf(g[e]);
+      }
+    }
+    bf16_t* dst = p.C + (size_t)m * p.ldc + n;
+    if (nv == 8 && !((uintptr_t)dst & 15)) {
+      *reinterpret_cast<u32x4*>(dst) = pack8(v);
+    } else {
+      for (int e = 0; e < nv; ++e) dst[e] = f2bf(v[e]);
+    }
+  }
+}
+
+template <int AMODE, int EPI, int BN>
+static int launch_one(const GemmArgs& a, hipStream_t s, int splits) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_kernel<AMODE, EPI>), dim3(nwg), dim3(256), GEMM_LDS, s, a);
+  hipLaunchKernelGGL((gemm_kernel<AMODE, EPI, BN>), dim3(nwg, 1, splits), dim3(256), gemm_lds_bytes<BN>(), s, a);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 
 static inline uint32_t clamp_bytes(size_t b) { return b > 0x7fffffffULL ? 0x7fffffffu : (uint32_t)b; }
 
+constexpr int kCUs = 256;
+
+// tile / split choice.  tile: 0 auto, 1 = 128x128, 2 = 128x64.  splits: 0 auto, >=1 forced.
+// tile codes: 1 = 128x128, 2 = 128x64 (gemm_kernel, 4 waves, up to 2 WG/CU);
+//             3 = 256x256, 4 = 256x128 (gemm_big_kernel, 8 waves, LDS-DMA staging, 1 WG/CU)
+static void choose(int M, int N, int K, int geglu, size_t ws_bytes, int& tile, int& splits) {
+  const int mt = (M + BM - 1) / BM;
+  const int t128 = mt * ((N + 127) / 128);
+  const int t64 = mt * ((N + 63) / 64);
+  const int nk = (K + BK - 1) / BK;
+  const int mb = (M + 255) / 256;
+  const int t256 = mb * ((N + 255) / 256), t256n = mb * ((N + 127) / 128);
+  const double waste256 = 1.0 - (double)N / (((N + 255) / 256) * 256);
+  const double waste128 = 1.0 - (double)N / (((N + 127) / 128) * 128);
+  const int nk32 = (K + 31) / 32;  // ring kernel k-tiles
+  (void)nk;
+  if (tile == 0) {
+    if (t256 >= 2 * kCUs && waste256 <= 0.1) tile = 3;
+    else if (t256n >= 2 * kCUs && waste128 <= 0.1) tile = 4;
+    else if (t128 >= kCUs && waste128 <= 0.1) tile = 1;
+    else tile = geglu ? 1 : 2;
+  }
+  if (geglu && tile == 2) tile = 1;
+  const int tiles = tile == 1 ? t128 : tile == 2 ? t64 : tile == 3 ? t256 : t256n;
+  if (splits == 0) {
+    splits = 1;
+    if (tiles < kCUs && nk32 >= 8) {
+      splits = std::min(std::min((2 * kCUs + tiles - 1) / tiles, nk32 / 4), 16);
+      if (splits < 2) splits = 1;
+    }
+  }
+  if (splits > nk32) splits = nk32;
+  if (splits > 1) {
+    const size_t need = (size_t)splits * M * N * sizeof(float);
+    if (need > ws_bytes) splits = 1;
+    if (splits > nk) splits = nk;
+  }
+}
+
+int launch_gemm_ring(const GemmArgs& a, int amode, int epi, int tile, int splits, hipStream_t s);
+
+static int gemm_ablate_env() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("VST_GEMM_ABLATE");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+
+static int run_gemm(GemmArgs& a, int amode, int geglu, int tile, int splits, hipStream_t s) {
+  a.ablate = gemm_ablate_env();
+  if (amode == 2) {  // scalar-gather conv (conv_in): register-staged kernel, no split
+    a.splits = 1;
+    return launch_one<2, 0, 64>(a, s, 1);
+  }
+  a.splits = splits;
+  if (splits > 1) {
+    const int rc = launch_gemm_ring(a, amode, 2, tile, splits, s);
+    if (rc) return rc;
+    const int Nout = geglu ? a.N / 2 : a.N;
+    const size_t chunks = (size_t)a.M * ((Nout + 7) / 8);
+    const int grid = (int)std::min<size_t>((chunks + 255) / 256, 4096);
+    hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(grid), dim3(256), 0, s, a, geglu);
+    return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+  }
+  return launch_gemm_ring(a, amode, geglu ? 1 : 0, tile, 1, s);
+}
+
 }  // namespace vst
 
 using namespace vst;
 
-extern "C" int vst_gemm(const void* A, int lda, const void* A2, int lda2, int K1,
-                        const void* W, int ldw, int M, int N, int K,
-                        const float* bias, const float* row_bias, int row_bias_div, int ld_row_bias,
-                        const void* R, int ldr, void* C, int ldc, int epilogue, void* stream) {
+extern "C" size_t vst_gemm_workspace_bytes(int M, int N, int K) {
+  int tile = 0, splits = 0;
+  choose(M, N, K, 0, (size_t)-1, tile, splits);
+  return splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
+}
+
+extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int K1, const void* W, int ldw, int M,
+                           int N, int K, const float* bias, const float* row_bias, int row_bias_div, int ld_row_bias,
+                           const void* R, int ldr, void* C, int ldc, int epilogue, int tile, int splits,
+                           void* workspace, size_t ws_bytes, void* stream) {
   if (!A || !W || !C || M <= 0 || N <= 0 || K <= 0) return VST_ERR_ARG;
   if ((K & 7) || (lda & 7) || (ldw & 7) || (ldc & 7)) return VST_ERR_ARG;
   if (A2) {
@@ -319,33 +467,43 @@ extern "C" int vst_gemm(const void* A, int lda, const void* A2, int lda2, int K1
   } else {
     K1 = K;
   }
-  if (epilogue == 1 && (N % BN)) return VST_ERR_ARG;
+  if (epilogue == 1 && (N % 128)) return VST_ERR_ARG;
   if (R && (ldr & 7)) return VST_ERR_ARG;
   if (row_bias && row_bias_div <= 0) return VST_ERR_ARG;
+  if (tile < 0 || tile > 4 || splits < 0) return VST_ERR_ARG;
   GemmArgs a{};
   a.A1 = (const bf16_t*)A; a.A2 = (const bf16_t*)A2; a.lda1 = lda; a.lda2 = lda2; a.K1 = K1;
   a.Wt = (const bf16_t*)W; a.ldw = ldw; a.M = M; a.N = N; a.K = K;
   a.bias = bias; a.rbias = row_bias; a.rbias_div = row_bias_div; a.ldrb = ld_row_bias;
   a.R = (const bf16_t*)R; a.ldr = ldr; a.C = (bf16_t*)C; a.ldc = ldc;
+  a.ws = (float*)workspace;
   a.a1_bytes = clamp_bytes(((size_t)(M - 1) * lda + K1) * 2);
   a.a2_bytes = A2 ? clamp_bytes(((size_t)(M - 1) * lda2 + (K - K1)) * 2) : 0;
   a.w_bytes = clamp_bytes(((size_t)(N - 1) * ldw + K) * 2);
   a.r_bytes = R ? clamp_bytes(((size_t)(M - 1) * ldr + N) * 2) : 0;
   a.C1 = 0; a.C2 = 0; a.stride = 1; a.up = 0;
-  hipStream_t s = (hipStream_t)stream;
-  return epilogue == 1 ? launch<0, 1>(a, s) : launch<0, 0>(a, s);
+  choose(M, N, K, epilogue == 1, workspace ? ws_bytes : 0, tile, splits);
+  return run_gemm(a, 0, epilogue == 1, tile, splits, (hipStream_t)stream);
+}
+
+extern "C" int vst_gemm(const void* A, int lda, const void* A2, int lda2, int K1, const void* W, int ldw, int M, int N,
+                        int K, const float* bias, const float* row_bias, int row_bias_div, int ld_row_bias,
+                        const void* R, int ldr, void* C, int ldc, int epilogue, void* stream) {
+  return vst_gemm_ex(A, lda, A2, lda2, K1, W, ldw, M, N, K, bias, row_bias, row_bias_div, ld_row_bias, R, ldr, C, ldc,
+                     epilogue, 0, 1, nullptr, 0, stream);
 }
 
 // 3x3 conv, padding 1, NHWC.  x1: [nimg,H,W,C1], optional x2: [nimg,H,W,C2] concatenated
 // on channels.  Wt: [Cout][3][3][C1+C2].  stride 1 or 2; upsample=1 applies nearest 2x to
 // the input first (output 2H x 2W).  Output [nimg, OH, OW, Cout] with row stride ldc.
-extern "C" int vst_conv3x3(const void* x1, int C1, const void* x2, int C2, int nimg, int H, int W,
-                           int stride, int upsample, const void* Wt, int Cout,
-                           const float* bias, const float* row_bias, int row_bias_div,
-                           const void* R, int ldr, void* out, int ldc, void* stream) {
+extern "C" int vst_conv3x3_ex(const void* x1, int C1, const void* x2, int C2, int nimg, int H, int W, int stride,
+                              int upsample, const void* Wt, int Cout, const float* bias, const float* row_bias,
+                              int row_bias_div, const void* R, int ldr, void* out, int ldc, int tile, int splits,
+                              void* workspace, size_t ws_bytes, void* stream) {
   if (!x1 || !Wt || !out || nimg <= 0 || H <= 0 || W <= 0 || Cout <= 0) return VST_ERR_ARG;
   if (stride != 1 && stride != 2) return VST_ERR_ARG;
   if (upsample && stride != 1) return VST_ERR_ARG;
+  if (tile < 0 || tile > 4 || splits < 0) return VST_ERR_ARG;
   const int Ct = C1 + (x2 ? C2 : 0);
   const bool vec = (Ct % BK == 0) && (C1 % 8 == 0);
   if (x2 && !vec) return VST_ERR_ARG;
@@ -360,11 +518,20 @@ extern "C" int vst_conv3x3(const void* x1, int C1, const void* x2, int C2, int n
   a.Wt = (const bf16_t*)Wt; a.ldw = a.K;
   a.bias = bias; a.rbias = row_bias; a.rbias_div = row_bias_div; a.ldrb = Cout;
   a.R = (const bf16_t*)R; a.ldr = ldr; a.C = (bf16_t*)out; a.ldc = ldc;
+  a.ws = (float*)workspace;
   a.a1_bytes = clamp_bytes((size_t)nimg * H * W * C1 * 2);
   a.a2_bytes = x2 ? clamp_bytes((size_t)nimg * H * W * C2 * 2) : 0;
   a.w_bytes = clamp_bytes((size_t)Cout * a.K * 2);
   a.r_bytes = R ? clamp_bytes(((size_t)(a.M - 1) * ldr + Cout) * 2) : 0;
   if ((ldc & 7) && Cout >= 8) return VST_ERR_ARG;
-  hipStream_t s = (hipStream_t)stream;
-  return vec ? launch<1, 0>(a, s) : launch<2, 0>(a, s);
+  if (!vec) { tile = 2; splits = 1; }
+  choose(a.M, a.N, a.K, 0, workspace ? ws_bytes : 0, tile, splits);
+  return run_gemm(a, vec ? 1 : 2, 0, tile, splits, (hipStream_t)stream);
+}
+
+extern "C" int vst_conv3x3(const void* x1, int C1, const void* x2, int C2, int nimg, int H, int W, int stride,
+                           int upsample, const void* Wt, int Cout, const float* bias, const float* row_bias,
+                           int row_bias_div, const void* R, int ldr, void* out, int ldc, void* stream) {
+  return vst_conv3x3_ex(x1, C1, x2, C2, nimg, H, W, stride, upsample, Wt, Cout, bias, row_bias, row_bias_div, R, ldr,
+                        out, ldc, 0, 1, nullptr, 0, stream);
 }

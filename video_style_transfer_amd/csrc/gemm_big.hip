@@ -1,0 +1,404 @@
+// LDS-DMA ring GEMM: the main bf16 MFMA GEMM of the denoise path (projections, GEGLU FF,
+// implicit-GEMM conv3x3, split-K partials).  Same contract as gemm.hip (GemmArgs, AMODE 0/1,
+// EPI 0/1/2).  Tiles (template): 256x256 and 256x128 (8 waves, 1 WG/CU), 128x128 and 128x64
+// (4 waves, 2-3 WG/CU).
+//
+// Staging: `buffer_load_dwordx4 ... lds` (__builtin_amdgcn_raw_ptr_buffer_load_lds) writes each
+// wave's 1 KiB piece (16 rows x 64 B) straight into LDS; the buffer range check supplies the
+// zeros for conv padding, M/N tails and the LoRA K tail.  BK = 32, 4-stage ring, ONE barrier per
+// k-tile: at iteration k the DMA for tile k+3 goes into the stage read at k-1 (every wave has
+// passed the barrier that ended k-1), the MFMAs of tile k run, then a counted
+// `s_waitcnt vmcnt(N)` retires only tile k+1 before the barrier — two tiles (~1 us) stay in flight,
+// covering the ~1.1 us issue->landed time of LDS-DMA under load (MI355X price list).
+//
+// LDS image per stage: [rows][32 bf16] (64-B rows), 16-B chunk c of row r stored at slot
+// c ^ G[(r >> 2) & 3] with G = {2,0,1,3}: every ds_read_b128 fragment read (16 rows x one chunk
+// per 16-lane block) is bank-conflict free under CDNA4's b128 lane grouping
+// {0-3,12-15,20-27},{4-11,16-19,28-31},... .  Because the DMA image is lane-linear, the inverse
+// permutation is applied to each lane's SOURCE address (lane l fetches chunk (l&3) ^ G[(l>>4)&3]).
+#include "gemm_common.h"
+
+namespace vst {
+
+constexpr int RBK = 32;
+
+__device__ __forceinline__ int gperm(int x) { return (0x3102 >> (4 * x)) & 3; }  // G = {2,0,1,3}
+__device__ __forceinline__ int rswz(int row, int chunk) {
+  return row * 64 + ((chunk ^ gperm((row >> 2) & 3)) << 4);
+}
+
+template <int BM_, int BN_, int WM_, int WN_, int STAGES_>
+struct RingCfg {
+  static constexpr int STAGES = STAGES_;
+  static constexpr int BM = BM_, BN = BN_;
+  static constexpr int WAVES_M = WM_, WAVES_N = WN_;
+  static constexpr int NWAVES = WM_ * WN_;
+  static constexpr int THREADS = 64 * NWAVES;
+  static constexpr int WM = BM / WM_, WN = BN / WN_;  // wave tile
+  static constexpr int MI = WM / 16, NJ = WN / 16;
+  static constexpr int A_BYTES = BM * RBK * 2, B_BYTES = BN * RBK * 2;
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int A_PIECES = A_BYTES / 1024 / NWAVES;  // per wave per tile
+  static constexpr int B_PIECES = B_BYTES / 1024 / NWAVES;
+  static constexpr int DPT = A_PIECES + B_PIECES;            // DMA instructions per thread per tile
+  static constexpr int EPI_BYTES = WM * BN * 4;
+  static constexpr int LDS = STAGES * STAGE > EPI_BYTES ? STAGES * STAGE : EPI_BYTES;
+  static_assert(A_BYTES % (1024 * NWAVES) == 0 && B_BYTES % (1024 * NWAVES) == 0, "piece split");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+// wait until at most `tiles` tiles' DMA (DPT instructions each) are still outstanding
+template <class Cfg>
+__device__ __forceinline__ void wait_tiles(int tiles) {
+  constexpr int D = Cfg::DPT;
+  switch (tiles) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D) : "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * D) : "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * D) : "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * D) : "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * D) : "memory"); break;
+  }
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds_piece, int off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)((__attribute__((address_space(3))) char*)(uintptr_t)lds_piece),
+                                           16, off, 0, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <class Cfg, int AMODE, int EPI>
+__global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) {
+  constexpr int BM = Cfg::BM, BN = Cfg::BN;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid / Cfg::WAVES_N, wc = wid - wr * Cfg::WAVES_N;
+  const int nbn = (p.N + BN - 1) / BN, nbm = (p.M + BM - 1) / BM;
+  // XCD-contiguous tile ranges, then grouped ordering inside a range: GROUP_M row panels sweep
+  // the N axis together, so the A and W panels a k-slice needs are shared by ~GROUP_M tiles
+  // that run concurrently on one XCD (L2 hits instead of repeated MALL fetches).
+  const int wg = xcd_remap(blockIdx.x, nbn * nbm);
+  constexpr int GROUP_M = 8;
+  const int in_group = GROUP_M * nbn;
+  const int gid = wg / in_group, first_m = gid * GROUP_M;
+  const int gsize = min(nbm - first_m, GROUP_M);
+  const int bm = first_m + (wg - gid * in_group) % gsize;
+  const int bn = (wg - gid * in_group) / gsize;
+  const int m0 = bm * BM, n0 = bn * BN;
+
+  const auto ra1 = make_rsrc(p.A1, p.a1_bytes);
+  const auto ra2 = make_rsrc(p.A2 ? p.A2 : p.A1, p.A2 ? p.a2_bytes : 0u);
+  const auto rw = make_rsrc(p.Wt, p.w_bytes);
+
+  // piece q (of this wave) = tile rows 16*(q*NWAVES + wid) .. +15; lane -> row +(lane>>2), slot lane&3
+  const int prow = lane >> 2;
+  const int lchunk = (lane & 3) ^ gperm((lane >> 4) & 3);
+
+  int rowA[Cfg::A_PIECES], oyv[Cfg::A_PIECES], oxv[Cfg::A_PIECES];
+#pragma unroll
+  for (int q = 0; q < Cfg::A_PIECES; ++q) {
+    const int m = m0 + 16 * (q * Cfg::NWAVES + wid) + prow;
+    if (AMODE == 0) {
+      rowA[q] = m < p.M ? m : -1;
+      oyv[q] = oxv[q] = 0;
+    } else if (m < p.M) {
+      const int hw = p.OH * p.OW;
+      const int img = m / hw, rem = m - img * hw;
+      rowA[q] = img;
+      oyv[q] = rem / p.OW;
+      oxv[q] = rem - oyv[q] * p.OW;
+    } else {
+      rowA[q] = -1; oyv[q] = oxv[q] = 0;
+    }
+  }
+  int rowB[Cfg::B_PIECES];
+#pragma unroll
+  for (int q = 0; q < Cfg::B_PIECES; ++q) {
+    const int n = n0 + 16 * (q * Cfg::NWAVES + wid) + prow;
+    rowB[q] = n < p.N ? n : -1;
+  }
+  const int Ctot = p.C1 + p.C2;
+  const int nk_all = (p.K + RBK - 1) / RBK;
+  int kt0 = 0, kt1 = nk_all;
+  if (EPI == 2) {
+    kt0 = (int)((long long)nk_all * blockIdx.z / p.splits);
+    kt1 = (int)((long long)nk_all * (blockIdx.z + 1) / p.splits);
+  }
+  const int nk = kt1 - kt0;
+
+  // per-tile DMA plan: byte offsets of this thread's DPT pieces (B pieces first, then A) and
+  // which A source they read (wave-uniform per tile).  prep() is cheap VALU; the DMA
+  // instructions themselves are interleaved with the MFMA chain (dma_piece) so the matrix pipe
+  // never idles behind a burst of LDS-DMA issues.
+  int offs[Cfg::DPT];
+  bool a_second = false;
+  auto prep = [&](int kt) {
+    const int k0 = kt * RBK;
+    const int k = k0 + lchunk * 8;
+#pragma unroll
+    for (int q = 0; q < Cfg::B_PIECES; ++q)
+      offs[q] = (rowB[q] >= 0 && k < p.K) ? (rowB[q] * p.ldw + k) * 2 : kOOB;
+    if (AMODE == 0) {
+      a_second = k0 >= p.K1;
+      if (!a_second) {
+#pragma unroll
+        for (int q = 0; q < Cfg::A_PIECES; ++q)
+          offs[Cfg::B_PIECES + q] = (rowA[q] >= 0 && k < p.K1) ? (rowA[q] * p.lda1 + k) * 2 : kOOB;
+      } else {
+        const int kk = k - p.K1;
+#pragma unroll
+        for (int q = 0; q < Cfg::A_PIECES; ++q)
+          offs[Cfg::B_PIECES + q] = (rowA[q] >= 0 && k < p.K) ? (rowA[q] * p.lda2 + kk) * 2 : kOOB;
+      }
+    } else {
+      const int tap = k0 / Ctot;
+      const int ci0 = k0 - tap * Ctot;
+      const int ky = tap / 3, kx = tap - ky * 3;
+      a_second = ci0 >= p.C1;
+      const int cs = a_second ? p.C2 : p.C1;
+      const int ci = (a_second ? ci0 - p.C1 : ci0) + lchunk * 8;
+#pragma unroll
+      for (int q = 0; q < Cfg::A_PIECES; ++q) {
+        int iy, ix;
+        bool ok = rowA[q] >= 0 && tap < 9;
+        if (p.up) {
+          const int uy = oyv[q] + ky - 1, ux = oxv[q] + kx - 1;
+          ok = ok && uy >= 0 && uy < 2 * p.H && ux >= 0 && ux < 2 * p.W;
+          iy = uy >> 1; ix = ux >> 1;
+        } else {
+          iy = oyv[q] * p.stride + ky - 1; ix = oxv[q] * p.stride + kx - 1;
+          ok = ok && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+        }
+        offs[Cfg::B_PIECES + q] = ok ? (((rowA[q] * p.H + iy) * p.W + ix) * cs + ci) * 2 : kOOB;
+      }
+    }
+  };
+  auto dma_piece = [&](int stage, int idx) {  // idx: compile-time after unrolling
+    char* As = smem + stage * Cfg::STAGE;
+    if (idx < Cfg::B_PIECES) {
+      dma16(rw, As + Cfg::A_BYTES + (idx * Cfg::NWAVES + wid) * 1024, offs[idx]);
+    } else {
+      const int q = idx - Cfg::B_PIECES;
+      dma16(a_second ? ra2 : ra1, As + (q * Cfg::NWAVES + wid) * 1024, offs[idx]);
+    }
+  };
+  auto issue = [&](int kt, int stage) {
+    prep(kt);
+#pragma unroll
+    for (int d = 0; d < Cfg::DPT; ++d) dma_piece(stage, d);
+  };
+
+  f32x4 acc[Cfg::MI][Cfg::NJ];
+#pragma unroll
+  for (int i = 0; i < Cfg::MI; ++i)
+#pragma unroll
+    for (int j = 0; j < Cfg::NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  constexpr int S = Cfg::STAGES;
+  const int fr = lane & 15, fq = lane >> 4;
+  // ---- prologue: tiles 0..S-2 in flight, retire tile 0 ----
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nk) issue(kt0 + s, s);
+  wait_tiles<Cfg>(min(nk, S - 1) - 1);
+  __builtin_amdgcn_s_barrier();
+
+  const bool no_dma = p.ablate & 1, no_mfma = p.ablate & 2;
+  // fragments of the current k-tile live in registers: all MI + NJ ds_read_b128 are issued
+  // right after the barrier that publishes the stage, so the MFMA chain below runs back to
+  // back (the compiler's lgkmcnt ladder exposes only the first read's latency).
+  // Fragments are double-buffered in registers: iteration `it` publishes tile it+1 (counted
+  // vmcnt + barrier), refills the stage tile it-1 used, issues the ds_reads of tile it+1 into
+  // the spare register set, and only then runs tile it's MFMA chain — the LDS read latency of
+  // the next tile hides under the current MFMAs instead of opening a bubble after every barrier.
+  typedef bf16x8 FragA[Cfg::MI];
+  typedef bf16x8 FragB[Cfg::NJ];
+  FragA fa0, fa1;
+  FragB fb0, fb1;
+  auto load_into = [&](FragA& fa, FragB& fb, int stage) {
+    const char* As = smem + stage * Cfg::STAGE;
+    const char* Bs = As + Cfg::A_BYTES;
+#pragma unroll
+    for (int j = 0; j < Cfg::NJ; ++j)
+      fb[j] = *reinterpret_cast<const bf16x8*>(Bs + rswz(wc * Cfg::WN + j * 16 + fr, fq));
+#pragma unroll
+    for (int i = 0; i < Cfg::MI; ++i)
+      fa[i] = *reinterpret_cast<const bf16x8*>(As + rswz(wr * Cfg::WM + i * 16 + fr, fq));
+  };
+  int wrs = S - 1, nrd = 1 % S;  // next stage to fill / stage holding tile it+1
+  auto step = [&](int it, FragA& ca, FragB& cb, FragA& na, FragB& nb) {
+    if (it + 1 < nk) {
+      wait_tiles<Cfg>(no_dma ? 0 : min(nk - 1, it + S - 2) - (it + 1));
+      __builtin_amdgcn_s_barrier();
+    }
+    if (it + S - 1 < nk && !no_dma) issue(kt0 + it + S - 1, wrs);
+    wrs = wrs + 1 == S ? 0 : wrs + 1;
+    if (it + 1 < nk) load_into(na, nb, nrd);
+    nrd = nrd + 1 == S ? 0 : nrd + 1;
+    __builtin_amdgcn_s_setprio(1);
+    if (!no_mfma) {
+#pragma unroll
+      for (int i = 0; i < Cfg::MI; ++i)
+#pragma unroll
+        for (int j = 0; j < Cfg::NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ca[i], cb[j], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < Cfg::MI; ++i) asm volatile("" ::"v"(ca[i]));
+#pragma unroll
+      for (int j = 0; j < Cfg::NJ; ++j) asm volatile("" ::"v"(cb[j]));
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  if (nk > 0) load_into(fa0, fb0, 0);
+  for (int it = 0; it < nk; it += 2) {
+    step(it, fa0, fb0, fa1, fb1);
+    if (it + 1 < nk) step(it + 1, fa1, fb1, fa0, fb0);
+  }
+  __builtin_amdgcn_s_barrier();  // all waves done with the ring before the epilogue reuses LDS
+
+  // ---------------- epilogue: one wave-row group at a time through LDS ----------------
+  float* Cs = reinterpret_cast<float*>(smem);
+  const auto rr = make_rsrc(p.R ? p.R : p.Wt, p.R ? p.r_bytes : 0u);
+#pragma unroll 1
+  for (int round = 0; round < Cfg::WAVES_M; ++round) {
+    if (wr == round) {
+#pragma unroll
+      for (int i = 0; i < Cfg::MI; ++i)
+#pragma unroll
+        for (int j = 0; j < Cfg::NJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            Cs[(i * 16 + fq * 4 + r) * BN + wc * Cfg::WN + j * 16 + fr] = acc[i][j][r];
+    }
+    __syncthreads();
+    const int rbase = m0 + round * Cfg::WM;
+    if (EPI == 2) {
+      constexpr int CPR = BN / 8;
+      float* slab = p.ws + (size_t)blockIdx.z * p.M * p.N;
+      for (int idx = tid; idx < Cfg::WM * CPR; idx += Cfg::THREADS) {
+        const int row = idx / CPR, cc = idx - row * CPR;
+        const int m = rbase + row, n = n0 + cc * 8;
+        if (m >= p.M || n >= p.N) continue;
+        const f32x4 c0 = *reinterpret_cast<const f32x4*>(Cs + row * BN + cc * 8);
+        const f32x4 c1 = *reinterpret_cast<const f32x4*>(Cs + row * BN + cc * 8 + 4);
+        float* dst = slab + (size_t)m * p.N + n;
+        if (n + 8 <= p.N) {
+          *reinterpret_cast<f32x4*>(dst) = c0;
+          *reinterpret_cast<f32x4*>(dst + 4) = c1;
+        } else {
+          for (int e = 0; e < p.N - n; ++e) dst[e] = e < 4 ? c0[e] : c1[e - 4];
+        }
+      }
+    } else if (EPI == 0) {
+      constexpr int CPR = BN / 8;
+#pragma unroll 2
+      for (int idx = tid; idx < Cfg::WM * CPR; idx += Cfg::THREADS) {
+        const int row = idx / CPR, cc = idx - row * CPR;
+        const int m = rbase + row, n = n0 + cc * 8;
+        if (m >= p.M || n >= p.N) continue;
+        float v[8];
+        const f32x4 c0 = *reinterpret_cast<const f32x4*>(Cs + row * BN + cc * 8);
+        const f32x4 c1 = *reinterpret_cast<const f32x4*>(Cs + row * BN + cc * 8 + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { v[e] = c0[e]; v[e + 4] = c1[e]; }
+        const int nv = min(8, p.N - n);
+        if (p.bias) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) if (e < nv) v[e] += p.bias[n + e];
+        }
+        if (p.rbias) {
+          const float* rb = p.rbias + (size_t)(m / p.rbias_div) * p.ldrb + n;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) if (e < nv) v[e] += rb[e];
+        }
+        if (nv == 8) {
+          if (p.R) {
+            float r8[8];
+            unpack8(buf_load16(rr, (m * p.ldr + n) * 2), r8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += r8[e];
+          }
+          *reinterpret_cast<u32x4*>(p.C + (size_t)m * p.ldc + n) = pack8(v);
+        } else {
+          for (int e = 0; e < nv; ++e) {
+            float x = v[e];
+            if (p.R) x += bf2f(p.R[(size_t)m * p.ldr + n + e]);
+            p.C[(size_t)m * p.ldc + n + e] = f2bf(x);
+          }
+        }
+      }
+    } else {  // GEGLU: per 128 weight rows [64 hidden | 64 gate] -> 64 outputs
+      constexpr int CPR = BN / 16;
+#pragma unroll 2
+      for (int idx = tid; idx < Cfg::WM * CPR; idx += Cfg::THREADS) {
+        const int row = idx / CPR, oc = idx - row * CPR;
+        const int blk = oc >> 3, c = (oc & 7) * 8;
+        const int m = rbase + row;
+        const int nh = n0 + blk * 128 + c;
+        if (m >= p.M || nh >= p.N) continue;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float h = Cs[row * BN + blk * 128 + c + e];
+          float g = Cs[row * BN + blk * 128 + 64 + c + e];
+          if (p.bias) { h += p.bias[nh + e]; g += p.bias[nh + 64 + e]; }
+          v[e] = h * gelu_erf(g);
+        }
+        *reinterpret_cast<u32x4*>(p.C + (size_t)m * p.ldc + (n0 >> 1) + blk * 64 + c) = pack8(v);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// stages: as many as the LDS budget allows at the intended residency (lookahead S-2 tiles)
+using Cfg256x256 = RingCfg<256, 256, 2, 4, 5>;  // 160 KiB, 1 WG/CU
+using Cfg256x128 = RingCfg<256, 128, 4, 2, 6>;  // 144 KiB, 1 WG/CU
+using Cfg128x128 = RingCfg<128, 128, 2, 2, 5>;  //  80 KiB, 2 WG/CU
+using Cfg128x64 = RingCfg<128, 64, 2, 2, 6>;    //  72 KiB, 2 WG/CU
+
+template <class Cfg, int AMODE, int EPI>
+static int launch_ring_t(const GemmArgs& a, hipStream_t s, int splits) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_ring_kernel<Cfg, AMODE, EPI>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS);
+    attr = true;
+  }
+  const int nwg = ((a.M + Cfg::BM - 1) / Cfg::BM) * ((a.N + Cfg::BN - 1) / Cfg::BN);
+  hipLaunchKernelGGL((gemm_ring_kernel<Cfg, AMODE, EPI>), dim3(nwg, 1, splits), dim3(Cfg::THREADS), Cfg::LDS, s, a);
+  return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+}
+
+template <class Cfg>
+static int dispatch_cfg(const GemmArgs& a, int amode, int epi, hipStream_t s, int splits) {
+  if (amode == 0) {
+    if (epi == 0) return launch_ring_t<Cfg, 0, 0>(a, s, splits);
+    if (epi == 1) return launch_ring_t<Cfg, 0, 1>(a, s, splits);
+    return launch_ring_t<Cfg, 0, 2>(a, s, splits);
+  }
+  if (epi == 0) return launch_ring_t<Cfg, 1, 0>(a, s, splits);
+  if (epi == 2) return launch_ring_t<Cfg, 1, 2>(a, s, splits);
+  return VST_ERR_ARG;
+}
+
+// tile: 1 = 128x128, 2 = 128x64, 3 = 256x256, 4 = 256x128.  epi: 0 plain, 1 GEGLU, 2 split-K partial
+int launch_gemm_ring(const GemmArgs& a, int amode, int epi, int tile, int splits, hipStream_t s) {
+  switch (tile) {
+    case 1: return dispatch_cfg<Cfg128x128>(a, amode, epi, s, splits);
+    case 2: return epi == 1 ? VST_ERR_ARG : dispatch_cfg<Cfg128x64>(a, amode, epi, s, splits);
+    case 3: return dispatch_cfg<Cfg256x256>(a, amode, epi, s, splits);
+    case 4: return dispatch_cfg<Cfg256x128>(a, amode, epi, s, splits);
+    default: return VST_ERR_ARG;
+  }
+}
+
+}  // namespace vst

@@ -1,0 +1,28 @@
+// Shared GEMM argument block and LDS swizzle (gemm.hip, gemm_big.hip).
+#pragma once
+#include "vst_common.h"
+
+namespace vst {
+
+struct GemmArgs {
+  const bf16_t* A1; const bf16_t* A2;
+  int lda1, lda2, K1;
+  // conv geometry (AMODE 1/2): input NHWC [nimg, H, W, C1 (+C2)] -> output [nimg, OH, OW, N]
+  int H, W, C1, C2, OH, OW, stride, up;
+  const bf16_t* Wt; int ldw;
+  int M, N, K;
+  const float* bias;
+  const float* rbias; int rbias_div, ldrb;
+  const bf16_t* R; int ldr;
+  bf16_t* C; int ldc;
+  float* ws;  // split-K slabs [splits][M][N] fp32
+  int splits;
+  int ablate;  // diagnostics only (VST_GEMM_ABLATE): bit0 skip loop DMA, bit1 skip MFMA
+  uint32_t a1_bytes, a2_bytes, w_bytes, r_bytes;
+};
+
+__device__ __forceinline__ int swz(int row, int chunk) {
+  return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
+}
+
+}  // namespace vst

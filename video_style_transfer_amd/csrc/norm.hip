@@ -76,52 +76,62 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const bf16_t* __restrict_
   }
 }
 
-// merge chunk partials -> mean, rstd per (sample, group)
-__global__ void gn_finalize_kernel(const float* __restrict__ part, int nchunk, int rows_per_sample, int groups,
-                                   int Cg, float eps, float* __restrict__ stats, int nsamples) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= nsamples * groups) return;
-  const int s = idx / groups, gi = idx - s * groups;
-  double n = 0.0, mean = 0.0, m2 = 0.0;
-  for (int c = 0; c < nchunk; ++c) {
+// one 64-thread block per (sample, group): merge the chunk partials (sum, sumsq) in double, then
+// emit the per-channel affine  y = x * scale[s,c] + shift[s,c]  (scale = rstd*gamma,
+// shift = beta - mean*rstd*gamma) so the apply pass is one FMA per element.
+__global__ __launch_bounds__(64) void gn_finalize_kernel(const float* __restrict__ part, int nchunk,
+                                                         int rows_per_sample, int groups, int Cg, float eps,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float* __restrict__ scale,
+                                                         float* __restrict__ shift, int C) {
+  const int s = blockIdx.x / groups, gi = blockIdx.x - s * groups;
+  const int lane = threadIdx.x;
+  double a = 0.0, q = 0.0;
+  for (int c = lane; c < nchunk; c += 64) {
     const float* p = part + (((size_t)s * nchunk + c) * groups + gi) * 2;
-    const int rows = min(GN_ROWS, rows_per_sample - c * GN_ROWS);
-    const double nb = (double)rows * Cg;
-    const double mb = p[0] / nb;
-    const double m2b = fmax((double)p[1] - (double)p[0] * mb, 0.0);
-    const double nn = n + nb;
-    const double d = mb - mean;
-    mean += d * nb / nn;
-    m2 += m2b + d * d * n * nb / nn;
-    n = nn;
+    a += p[0];
+    q += p[1];
   }
-  const double var = m2 / n;
-  stats[idx * 2] = (float)mean;
-  stats[idx * 2 + 1] = (float)(1.0 / sqrt(var + (double)eps));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o);
+    q += __shfl_xor(q, o);
+  }
+  const double n = (double)rows_per_sample * Cg;
+  const double mean = a / n;
+  const double var = fmax(q / n - mean * mean, 0.0);
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  for (int c = gi * Cg + lane; c < (gi + 1) * Cg; c += 64) {
+    const float sc = rstd * gamma[c];
+    scale[(size_t)s * C + c] = sc;
+    shift[(size_t)s * C + c] = beta[c] - (float)mean * sc;
+  }
 }
 
 __global__ __launch_bounds__(256) void gn_apply_kernel(const bf16_t* __restrict__ x1, int ld1, int C1,
                                                        const bf16_t* __restrict__ x2, int ld2, int C2,
-                                                       int rows_per_sample, int groups, const float* __restrict__ stats,
-                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                       int act, bf16_t* __restrict__ y, int ldy, size_t total_chunks) {
+                                                       int rows_per_sample, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, int act,
+                                                       bf16_t* __restrict__ y, int ldy, size_t total_chunks) {
   const int C = C1 + C2;
   const int CH = C / 8;
-  const int Cg = C / groups;
   for (size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x; idx < total_chunks; idx += (size_t)gridDim.x * 256) {
     const size_t row = idx / CH;
     const int c = (int)(idx - row * CH) * 8;
     const int s = (int)(row / rows_per_sample);
     float f[8];
     unpack8(*reinterpret_cast<const u32x4*>(chan_ptr(x1, ld1, C1, x2, ld2, row, c)), f);
+    const f32x4* sc = reinterpret_cast<const f32x4*>(scale + (size_t)s * C + c);
+    const f32x4* sh = reinterpret_cast<const f32x4*>(shift + (size_t)s * C + c);
+    const f32x4 a0 = sc[0], a1 = sc[1], b0 = sh[0], b1 = sh[1];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int ch = c + e;
-      const int gi = ch / Cg;
-      const float mean = stats[(s * groups + gi) * 2], rstd = stats[(s * groups + gi) * 2 + 1];
-      float v = (f[e] - mean) * rstd * gamma[ch] + beta[ch];
-      if (act) v = silu(v);
-      f[e] = v;
+    for (int e = 0; e < 4; ++e) {
+      f[e] = f[e] * a0[e] + b0[e];
+      f[e + 4] = f[e + 4] * a1[e] + b1[e];
+    }
+    if (act) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = silu(f[e]);
     }
     *reinterpret_cast<u32x4*>(y + row * ldy + c) = pack8(f);
   }
@@ -164,14 +174,21 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const bf16_t* __restrict
   for (int i = 0; i < MAXCH; ++i) {
     const int cc = lane + 64 * i;
     if (cc < CH) {
+      const f32x4* g4 = reinterpret_cast<const f32x4*>(gamma + cc * 8);
+      const f32x4* b4 = reinterpret_cast<const f32x4*>(beta + cc * 8);
+      float gg[8], bb[8];
+      const f32x4 g0 = g4[0], g1 = g4[1], b0 = b4[0], b1 = b4[1];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { gg[e] = g0[e]; gg[e + 4] = g1[e]; bb[e] = b0[e]; bb[e + 4] = b1[e]; }
+      if (pr) {
+        const f32x4* p4 = reinterpret_cast<const f32x4*>(pr + cc * 8);
+        const f32x4 p0 = p4[0], p1 = p4[1];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { bb[e] += p0[e]; bb[e + 4] += p1[e]; }
+      }
       float o[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int c = cc * 8 + e;
-        float t = (v[i][e] - mean) * rstd * gamma[c] + beta[c];
-        if (pr) t += pr[c];
-        o[e] = t;
-      }
+      for (int e = 0; e < 8; ++e) o[e] = (v[i][e] - mean) * (rstd * gg[e]) + bb[e];
       *reinterpret_cast<u32x4*>(y + (size_t)row * ldy + cc * 8) = pack8(o);
     }
   }
@@ -181,9 +198,13 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const bf16_t* __restrict
 
 using namespace vst;
 
-extern "C" size_t vst_groupnorm_workspace_bytes(int nsamples, int rows_per_sample, int groups) {
+static inline size_t gn_part_floats(int nsamples, int rows_per_sample, int groups) {
   const int nchunk = (rows_per_sample + GN_ROWS - 1) / GN_ROWS;
-  return ((size_t)nsamples * nchunk * groups * 2 + (size_t)nsamples * groups * 2) * sizeof(float);
+  return ((size_t)nsamples * nchunk * groups * 2 + 3) & ~(size_t)3;  // keep scale/shift 16-B aligned
+}
+
+extern "C" size_t vst_groupnorm_workspace_bytes(int nsamples, int rows_per_sample, int groups, int C) {
+  return (gn_part_floats(nsamples, rows_per_sample, groups) + (size_t)2 * nsamples * C) * sizeof(float);
 }
 
 extern "C" int vst_groupnorm(const void* x1, int ld1, int C1, const void* x2, int ld2, int C2, int nsamples,
@@ -198,20 +219,20 @@ extern "C" int vst_groupnorm(const void* x1, int ld1, int C1, const void* x2, in
   hipStream_t s = (hipStream_t)stream;
   const int nchunk = (rows_per_sample + GN_ROWS - 1) / GN_ROWS;
   float* part = (float*)workspace;
-  float* stats = part + (size_t)nsamples * nchunk * groups * 2;
+  float* scale = part + gn_part_floats(nsamples, rows_per_sample, groups);
+  float* shift = scale + (size_t)nsamples * C;
   const int CH = C / 8;
   const int rps = CH >= 256 ? 1 : 256 / CH;
   const size_t lds = (size_t)2 * rps * C * sizeof(float);
   if (lds > 64 * 1024) return VST_ERR_ARG;
   hipLaunchKernelGGL(gn_stats_kernel, dim3(nchunk, nsamples), dim3(256), lds, s, (const bf16_t*)x1, ld1, C1,
                      (const bf16_t*)x2, ld2, C2, rows_per_sample, groups, part);
-  const int ng = nsamples * groups;
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3((ng + 255) / 256), dim3(256), 0, s, part, nchunk, rows_per_sample,
-                     groups, C / groups, eps, stats, nsamples);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(nsamples * groups), dim3(64), 0, s, part, nchunk, rows_per_sample,
+                     groups, C / groups, eps, gamma, beta, scale, shift, C);
   const size_t total = (size_t)nsamples * rows_per_sample * CH;
-  const int grid = (int)std::min<size_t>((total + 255) / 256, 8192);
+  const int grid = (int)std::min<size_t>((total + 255) / 256, 16384);
   hipLaunchKernelGGL(gn_apply_kernel, dim3(grid), dim3(256), 0, s, (const bf16_t*)x1, ld1, C1, (const bf16_t*)x2,
-                     ld2, C2, rows_per_sample, groups, stats, gamma, beta, silu_act, (bf16_t*)y, ldy, total);
+                     ld2, C2, rows_per_sample, scale, shift, silu_act, (bf16_t*)y, ldy, total);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 

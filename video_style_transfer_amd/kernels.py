@@ -55,6 +55,20 @@ class _Rec:
             _PROF.append((self.kind, self.flops, self.nbytes, self.s, e))
 
 
+GEMM_POLICY = {"tile": 0, "splits": 0}  # 0 = library heuristic (tuning / tests may force)
+_WS = {}
+_WS_BYTES = 64 << 20
+
+
+def _workspace(device):
+    """Per-device fp32 split-K slab workspace (allocated once, reused stream-ordered)."""
+    ws = _WS.get(device)
+    if ws is None:
+        ws = torch.empty(_WS_BYTES // 4, dtype=F32, device=device)
+        _WS[device] = ws
+    return ws
+
+
 def _dev(t: torch.Tensor, dtype, name):
     if not t.is_cuda:
         raise _lib.VstError(f"{name}: tensor is on {t.device}; the HIP path has no CPU fallback")
@@ -108,9 +122,11 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
     kind = kind or ("gemm_geglu" if geglu else ("gemm_lora" if x2 is not None and alg_k2 is not None else "gemm"))
     n_alg = N if alg_n is None else alg_n
     with _Rec(kind, 2.0 * M * n_alg * k_alg, 2.0 * (M * k_alg + N * k_alg + M * n_out * (2 if residual is not None else 1))):
-        _lib.call("vst_gemm", _p(x), _ld(x), _p(x2), 0 if x2 is None else _ld(x2), K1, _p(w), _ld(w), M, N, K,
+        ws = _workspace(x.device)
+        _lib.call("vst_gemm_ex", _p(x), _ld(x), _p(x2), 0 if x2 is None else _ld(x2), K1, _p(w), _ld(w), M, N, K,
                   _p(bias), _p(row_bias), row_bias_div, N if row_bias is not None else 0, _p(residual),
-                  0 if residual is None else _ld(residual), _p(out), _ld(out), 1 if geglu else 0, _stream())
+                  0 if residual is None else _ld(residual), _p(out), _ld(out), 1 if geglu else 0,
+                  GEMM_POLICY["tile"], GEMM_POLICY["splits"], _p(ws), _WS_BYTES, _stream())
     return out
 
 
@@ -149,9 +165,11 @@ def conv3x3(x1: torch.Tensor, nimg: int, H: int, W: int, w: torch.Tensor, bias: 
         _dev(residual, BF16, "residual")
     kind = "conv3x3" if (C1 + C2) % 64 == 0 else "conv3x3_small_cin"
     with _Rec(kind, 2.0 * M * Cout * kreal, 2.0 * (nimg * H * W * (C1 + C2) + Cout * kreal + M * Cout)):
-        _lib.call("vst_conv3x3", _p(x1), C1, _p(x2), C2, nimg, H, W, stride, 1 if upsample else 0, _p(w), Cout,
+        ws = _workspace(x1.device)
+        _lib.call("vst_conv3x3_ex", _p(x1), C1, _p(x2), C2, nimg, H, W, stride, 1 if upsample else 0, _p(w), Cout,
                   _p(bias), _p(row_bias), row_bias_div, _p(residual), 0 if residual is None else _ld(residual),
-                  _p(out), _ld(out) if Cout >= 8 else Cout, _stream())
+                  _p(out), _ld(out) if Cout >= 8 else Cout, GEMM_POLICY["tile"], GEMM_POLICY["splits"], _p(ws),
+                  _WS_BYTES, _stream())
     return out
 
 
@@ -201,7 +219,7 @@ def group_norm(x1, nsamples, rows_per_sample, groups, eps, gamma, beta, *, silu=
         raise _lib.VstError("group_norm: rows != nsamples*rows_per_sample")
     if out is None:
         out = torch.empty((x1.shape[0], C), dtype=BF16, device=x1.device)
-    ws_bytes = _lib.load().vst_groupnorm_workspace_bytes(nsamples, rows_per_sample, groups)
+    ws_bytes = _lib.load().vst_groupnorm_workspace_bytes(nsamples, rows_per_sample, groups, C)
     ws = torch.empty((ws_bytes + 3) // 4, dtype=F32, device=x1.device)
     with _Rec("groupnorm", 0.0, 2.0 * 3 * x1.shape[0] * C):  # two reads + one write
         _lib.call("vst_groupnorm", _p(x1), _ld(x1), x1.shape[1], _p(x2), 0 if x2 is None else _ld(x2),
