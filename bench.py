@@ -27,13 +27,7 @@ sys.path.insert(0, ROOT)
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table; no sparsity)
 PEAK_HBM_GBS = 8000.0
 
-KERNEL_OF_KIND = {
-    "gemm": "gemm_kernel<0,0> (dense projection)",
-    "gemm_lora": "gemm_kernel<0,0> (dense projection)",
-    "gemm_lora_down": "gemm_kernel<0,0> (dense projection)",
-    "gemm_geglu": "gemm_kernel<0,1> (GEGLU FF)",
-    "conv3x3": "gemm_kernel<1,0> (implicit-GEMM conv3x3)",
-    "conv3x3_small_cin": "gemm_kernel<2,0> (conv_in)",
+KERNEL_OF_KIND = {  # non-GEMM kinds; GEMM/conv launches carry the library's own kernel name
     "spatial_attention": "spatial_attn_kernel",
     "temporal_attention": "temporal_attn_kernel",
     "groupnorm": "gn_stats/gn_finalize/gn_apply",
@@ -71,8 +65,8 @@ def roofline(den):
     K.profile_launches(False)
     den.step_idx.zero_()
     by = {}
-    for kind, fl, nb, ms in rec:
-        sym = KERNEL_OF_KIND.get(kind, kind)
+    for kind, sym, fl, nb, ms in rec:
+        sym = sym or KERNEL_OF_KIND.get(kind, kind)
         d = by.setdefault(sym, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
         d["launches"] += 1
         d["ms"] += ms

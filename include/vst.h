@@ -29,13 +29,18 @@ extern "C" {
 int vst_gemm(const void* A, int lda, const void* A2, int lda2, int K1, const void* W, int ldw, int M, int N, int K,
              const float* bias, const float* row_bias, int row_bias_div, int ld_row_bias, const void* R, int ldr,
              void* C, int ldc, int epilogue, void* stream);
-/* Same, with the tile (0 auto, 1 = 128x128, 2 = 128x64) and split-K (0 auto, >= 1 forced) choice and a
+/* Same, with the tile (0 auto, 1 = 128x128, 2 = 128x64, 3 = 256x256, 4 = 256x128) and split-K (0 auto, >= 1 forced) choice and a
  * caller-owned fp32 workspace for split-K slabs (NULL / too small disables split-K). */
 int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int K1, const void* W, int ldw, int M, int N, int K,
                 const float* bias, const float* row_bias, int row_bias_div, int ld_row_bias, const void* R, int ldr,
                 void* C, int ldc, int epilogue, int tile, int splits, void* workspace, size_t ws_bytes,
                 void* stream);
 size_t vst_gemm_workspace_bytes(int M, int N, int K);
+
+/* Diagnostics: short name of the kernel (tile shape, epilogue, split-K) that a vst_gemm_ex
+ * (kind 0 linear, 1 GEGLU) or vst_conv3x3_ex (kind 2, kind 3 = Cin not a multiple of 64) call with
+ * these sizes and policy would launch.  Used by bench.py to attribute per-launch timings. */
+const char* vst_gemm_kernel_name(int M, int N, int K, int kind, int tile, int splits, size_t ws_bytes);
 
 /* 3x3 conv, padding 1, NHWC, optional channel-concat second input, stride 1|2, fused nearest-2x
  * upsample; Wt = [Cout][3][3][C1+C2].  Replaces the per-frame torch conv2d calls of diffusers

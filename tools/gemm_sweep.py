@@ -62,7 +62,7 @@ def timeit(fn, iters=20):
 
 def main():
     dev = torch.device("cuda")
-    variants = [(0, 0), (1, 1), (2, 1), (3, 1), (4, 1), (2, 4), (2, 8)]
+    variants = [(0, 0), (1, 1), (2, 1), (3, 1), (4, 1), (1, 2), (1, 4), (3, 2), (3, 4)]
     res = []
     for name, M, N, Kd, K2, geglu in SHAPES:
         x = torch.randn(M, Kd, device=dev).to(BF)

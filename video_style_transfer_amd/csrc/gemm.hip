@@ -382,7 +382,7 @@ constexpr int kCUs = 256;
 // tile / split choice.  tile: 0 auto, 1 = 128x128, 2 = 128x64.  splits: 0 auto, >=1 forced.
 // tile codes: 1 = 128x128, 2 = 128x64 (gemm_kernel, 4 waves, up to 2 WG/CU);
 //             3 = 256x256, 4 = 256x128 (gemm_big_kernel, 8 waves, LDS-DMA staging, 1 WG/CU)
-static void choose(int M, int N, int K, int geglu, size_t ws_bytes, int& tile, int& splits) {
+static void choose(int M, int N, int K, int geglu, int conv, size_t ws_bytes, int& tile, int& splits) {
   const int mt = (M + BM - 1) / BM;
   const int t128 = mt * ((N + 127) / 128);
   const int t64 = mt * ((N + 63) / 64);
@@ -390,14 +390,15 @@ static void choose(int M, int N, int K, int geglu, size_t ws_bytes, int& tile, i
   const int mb = (M + 255) / 256;
   const int t256 = mb * ((N + 255) / 256), t256n = mb * ((N + 127) / 128);
   const double waste256 = 1.0 - (double)N / (((N + 255) / 256) * 256);
-  const double waste128 = 1.0 - (double)N / (((N + 127) / 128) * 128);
   const int nk32 = (K + 31) / 32;  // ring kernel k-tiles
-  (void)nk;
+  // Tile policy from tools/gemm_sweep.py on MI355X (UNet shapes at 16x512^2, CFG batch 2):
+  // implicit-GEMM convs (K = 9*Cin >= 2880) run best on 256x256; linears only when K is long
+  // and N fills 256-wide tiles; short-K linears (K=320) want the extra parallelism of 128x64.
   if (tile == 0) {
-    if (t256 >= 2 * kCUs && waste256 <= 0.1) tile = 3;
-    else if (t256n >= 2 * kCUs && waste128 <= 0.1) tile = 4;
-    else if (t128 >= kCUs && waste128 <= 0.1) tile = 1;
-    else tile = geglu ? 1 : 2;
+    if (conv && t256 >= kCUs / 2) tile = 3;
+    else if (!conv && K >= 1280 && waste256 <= 0.1 && t256 >= kCUs / 2) tile = 3;
+    else if (!geglu && (N <= 64 || K <= 320)) tile = 2;
+    else tile = 1;
   }
   if (geglu && tile == 2) tile = 1;
   const int tiles = tile == 1 ? t128 : tile == 2 ? t64 : tile == 3 ? t256 : t256n;
@@ -452,8 +453,26 @@ using namespace vst;
 
 extern "C" size_t vst_gemm_workspace_bytes(int M, int N, int K) {
   int tile = 0, splits = 0;
-  choose(M, N, K, 0, (size_t)-1, tile, splits);
+  choose(M, N, K, 0, 0, (size_t)-1, tile, splits);
   return splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
+}
+
+// Name of the kernel a vst_gemm_ex / vst_conv3x3_ex call with these arguments launches (the
+// symbol rocprofv3 reports), so per-launch timings can be attributed to kernels.  kind: 0 linear,
+// 1 GEGLU linear, 2 vectorized conv, 3 scalar-gather conv.  Returns a static string.
+extern "C" const char* vst_gemm_kernel_name(int M, int N, int K, int kind, int tile, int splits, size_t ws_bytes) {
+  static const char* names[4][3] = {
+      {"gemm_ring<128x128>", "gemm_ring<128x128,geglu>", "gemm_ring<128x128,conv>"},
+      {"gemm_ring<128x64>", "gemm_ring<128x64,geglu>", "gemm_ring<128x64,conv>"},
+      {"gemm_ring<256x256>", "gemm_ring<256x256,geglu>", "gemm_ring<256x256,conv>"},
+      {"gemm_ring<256x128>", "gemm_ring<256x128,geglu>", "gemm_ring<256x128,conv>"}};
+  static const char* split_names[4] = {"gemm_ring<128x128,splitk>", "gemm_ring<128x64,splitk>",
+                                       "gemm_ring<256x256,splitk>", "gemm_ring<256x128,splitk>"};
+  if (kind == 3) return "gemm_kernel<conv_in>";
+  if (kind < 0 || kind > 3 || tile < 0 || tile > 4 || splits < 0) return "";
+  choose(M, N, K, kind == 1, kind == 2, ws_bytes, tile, splits);
+  if (splits > 1) return split_names[tile - 1];
+  return names[tile - 1][kind == 2 ? 2 : kind];
 }
 
 extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int K1, const void* W, int ldw, int M,
@@ -482,7 +501,7 @@ extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int
   a.w_bytes = clamp_bytes(((size_t)(N - 1) * ldw + K) * 2);
   a.r_bytes = R ? clamp_bytes(((size_t)(M - 1) * ldr + N) * 2) : 0;
   a.C1 = 0; a.C2 = 0; a.stride = 1; a.up = 0;
-  choose(M, N, K, epilogue == 1, workspace ? ws_bytes : 0, tile, splits);
+  choose(M, N, K, epilogue == 1, 0, workspace ? ws_bytes : 0, tile, splits);
   return run_gemm(a, 0, epilogue == 1, tile, splits, (hipStream_t)stream);
 }
 
@@ -525,7 +544,7 @@ extern "C" int vst_conv3x3_ex(const void* x1, int C1, const void* x2, int C2, in
   a.r_bytes = R ? clamp_bytes(((size_t)(a.M - 1) * ldr + Cout) * 2) : 0;
   if ((ldc & 7) && Cout >= 8) return VST_ERR_ARG;
   if (!vec) { tile = 2; splits = 1; }
-  choose(a.M, a.N, a.K, 0, workspace ? ws_bytes : 0, tile, splits);
+  choose(a.M, a.N, a.K, 0, 1, workspace ? ws_bytes : 0, tile, splits);
   return run_gemm(a, vec ? 1 : 2, 0, tile, splits, (hipStream_t)stream);
 }
 

@@ -20,7 +20,7 @@ def _stream():
 
 
 # ---- launch profiler (bench.py roofline): HIP events around every launch of an instrumented op
-_PROF = None  # list of (kind, flops, bytes, ev_start, ev_end) while active
+_PROF = None  # list of (kind, symbol, flops, bytes, ev_start, ev_end) while active
 
 
 def profile_launches(active: bool):
@@ -29,18 +29,20 @@ def profile_launches(active: bool):
 
 
 def collect_launches():
-    """[(kind, flops, bytes, ms)] for the launches recorded since profile_launches(True)."""
+    """[(kind, kernel symbol or None, flops, bytes, ms)] for the launches recorded since
+    profile_launches(True)."""
     torch.cuda.synchronize()
-    out = [(k, f, b, s.elapsed_time(e)) for k, f, b, s, e in (_PROF or [])]
+    out = [(k, y, f, b, s.elapsed_time(e)) for k, y, f, b, s, e in (_PROF or [])]
     return out
 
 
 class _Rec:
-    __slots__ = ("kind", "flops", "nbytes", "s")
+    __slots__ = ("kind", "flops", "nbytes", "s", "sym")
 
-    def __init__(self, kind, flops, nbytes):
+    def __init__(self, kind, flops, nbytes, sym=None):
         self.kind, self.flops, self.nbytes = kind, flops, nbytes
         self.s = None
+        self.sym = sym  # callable -> kernel symbol (evaluated only while profiling)
 
     def __enter__(self):
         if _PROF is not None:
@@ -52,10 +54,17 @@ class _Rec:
         if _PROF is not None and self.s is not None:
             e = torch.cuda.Event(enable_timing=True)
             e.record()
-            _PROF.append((self.kind, self.flops, self.nbytes, self.s, e))
+            _PROF.append((self.kind, self.sym() if self.sym else None, self.flops, self.nbytes, self.s, e))
 
 
 GEMM_POLICY = {"tile": 0, "splits": 0}  # 0 = library heuristic (tuning / tests may force)
+
+
+def gemm_kernel_name(M, N, K, kind):
+    """Kernel the library launches for a GEMM / conv of this size (kind: 0 linear, 1 GEGLU, 2 conv,
+    3 scalar-gather conv) under the current GEMM_POLICY."""
+    name = _lib.load().vst_gemm_kernel_name(M, N, K, kind, GEMM_POLICY["tile"], GEMM_POLICY["splits"], _WS_BYTES)
+    return name.decode() if name else None
 _WS = {}
 _WS_BYTES = 64 << 20
 
@@ -121,7 +130,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
     k_alg = K1 + (0 if x2 is None else (x2.shape[1] if alg_k2 is None else alg_k2))
     kind = kind or ("gemm_geglu" if geglu else ("gemm_lora" if x2 is not None and alg_k2 is not None else "gemm"))
     n_alg = N if alg_n is None else alg_n
-    with _Rec(kind, 2.0 * M * n_alg * k_alg, 2.0 * (M * k_alg + N * k_alg + M * n_out * (2 if residual is not None else 1))):
+    with _Rec(kind, 2.0 * M * n_alg * k_alg, 2.0 * (M * k_alg + N * k_alg + M * n_out * (2 if residual is not None else 1)),
+              lambda: gemm_kernel_name(M, N, K, 1 if geglu else 0)):
         ws = _workspace(x.device)
         _lib.call("vst_gemm_ex", _p(x), _ld(x), _p(x2), 0 if x2 is None else _ld(x2), K1, _p(w), _ld(w), M, N, K,
                   _p(bias), _p(row_bias), row_bias_div, N if row_bias is not None else 0, _p(residual),
@@ -164,7 +174,8 @@ def conv3x3(x1: torch.Tensor, nimg: int, H: int, W: int, w: torch.Tensor, bias: 
     if residual is not None:
         _dev(residual, BF16, "residual")
     kind = "conv3x3" if (C1 + C2) % 64 == 0 else "conv3x3_small_cin"
-    with _Rec(kind, 2.0 * M * Cout * kreal, 2.0 * (nimg * H * W * (C1 + C2) + Cout * kreal + M * Cout)):
+    with _Rec(kind, 2.0 * M * Cout * kreal, 2.0 * (nimg * H * W * (C1 + C2) + Cout * kreal + M * Cout),
+              lambda: gemm_kernel_name(M, Cout, w.shape[1], 2 if kind == "conv3x3" else 3)):
         ws = _workspace(x1.device)
         _lib.call("vst_conv3x3_ex", _p(x1), C1, _p(x2), C2, nimg, H, W, stride, 1 if upsample else 0, _p(w), Cout,
                   _p(bias), _p(row_bias), row_bias_div, _p(residual), 0 if residual is None else _ld(residual),
