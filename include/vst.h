@@ -71,9 +71,28 @@ int vst_groupnorm(const void* x1, int ld1, int C1, const void* x2, int ld2, int 
                   int rows_per_sample, int groups, float eps, const float* gamma, const float* beta, int silu_act,
                   void* y, int ldy, void* workspace, void* stream);
 
+/* Frame-sharded motion-module GroupNorm (diffusers AnimateDiffTransformer3D norm: statistics over
+ * every frame of a clip, inference_animatediff.py:213-214 keeps it on the motion path).  When a
+ * clip's frames are spread over ranks, each rank computes per-(sample, group) double (sum, sumsq)
+ * over its rows, the host all-reduces them (RCCL), and every rank normalises its own rows with the
+ * clip-wide statistics; `count` = elements per (sample, group) over the whole clip. */
+int vst_groupnorm_sums(const void* x1, int ld1, int C1, const void* x2, int ld2, int C2, int nsamples,
+                       int rows_per_sample, int groups, double* sums, void* workspace, void* stream);
+int vst_groupnorm_apply_sums(const void* x1, int ld1, int C1, const void* x2, int ld2, int C2, int nsamples,
+                             int rows_per_sample, int groups, const double* sums, double count, float eps,
+                             const float* gamma, const float* beta, int silu_act, void* y, int ldy, void* workspace,
+                             void* stream);
+
 /* LayerNorm over C (+ sinusoidal PE row pe[(row/pe_div)%pe_mod], temporal_transformer.py:6-27). */
 int vst_layernorm(const void* x, int ldx, int C, int rows, const float* gamma, const float* beta, float eps,
                   const float* pe, int pe_div, int pe_mod, void* y, int ldy, void* stream);
+
+/* Row-block permutation: rows of C bf16 indexed (i0,i1,i2,i3) over dims (d0..d3) in src; dst
+ * axis k is src axis p_k.  Used for the frame-shard <-> pixel-shard exchange around the motion
+ * module's frame-axis attention (the reference's (B*F,HW,C) <-> (B*HW,F,C) permutes of
+ * AnimateDiffTransformer3D, here across ranks). */
+int vst_permute_rows(const void* src, void* dst, int C, int d0, int d1, int d2, int d3, int p0, int p1, int p2,
+                     int p3, void* stream);
 
 /* Denoise-loop glue (inference_animatediff.py:104-131). */
 int vst_timestep_embedding(const float* t, const int* step_idx, int n, int dim, int flip_sin_to_cos,

@@ -1,0 +1,177 @@
+"""Frame sharding of a clip over ranks (video_style_transfer_amd/frame_shard.py).
+
+CPU (gloo, world size 2): the layout algebra of the frame <-> pixel shard exchange, and that the
+sharded motion module (all-reduced GroupNorm statistics + frame-axis work on pixel shards) equals the
+oracle's unsharded motion module (oracle/unet.py motion_module) on each rank's frames.
+
+GPU (gloo transport, 2 ranks on one GPU, HIP kernels): a frame-sharded tiny-UNet forward is as close
+to the fp32 oracle's whole-clip forward as the unsharded HIP forward is (both bf16).
+"""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def torch_permute_rows(src, dims, perm):
+    """Semantics of vst_permute_rows, restated in torch for CPU ranks."""
+    C = src.shape[1]
+    return src.view(*dims, C).permute(*perm, 4).reshape(-1, C).contiguous()
+
+
+def _init(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+# ------------------------------------------------------------------------------------- CPU
+def _cpu_worker(rank, world, port, q):
+    try:
+        sys.path.insert(0, ROOT)
+        _init(rank, world, port)
+        from oracle import unet as OU
+        from video_style_transfer_amd.frame_shard import FrameShard
+        sh = FrameShard(permute=torch_permute_rows)
+        torch.manual_seed(0)
+        B, F, H, W, C = 2, 4, 4, 6, 64
+        HW = H * W
+        X = torch.randn(B, F, HW, C)
+        Fl, f0 = sh.local_frames(F)
+        x_loc = X[:, f0:f0 + Fl].reshape(-1, C).contiguous()
+        # (a) frame shard -> pixel shard: rank r holds pixel slab r of every frame
+        hp = HW // world
+        px = sh.to_pixels(x_loc, B, Fl, HW)
+        ref = X[:, :, rank * hp:(rank + 1) * hp].reshape(-1, C)
+        assert torch.equal(px, ref), "to_pixels layout"
+        # (b) round trip
+        assert torch.equal(sh.to_frames(px, B, Fl, HW), x_loc), "to_frames(to_pixels(x)) != x"
+        # (c) sharded motion module == oracle motion module
+        P = {}
+        g = torch.Generator().manual_seed(1)
+        name = "mm"
+        P[name + ".norm.weight"] = 1 + 0.1 * torch.randn(C, generator=g)
+        P[name + ".norm.bias"] = 0.1 * torch.randn(C, generator=g)
+        for lin in ("proj_in", "proj_out"):
+            P[f"{name}.{lin}.weight"] = torch.randn(C, C, generator=g) / C ** 0.5
+            P[f"{name}.{lin}.bias"] = 0.1 * torch.randn(C, generator=g)
+        blk = name + ".transformer_blocks.0"
+        for a in ("attn1", "attn2"):
+            for pj in ("to_q", "to_k", "to_v"):
+                P[f"{blk}.{a}.{pj}.weight"] = torch.randn(C, C, generator=g) / C ** 0.5
+            P[f"{blk}.{a}.to_out.0.weight"] = torch.randn(C, C, generator=g) / C ** 0.5
+            P[f"{blk}.{a}.to_out.0.bias"] = 0.1 * torch.randn(C, generator=g)
+        for n in ("norm1", "norm2", "norm3"):
+            P[f"{blk}.{n}.weight"] = 1 + 0.1 * torch.randn(C, generator=g)
+            P[f"{blk}.{n}.bias"] = 0.1 * torch.randn(C, generator=g)
+        P[f"{blk}.ff.net.0.proj.weight"] = torch.randn(8 * C, C, generator=g) / C ** 0.5
+        P[f"{blk}.ff.net.0.proj.bias"] = 0.1 * torch.randn(8 * C, generator=g)
+        P[f"{blk}.ff.net.2.weight"] = torch.randn(C, 4 * C, generator=g) / (4 * C) ** 0.5
+        P[f"{blk}.ff.net.2.bias"] = 0.1 * torch.randn(C, generator=g)
+        from video_style_transfer_amd.weights import sinusoid_table
+        P[f"{blk}.pos_embed.pe"] = sinusoid_table(C, 32)
+        x_nchw = X.reshape(B * F, H, W, C).permute(0, 3, 1, 2).contiguous()
+        full = OU.motion_module(P, name, x_nchw, F)                       # (B*F, C, H, W)
+        full_tok = full.permute(0, 2, 3, 1).reshape(B, F, HW, C)[:, f0:f0 + Fl].reshape(-1, C)
+        # sharded: GN statistics all-reduced over ranks
+        G = 32
+        xs = x_loc.double().view(B, Fl * HW, G, C // G)
+        sums = torch.stack([xs.sum((1, 3)), (xs * xs).sum((1, 3))], -1).reshape(-1)
+        sh.all_reduce_(sums)
+        cnt = F * HW * (C // G)
+        mean = (sums.view(B, G, 2)[..., 0] / cnt)
+        var = sums.view(B, G, 2)[..., 1] / cnt - mean * mean
+        h = (xs - mean[:, None, :, None]) / torch.sqrt(var[:, None, :, None] + 1e-6)
+        h = h.float().reshape(B, Fl * HW, C) * P[name + ".norm.weight"] + P[name + ".norm.bias"]
+        h = OU.linear(P, name + ".proj_in", h.reshape(-1, C))
+        h = sh.to_pixels(h, B, Fl, HW)                                    # rows (b, f, p')
+        h = h.view(B, F, hp, C).permute(0, 2, 1, 3).reshape(B * hp, F, C)  # oracle layout (B*HW', F, C)
+        h = OU.basic_block(P, blk, h, None, 8, None, pe=P[f"{blk}.pos_embed.pe"])
+        h = h.view(B, hp, F, C).permute(0, 2, 1, 3).reshape(-1, C)
+        h = sh.to_frames(h, B, Fl, HW)
+        out = OU.linear(P, name + ".proj_out", h) + x_loc
+        err = ((out - full_tok).norm() / full_tok.norm()).item()
+        assert err < 1e-5, f"sharded motion module rel err {err}"
+        q.put((rank, "ok", err))
+    except BaseException as e:  # noqa: BLE001
+        q.put((rank, "fail", repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def _spawn(fn, world, *extra):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=fn, args=(r, world, port, q) + extra) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=600) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    return res
+
+
+def test_frame_shard_cpu_world2():
+    res = _spawn(_cpu_worker, 2)
+    for rank, status, info in res:
+        assert status == "ok", f"rank {rank}: {info}"
+
+
+# ------------------------------------------------------------------------------------- GPU
+def _gpu_worker(rank, world, port, q):
+    try:
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        _init(rank, world, port)
+        from oracle.unet import unet_forward
+        from test_parity_gpu import _setup
+        from video_style_transfer_amd.frame_shard import FrameShard
+        from video_style_transfer_amd.utils import build_unet
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        F = 8
+        cfg, sd, lat, enc, pooled, tids = _setup("tiny", F, 16)
+        t = torch.tensor([761.0, 761.0])
+        ref = unet_forward(sd, cfg.to_dict(), lat, t, enc, pooled, tids)        # fp32 oracle, whole clip
+        unet = build_unet(cfg, state_dict=sd, device=dev)
+        sh = FrameShard()
+        Fl, f0 = sh.local_frames(F)
+        kw = dict(added_cond_kwargs={"text_embeds": pooled.to(dev), "time_ids": tids.to(dev)})
+        full = unet(lat.to(dev), t.to(dev), enc.to(dev), **kw).sample.float().cpu()
+        part = unet(lat[:, :, f0:f0 + Fl].contiguous().to(dev), t.to(dev), enc.to(dev), frame_shard=sh,
+                    **kw).sample.float().cpu()
+        r = ref[:, :, f0:f0 + Fl]
+
+        def rel(a, b):
+            return ((a - b).norm() / b.norm()).item()
+        e_full, e_shard = rel(full[:, :, f0:f0 + Fl], r), rel(part, r)
+        ok = e_shard <= 3e-2 and e_shard <= 1.25 * e_full + 2e-3
+        q.put((rank, "ok" if ok else "fail", f"vs fp32 oracle: sharded {e_shard:.3e}, unsharded {e_full:.3e}"))
+    except BaseException as e:  # noqa: BLE001
+        q.put((rank, "fail", repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_frame_shard_unet_two_ranks_one_gpu():
+    if torch.cuda.device_count() == 0:
+        pytest.skip("no HIP device")
+    res = _spawn(_gpu_worker, 2)
+    for rank, status, info in res:
+        print(f"[shard] rank {rank}: {status} {info}")
+        assert status == "ok", f"rank {rank}: {info}"

@@ -230,6 +230,33 @@ def test_group_norm(cuda, K, ns, rps, C1, C2, silu):
     check(out, ref, name="groupnorm")
 
 
+def test_group_norm_split_sums(cuda, K):
+    """Sharded motion GN: per-shard fp64 sums, summed over two 'ranks', then apply == whole-clip GN."""
+    g = torch.Generator().manual_seed(11)
+    ns, rps, C = 2, 4 * 64, 320
+    x = rnd(ns * rps, C, gen=g) + 0.3
+    gam, bet = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g) * 0.1
+    xv = x.view(ns, rps, C)
+    halves = [xv[:, : rps // 2].reshape(-1, C).contiguous(), xv[:, rps // 2:].reshape(-1, C).contiguous()]
+    sums = sum(K.group_norm_sums(h.to(cuda), ns, rps // 2, 32) for h in halves)
+    outs = [K.group_norm_apply_sums(h.to(cuda), ns, rps // 2, 32, 1e-6, gam.to(cuda), bet.to(cuda), sums,
+                                    rps * (C // 32)).cpu() for h in halves]
+    out = torch.cat([o.view(ns, rps // 2, C) for o in outs], 1).reshape(-1, C)
+    ref = F.group_norm(x.float().view(ns, rps, C).permute(0, 2, 1), 32, gam, bet, 1e-6).permute(0, 2, 1)
+    check(out, ref.reshape(-1, C), name="groupnorm_split")
+
+
+@pytest.mark.parametrize("dims,perm", [((2, 3, 4, 5), (2, 0, 1, 3)), ((4, 2, 3, 8), (1, 0, 2, 3)),
+                                       ((4, 2, 3, 8), (1, 2, 0, 3)), ((3, 1, 2, 2), (3, 2, 1, 0))])
+def test_permute_rows(cuda, K, dims, perm):
+    C = 40
+    n = dims[0] * dims[1] * dims[2] * dims[3]
+    x = torch.arange(n * C, dtype=torch.float32).remainder(251).view(n, C).to(torch.bfloat16)
+    out = K.permute_rows(x.to(cuda), dims, perm).cpu()
+    ref = x.view(*dims, C).permute(*perm, 4).reshape(n, C)
+    assert torch.equal(out, ref)
+
+
 @pytest.mark.parametrize("rows,C,use_pe", [(300, 320, False), (64, 1280, True), (513, 640, True), (10, 64, False)])
 def test_layer_norm(cuda, K, rows, C, use_pe):
     g = torch.Generator().manual_seed(rows + C)

@@ -29,6 +29,10 @@ SIGNATURES = {
     "vst_spatial_attention": (_I, [_P, _I, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _F, _P]),
     "vst_temporal_attention": (_I, [_P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _F, _P]),
     "vst_groupnorm_workspace_bytes": (_S, [_I, _I, _I, _I]),
+    "vst_groupnorm_sums": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "vst_groupnorm_apply_sums": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _P, ctypes.c_double, _F, _P, _P, _I, _P,
+                                      _I, _P, _P]),
+    "vst_permute_rows": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "vst_groupnorm": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _F, _P, _P, _I, _P, _I, _P, _P]),
     "vst_layernorm": (_I, [_P, _I, _I, _I, _P, _P, _F, _P, _I, _I, _P, _I, _P]),
     "vst_timestep_embedding": (_I, [_P, _P, _I, _I, _I, _F, _P, _I, _I, _I, _P]),

@@ -87,6 +87,32 @@ __global__ void euler_cfg_kernel(const bf16_t* __restrict__ noise, int ncopy, fl
   lat[idx] += (sigmas[s + 1] - sigmas[s]) * eps;
 }
 
+// Row-block permutation for the frame <-> pixel shard exchange of the motion module.  Rows of C
+// bf16 are indexed 4-D in the source, (i0, i1, i2, i3) with dims d[0..3]; destination axis k is
+// source axis perm[k].  One thread moves 16 B.
+__global__ __launch_bounds__(256) void permute_rows_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__ dst,
+                                                           int C, int4 d, int4 perm, size_t total_chunks) {
+  const int dd[4] = {d.x, d.y, d.z, d.w};
+  const int pp[4] = {perm.x, perm.y, perm.z, perm.w};
+  const int CH = C / 8;
+  for (size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x; idx < total_chunks; idx += (size_t)gridDim.x * 256) {
+    size_t row = idx / CH;
+    const int c = (int)(idx - row * CH) * 8;
+    int j[4], i[4];
+#pragma unroll
+    for (int k = 3; k >= 0; --k) {
+      const int dk = dd[pp[k]];
+      j[k] = (int)(row % dk);
+      row /= dk;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) i[pp[k]] = j[k];
+    const size_t srow = (((size_t)i[0] * dd[1] + i[1]) * dd[2] + i[2]) * dd[3] + i[3];
+    const size_t drow = idx / CH;
+    *reinterpret_cast<u32x4*>(dst + drow * C + c) = *reinterpret_cast<const u32x4*>(src + srow * C + c);
+  }
+}
+
 __global__ void step_advance_kernel(int* step) {
   if (threadIdx.x == 0 && blockIdx.x == 0) *step += 1;
 }
@@ -152,6 +178,22 @@ extern "C" int vst_euler_cfg_step(const void* noise, int ncopy, float guidance, 
 extern "C" int vst_step_advance(int* step_idx, void* stream) {
   if (!step_idx) return VST_ERR_ARG;
   hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, step_idx);
+  return ok();
+}
+
+extern "C" int vst_permute_rows(const void* src, void* dst, int C, int d0, int d1, int d2, int d3, int p0, int p1,
+                                int p2, int p3, void* stream) {
+  if (!src || !dst || src == dst || C <= 0 || (C & 7) || d0 <= 0 || d1 <= 0 || d2 <= 0 || d3 <= 0) return VST_ERR_ARG;
+  const int pp[4] = {p0, p1, p2, p3};
+  int seen = 0;
+  for (int k = 0; k < 4; ++k) {
+    if (pp[k] < 0 || pp[k] > 3 || (seen >> pp[k]) & 1) return VST_ERR_ARG;
+    seen |= 1 << pp[k];
+  }
+  const size_t total = (size_t)d0 * d1 * d2 * d3 * (C / 8);
+  const int grid = (int)std::min<size_t>((total + 255) / 256, 16384);
+  hipLaunchKernelGGL(permute_rows_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)src,
+                     (bf16_t*)dst, C, make_int4(d0, d1, d2, d3), make_int4(p0, p1, p2, p3), total);
   return ok();
 }
 

@@ -41,7 +41,7 @@ struct RingCfg {
   static constexpr int A_PIECES = A_BYTES / 1024 / NWAVES;  // per wave per tile
   static constexpr int B_PIECES = B_BYTES / 1024 / NWAVES;
   static constexpr int DPT = A_PIECES + B_PIECES;            // DMA instructions per thread per tile
-  static constexpr int EPI_BYTES = WM * BN * 4;
+  static constexpr int EPI_BYTES = BM * (BN * 2 + 16);  // bf16 tile staged for the epilogue
   static constexpr int LDS = STAGES * STAGE > EPI_BYTES ? STAGES * STAGE : EPI_BYTES;
   static_assert(A_BYTES % (1024 * NWAVES) == 0 && B_BYTES % (1024 * NWAVES) == 0, "piece split");
   static_assert(LDS <= 160 * 1024, "LDS budget");
@@ -203,21 +203,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
 
   constexpr int S = Cfg::STAGES;
   const int fr = lane & 15, fq = lane >> 4;
-  // ---- prologue: tiles 0..S-2 in flight, retire tile 0 ----
-#pragma unroll
-  for (int s = 0; s < S - 1; ++s)
-    if (s < nk) issue(kt0 + s, s);
-  wait_tiles<Cfg>(min(nk, S - 1) - 1);
-  __builtin_amdgcn_s_barrier();
-
   const bool no_dma = p.ablate & 1, no_mfma = p.ablate & 2;
-  // fragments of the current k-tile live in registers: all MI + NJ ds_read_b128 are issued
-  // right after the barrier that publishes the stage, so the MFMA chain below runs back to
-  // back (the compiler's lgkmcnt ladder exposes only the first read's latency).
-  // Fragments are double-buffered in registers: iteration `it` publishes tile it+1 (counted
-  // vmcnt + barrier), refills the stage tile it-1 used, issues the ds_reads of tile it+1 into
-  // the spare register set, and only then runs tile it's MFMA chain — the LDS read latency of
-  // the next tile hides under the current MFMAs instead of opening a bubble after every barrier.
   typedef bf16x8 FragA[Cfg::MI];
   typedef bf16x8 FragB[Cfg::NJ];
   FragA fa0, fa1;
@@ -232,6 +218,76 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
     for (int i = 0; i < Cfg::MI; ++i)
       fa[i] = *reinterpret_cast<const bf16x8*>(As + rswz(wr * Cfg::WM + i * 16 + fr, fq));
   };
+  auto mfmas = [&](FragA& ca, FragB& cb) {
+    __builtin_amdgcn_s_setprio(1);
+    if (!no_mfma) {
+#pragma unroll
+      for (int i = 0; i < Cfg::MI; ++i)
+#pragma unroll
+        for (int j = 0; j < Cfg::NJ; ++j)
+          // W fragment as the MFMA's A operand: acc[i][j][r] = C[m = i*16 + (lane&15)][n = j*16 +
+          // 4*(lane>>4) + r] — four consecutive output columns per lane (vector epilogue).
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cb[j], ca[i], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < Cfg::MI; ++i) asm volatile("" ::"v"(ca[i]));
+#pragma unroll
+      for (int j = 0; j < Cfg::NJ; ++j) asm volatile("" ::"v"(cb[j]));
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  if constexpr (Cfg::NWAVES == 8) {
+    // ---- ping-pong schedule (8 waves; waves w and w+4 share a SIMD) ----
+    // Each k-tile is two barrier intervals: L = {LDS-DMA issue of tile it+S-1, ds_reads of tile
+    // it+1's fragments, counted wait for this wave's DMA of tile it+2} and C = {the MFMA chain of
+    // tile it}.  Waves 4-7 run one barrier behind waves 0-3 (one extra s_barrier up front, which
+    // waves 0-3 pay back after the loop), so in every interval one wave of each SIMD issues MFMAs
+    // while its partner issues loads: the load work hides under the matrix pipe.
+    // Hazards (intervals counted globally, group g's L(it) at 2it+g, C(it) at 2it+1+g):
+    //  RAW: tile it+1 is read in L(it) (interval >= 2it); each group waited for its own DMA of
+    //       tile it+1 in L(it-1) (interval <= 2it-1), before the barrier that ends it.
+    //  WAR: L(it) refills the stage of tile it-1, whose fragments every group read in L(it-2)
+    //       and consumed in C(it-2) (interval <= 2it-2), two barriers earlier.
+    const bool late = wid >= 4;
+#pragma unroll
+    for (int s = 0; s < S - 1; ++s)
+      if (s < nk) issue(kt0 + s, s);
+    wait_tiles<Cfg>(max(0, min(nk - 1, S - 2) - 1));  // own DMA of tiles 0 and 1 landed
+    __builtin_amdgcn_s_barrier();
+    if (nk > 0) load_into(fa0, fb0, 0);
+    if (late) __builtin_amdgcn_s_barrier();
+    int wrs = S - 1, nrd = 1 % S;
+    auto pp_step = [&](int it, FragA& ca, FragB& cb, FragA& na, FragB& nb) {
+      if (it + S - 1 < nk && !no_dma) issue(kt0 + it + S - 1, wrs);
+      wrs = wrs + 1 == S ? 0 : wrs + 1;
+      if (it + 1 < nk) load_into(na, nb, nrd);
+      nrd = nrd + 1 == S ? 0 : nrd + 1;
+      if (it + 2 < nk) wait_tiles<Cfg>(no_dma ? 0 : min(nk - 1, it + S - 1) - (it + 2));
+      __builtin_amdgcn_s_barrier();
+      mfmas(ca, cb);
+      __builtin_amdgcn_s_barrier();
+    };
+    for (int it = 0; it < nk; it += 2) {
+      pp_step(it, fa0, fb0, fa1, fb1);
+      if (it + 1 < nk) pp_step(it + 1, fa1, fb1, fa0, fb0);
+    }
+    if (!late) __builtin_amdgcn_s_barrier();
+  } else {
+  // ---- prologue: tiles 0..S-2 in flight, retire tile 0 ----
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nk) issue(kt0 + s, s);
+  wait_tiles<Cfg>(min(nk, S - 1) - 1);
+  __builtin_amdgcn_s_barrier();
+
+  // fragments of the current k-tile live in registers: all MI + NJ ds_read_b128 are issued
+  // right after the barrier that publishes the stage, so the MFMA chain below runs back to
+  // back (the compiler's lgkmcnt ladder exposes only the first read's latency).
+  // Fragments are double-buffered in registers: iteration `it` publishes tile it+1 (counted
+  // vmcnt + barrier), refills the stage tile it-1 used, issues the ds_reads of tile it+1 into
+  // the spare register set, and only then runs tile it's MFMA chain — the LDS read latency of
+  // the next tile hides under the current MFMAs instead of opening a bubble after every barrier.
   int wrs = S - 1, nrd = 1 % S;  // next stage to fill / stage holding tile it+1
   auto step = [&](int it, FragA& ca, FragB& cb, FragA& na, FragB& nb) {
     if (it + 1 < nk) {
@@ -242,87 +298,108 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
     wrs = wrs + 1 == S ? 0 : wrs + 1;
     if (it + 1 < nk) load_into(na, nb, nrd);
     nrd = nrd + 1 == S ? 0 : nrd + 1;
-    __builtin_amdgcn_s_setprio(1);
-    if (!no_mfma) {
-#pragma unroll
-      for (int i = 0; i < Cfg::MI; ++i)
-#pragma unroll
-        for (int j = 0; j < Cfg::NJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ca[i], cb[j], acc[i][j], 0, 0, 0);
-    } else {
-#pragma unroll
-      for (int i = 0; i < Cfg::MI; ++i) asm volatile("" ::"v"(ca[i]));
-#pragma unroll
-      for (int j = 0; j < Cfg::NJ; ++j) asm volatile("" ::"v"(cb[j]));
-    }
-    __builtin_amdgcn_s_setprio(0);
+    mfmas(ca, cb);
   };
   if (nk > 0) load_into(fa0, fb0, 0);
   for (int it = 0; it < nk; it += 2) {
     step(it, fa0, fb0, fa1, fb1);
     if (it + 1 < nk) step(it + 1, fa1, fb1, fa0, fb0);
   }
+  }
   __builtin_amdgcn_s_barrier();  // all waves done with the ring before the epilogue reuses LDS
 
-  // ---------------- epilogue: one wave-row group at a time through LDS ----------------
-  float* Cs = reinterpret_cast<float*>(smem);
-  const auto rr = make_rsrc(p.R ? p.R : p.Wt, p.R ? p.r_bytes : 0u);
-#pragma unroll 1
-  for (int round = 0; round < Cfg::WAVES_M; ++round) {
-    if (wr == round) {
+  // ---------------- epilogue ----------------
+  // Split-K partials go straight from registers to the fp32 slab (16 B per lane).  Otherwise
+  // bias is added in registers, the whole BMxBN tile is staged ONCE in LDS as bf16 (the rounding
+  // point of the reference's bf16 linear/conv output), and a vectorized pass applies the per-frame
+  // row bias / residual add (after that rounding, as the reference's separate add does) or GEGLU
+  // and writes full 16-B chunks.  All residual loads of a thread are issued before any use.
+  const int lrow0 = wr * Cfg::WM + fr;          // + i*16
+  const int lcol0 = wc * Cfg::WN + 4 * fq;      // + j*16
+  if constexpr (EPI == 2) {
+    float* slab = p.ws + (size_t)blockIdx.z * p.M * p.N;
 #pragma unroll
-      for (int i = 0; i < Cfg::MI; ++i)
+    for (int i = 0; i < Cfg::MI; ++i) {
+      const int m = m0 + lrow0 + i * 16;
+      if (m >= p.M) continue;
 #pragma unroll
-        for (int j = 0; j < Cfg::NJ; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            Cs[(i * 16 + fq * 4 + r) * BN + wc * Cfg::WN + j * 16 + fr] = acc[i][j][r];
-    }
-    __syncthreads();
-    const int rbase = m0 + round * Cfg::WM;
-    if (EPI == 2) {
-      constexpr int CPR = BN / 8;
-      float* slab = p.ws + (size_t)blockIdx.z * p.M * p.N;
-      for (int idx = tid; idx < Cfg::WM * CPR; idx += Cfg::THREADS) {
-        const int row = idx / CPR, cc = idx - row * CPR;
-        const int m = rbase + row, n = n0 + cc * 8;
-        if (m >= p.M || n >= p.N) continue;
-        const f32x4 c0 = *reinterpret_cast<const f32x4*>(Cs + row * BN + cc * 8);
-        const f32x4 c1 = *reinterpret_cast<const f32x4*>(Cs + row * BN + cc * 8 + 4);
+      for (int j = 0; j < Cfg::NJ; ++j) {
+        const int n = n0 + lcol0 + j * 16;
         float* dst = slab + (size_t)m * p.N + n;
-        if (n + 8 <= p.N) {
-          *reinterpret_cast<f32x4*>(dst) = c0;
-          *reinterpret_cast<f32x4*>(dst + 4) = c1;
+        if (n + 4 <= p.N) {
+          *reinterpret_cast<f32x4*>(dst) = acc[i][j];
         } else {
-          for (int e = 0; e < p.N - n; ++e) dst[e] = e < 4 ? c0[e] : c1[e - 4];
+          for (int e = 0; e < p.N - n; ++e) dst[e] = acc[i][j][e];
         }
       }
-    } else if (EPI == 0) {
-      constexpr int CPR = BN / 8;
-#pragma unroll 2
-      for (int idx = tid; idx < Cfg::WM * CPR; idx += Cfg::THREADS) {
-        const int row = idx / CPR, cc = idx - row * CPR;
-        const int m = rbase + row, n = n0 + cc * 8;
-        if (m >= p.M || n >= p.N) continue;
-        float v[8];
-        const f32x4 c0 = *reinterpret_cast<const f32x4*>(Cs + row * BN + cc * 8);
-        const f32x4 c1 = *reinterpret_cast<const f32x4*>(Cs + row * BN + cc * 8 + 4);
+    }
+    return;
+  } else {
+    constexpr int LROW = BN * 2 + 16;  // staged bf16 row (16-B pad: conflict-light b64 writes)
+    static_assert(BM * LROW <= Cfg::LDS, "epilogue staging must fit in the ring's LDS");
+    if (p.bias) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) { v[e] = c0[e]; v[e + 4] = c1[e]; }
-        const int nv = min(8, p.N - n);
-        if (p.bias) {
+      for (int j = 0; j < Cfg::NJ; ++j) {
+        const int n = n0 + lcol0 + j * 16;
+        f32x4 b4;
+        if (n + 4 <= p.N) {
+          b4 = *reinterpret_cast<const f32x4*>(p.bias + n);
+        } else {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) if (e < nv) v[e] += p.bias[n + e];
+          for (int e = 0; e < 4; ++e) b4[e] = n + e < p.N ? p.bias[n + e] : 0.f;
         }
+#pragma unroll
+        for (int i = 0; i < Cfg::MI; ++i) acc[i][j] += b4;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < Cfg::MI; ++i)
+#pragma unroll
+      for (int j = 0; j < Cfg::NJ; ++j) {
+        u32x2 v;
+        v[0] = pack2bf(acc[i][j][0], acc[i][j][1]);
+        v[1] = pack2bf(acc[i][j][2], acc[i][j][3]);
+        *reinterpret_cast<u32x2*>(smem + (lrow0 + i * 16) * LROW + (lcol0 + j * 16) * 2) = v;
+      }
+    __syncthreads();
+    const auto rr = make_rsrc(p.R ? p.R : p.Wt, p.R ? p.r_bytes : 0u);
+    if constexpr (EPI == 0) {
+      constexpr int CPR = BN / 8;                 // 16-B chunks per row
+      constexpr int RSTEP = Cfg::THREADS / CPR;   // rows advanced per item
+      constexpr int ITEMS = BM / RSTEP;
+      static_assert(Cfg::THREADS % CPR == 0 && BM % RSTEP == 0, "item split");
+      const int cc = tid % CPR, row0 = tid / CPR;
+      const int n = n0 + cc * 8;
+      const int nv = min(8, p.N - n);
+      u32x4 res[ITEMS];
+      if (p.R) {
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+          const int m = m0 + row0 + k * RSTEP;
+          res[k] = buf_load16(rr, (m < p.M && nv == 8) ? (m * p.ldr + n) * 2 : kOOB);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < ITEMS; ++k) {
+        const int row = row0 + k * RSTEP, m = m0 + row;
+        if (m >= p.M || nv <= 0) continue;
+        float v[8];
+        unpack8(*reinterpret_cast<const u32x4*>(smem + row * LROW + cc * 16), v);
         if (p.rbias) {
           const float* rb = p.rbias + (size_t)(m / p.rbias_div) * p.ldrb + n;
+          if (nv == 8) {
+            const f32x4 r0 = *reinterpret_cast<const f32x4*>(rb);
+            const f32x4 r1 = *reinterpret_cast<const f32x4*>(rb + 4);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) if (e < nv) v[e] += rb[e];
+            for (int e = 0; e < 4; ++e) { v[e] += r0[e]; v[e + 4] += r1[e]; }
+          } else {
+            for (int e = 0; e < nv; ++e) v[e] += rb[e];
+          }
         }
         if (nv == 8) {
           if (p.R) {
             float r8[8];
-            unpack8(buf_load16(rr, (m * p.ldr + n) * 2), r8);
+            unpack8(res[k], r8);
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] += r8[e];
           }
@@ -335,27 +412,26 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
           }
         }
       }
-    } else {  // GEGLU: per 128 weight rows [64 hidden | 64 gate] -> 64 outputs
-      constexpr int CPR = BN / 16;
-#pragma unroll 2
-      for (int idx = tid; idx < Cfg::WM * CPR; idx += Cfg::THREADS) {
-        const int row = idx / CPR, oc = idx - row * CPR;
-        const int blk = oc >> 3, c = (oc & 7) * 8;
-        const int m = rbase + row;
-        const int nh = n0 + blk * 128 + c;
-        if (m >= p.M || nh >= p.N) continue;
-        float v[8];
+    } else {  // GEGLU: per 128 weight rows [64 hidden | 64 gate] -> 64 outputs, bias already in
+      constexpr int CPR = BN / 16;                // 8-output chunks per row
+      constexpr int RSTEP = Cfg::THREADS / CPR;
+      constexpr int ITEMS = BM / RSTEP;
+      static_assert(Cfg::THREADS % CPR == 0 && BM % RSTEP == 0, "item split");
+      const int oc = tid % CPR, row0 = tid / CPR;
+      const int blk = oc >> 3, c = (oc & 7) * 8;
+      const int nh = n0 + blk * 128 + c;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float h = Cs[row * BN + blk * 128 + c + e];
-          float g = Cs[row * BN + blk * 128 + 64 + c + e];
-          if (p.bias) { h += p.bias[nh + e]; g += p.bias[nh + 64 + e]; }
-          v[e] = h * gelu_erf(g);
-        }
+      for (int k = 0; k < ITEMS; ++k) {
+        const int row = row0 + k * RSTEP, m = m0 + row;
+        if (m >= p.M || nh >= p.N) continue;
+        float h[8], g[8], v[8];
+        unpack8(*reinterpret_cast<const u32x4*>(smem + row * LROW + (blk * 128 + c) * 2), h);
+        unpack8(*reinterpret_cast<const u32x4*>(smem + row * LROW + (blk * 128 + 64 + c) * 2), g);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = h[e] * gelu_erf(g[e]);
         *reinterpret_cast<u32x4*>(p.C + (size_t)m * p.ldc + (n0 >> 1) + blk * 64 + c) = pack8(v);
       }
     }
-    __syncthreads();
   }
 }
 

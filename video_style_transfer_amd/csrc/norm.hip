@@ -137,6 +137,47 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const bf16_t* __restrict_
   }
 }
 
+// Frame-sharded motion GroupNorm (statistics over all frames of a clip, frames spread over
+// ranks): merge this rank's chunk partials into per-(sample, group) double (sum, sumsq), which the
+// host all-reduces across ranks, then finalize from the reduced sums.
+__global__ __launch_bounds__(64) void gn_sums_kernel(const float* __restrict__ part, int nchunk, int groups,
+                                                     double* __restrict__ sums) {
+  const int s = blockIdx.x / groups, gi = blockIdx.x - s * groups;
+  const int lane = threadIdx.x;
+  double a = 0.0, q = 0.0;
+  for (int c = lane; c < nchunk; c += 64) {
+    const float* p = part + (((size_t)s * nchunk + c) * groups + gi) * 2;
+    a += p[0];
+    q += p[1];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o);
+    q += __shfl_xor(q, o);
+  }
+  if (lane == 0) {
+    sums[(size_t)blockIdx.x * 2] = a;
+    sums[(size_t)blockIdx.x * 2 + 1] = q;
+  }
+}
+
+__global__ __launch_bounds__(64) void gn_finalize_sums_kernel(const double* __restrict__ sums, double count,
+                                                              int groups, int Cg, float eps,
+                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta,
+                                                              float* __restrict__ scale, float* __restrict__ shift,
+                                                              int C) {
+  const int s = blockIdx.x / groups, gi = blockIdx.x - s * groups;
+  const double mean = sums[(size_t)blockIdx.x * 2] / count;
+  const double var = fmax(sums[(size_t)blockIdx.x * 2 + 1] / count - mean * mean, 0.0);
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  for (int c = gi * Cg + threadIdx.x; c < (gi + 1) * Cg; c += 64) {
+    const float sc = rstd * gamma[c];
+    scale[(size_t)s * C + c] = sc;
+    shift[(size_t)s * C + c] = beta[c] - (float)mean * sc;
+  }
+}
+
 // LayerNorm: one wave per row, up to MAXCH 8-channel chunks per lane.
 template <int MAXCH>
 __global__ __launch_bounds__(256) void layernorm_kernel(const bf16_t* __restrict__ x, int ldx, int C, int rows,
@@ -230,6 +271,55 @@ extern "C" int vst_groupnorm(const void* x1, int ld1, int C1, const void* x2, in
   hipLaunchKernelGGL(gn_finalize_kernel, dim3(nsamples * groups), dim3(64), 0, s, part, nchunk, rows_per_sample,
                      groups, C / groups, eps, gamma, beta, scale, shift, C);
   const size_t total = (size_t)nsamples * rows_per_sample * CH;
+  const int grid = (int)std::min<size_t>((total + 255) / 256, 16384);
+  hipLaunchKernelGGL(gn_apply_kernel, dim3(grid), dim3(256), 0, s, (const bf16_t*)x1, ld1, C1, (const bf16_t*)x2,
+                     ld2, C2, rows_per_sample, scale, shift, silu_act, (bf16_t*)y, ldy, total);
+  return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+}
+
+static int gn_check(const void* x1, int ld1, int C1, const void* x2, int ld2, int C2, int nsamples,
+                    int rows_per_sample, int groups) {
+  const int C = C1 + (x2 ? C2 : 0);
+  if (!x1 || nsamples <= 0 || rows_per_sample <= 0 || groups <= 0) return VST_ERR_ARG;
+  if (C % groups || C % 8 || C1 % 8 || (ld1 & 7) || (x2 && (ld2 & 7))) return VST_ERR_ARG;
+  if (C > 4096) return VST_ERR_ARG;
+  return VST_OK;
+}
+
+extern "C" int vst_groupnorm_sums(const void* x1, int ld1, int C1, const void* x2, int ld2, int C2, int nsamples,
+                                  int rows_per_sample, int groups, double* sums, void* workspace, void* stream) {
+  if (gn_check(x1, ld1, C1, x2, ld2, C2, nsamples, rows_per_sample, groups) || !sums || !workspace)
+    return VST_ERR_ARG;
+  if (!x2) C2 = 0;
+  const int C = C1 + C2;
+  hipStream_t s = (hipStream_t)stream;
+  const int nchunk = (rows_per_sample + GN_ROWS - 1) / GN_ROWS;
+  const int CH = C / 8;
+  const int rps = CH >= 256 ? 1 : 256 / CH;
+  const size_t lds = (size_t)2 * rps * C * sizeof(float);
+  if (lds > 64 * 1024) return VST_ERR_ARG;
+  float* part = (float*)workspace;
+  hipLaunchKernelGGL(gn_stats_kernel, dim3(nchunk, nsamples), dim3(256), lds, s, (const bf16_t*)x1, ld1, C1,
+                     (const bf16_t*)x2, ld2, C2, rows_per_sample, groups, part);
+  hipLaunchKernelGGL(gn_sums_kernel, dim3(nsamples * groups), dim3(64), 0, s, part, nchunk, groups, sums);
+  return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+}
+
+extern "C" int vst_groupnorm_apply_sums(const void* x1, int ld1, int C1, const void* x2, int ld2, int C2,
+                                        int nsamples, int rows_per_sample, int groups, const double* sums,
+                                        double count, float eps, const float* gamma, const float* beta, int silu_act,
+                                        void* y, int ldy, void* workspace, void* stream) {
+  if (gn_check(x1, ld1, C1, x2, ld2, C2, nsamples, rows_per_sample, groups) || !sums || !workspace || !y ||
+      !gamma || !beta || (ldy & 7) || !(count > 0.0))
+    return VST_ERR_ARG;
+  if (!x2) C2 = 0;
+  const int C = C1 + C2;
+  hipStream_t s = (hipStream_t)stream;
+  float* scale = (float*)workspace + gn_part_floats(nsamples, rows_per_sample, groups);
+  float* shift = scale + (size_t)nsamples * C;
+  hipLaunchKernelGGL(gn_finalize_sums_kernel, dim3(nsamples * groups), dim3(64), 0, s, sums, count, groups,
+                     C / groups, eps, gamma, beta, scale, shift, C);
+  const size_t total = (size_t)nsamples * rows_per_sample * (C / 8);
   const int grid = (int)std::min<size_t>((total + 255) / 256, 16384);
   hipLaunchKernelGGL(gn_apply_kernel, dim3(grid), dim3(256), 0, s, (const bf16_t*)x1, ld1, C1, (const bf16_t*)x2,
                      ld2, C2, rows_per_sample, scale, shift, silu_act, (bf16_t*)y, ldy, total);

@@ -1,0 +1,106 @@
+"""Frame sharding of a clip across the GPUs of a node (one process per GPU, torch.distributed / RCCL).
+
+SURVEY.md §8(e): everything in the UNet is frame-local except the 15 motion modules, whose frame-axis
+attention needs every frame of a clip at each pixel, and whose GroupNorm takes its statistics over the
+whole clip (diffusers AnimateDiffTransformer3D, built at animatediff/utils.py:31).
+
+With P ranks each holding F/P contiguous frames of every clip, a motion module runs as:
+  1. GroupNorm statistics: per-(clip, group) fp64 (sum, sumsq) over this rank's frames
+     -> all-reduce (2*B*32 doubles) -> every rank normalises its own frames with the clip-wide
+     statistics, then applies proj_in (per token, frame-local);
+  2. frame shard -> pixel shard: one all-to-all hands rank q the pixel slab q (H*W/P pixels) of every
+     frame. Each rank now holds all F frames for H*W/P pixels. That is exactly the data the
+     frame-axis attention needs. The whole transformer block runs unchanged on it (LN, q/k/v, temporal
+     attention, out, GEGLU FF are all per token or per pixel);
+  3. pixel shard -> frame shard: the inverse all-to-all, then proj_out + residual frame-local.
+Per module and rank this moves 2 x (P-1)/P of the rank's activation over xGMI. That is P x less than
+an all-gather of the clip before the attention (the north-star formulation), and no motion-module
+work is duplicated across ranks.
+
+The layout permutations around the all-to-all are one HIP kernel each (vst_permute_rows). With the
+nccl (= RCCL) backend the collectives run on the current stream and are captured in the step's HIP
+graph. The gloo backend (CPU transport; used by tests to run several ranks on one GPU or on CPU) stages
+through host memory and cannot be graph-captured.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from . import kernels as K
+
+Permute = Callable[[torch.Tensor, Sequence[int], Sequence[int]], torch.Tensor]
+
+
+class FrameShard:
+    def __init__(self, group=None, permute: Optional[Permute] = None):
+        if not dist.is_initialized():
+            raise RuntimeError("FrameShard needs an initialised torch.distributed process group")
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.backend = str(dist.get_backend(group)).lower()
+        self._permute = permute or K.permute_rows
+
+    @property
+    def graph_capturable(self) -> bool:
+        return self.backend == "nccl"
+
+    def local_frames(self, F: int):
+        """(frames per rank, first global frame of this rank)."""
+        if F % self.world:
+            raise ValueError(f"{F} frames do not split over {self.world} ranks")
+        fl = F // self.world
+        return fl, self.rank * fl
+
+    # ---- collectives ----------------------------------------------------------------------
+    def _staged(self, t: torch.Tensor) -> bool:
+        return t.is_cuda and self.backend != "nccl"
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world == 1:
+            return t
+        if self._staged(t):
+            h = t.cpu()
+            dist.all_reduce(h, group=self.group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, group=self.group)
+        return t
+
+    def _all_to_all(self, out: torch.Tensor, inp: torch.Tensor):
+        if self._staged(inp):
+            ho = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_to_all_single(ho, inp.cpu(), group=self.group)
+            out.copy_(ho)
+        else:
+            dist.all_to_all_single(out, inp, group=self.group)
+
+    # ---- layout exchange ------------------------------------------------------------------
+    def to_pixels(self, h: torch.Tensor, B: int, Fl: int, HW: int) -> torch.Tensor:
+        """rows (b, f_local, p) over this rank's frames -> rows (b, f_global, p') over pixel slab `rank`
+        (p' < HW/P), every frame of every clip."""
+        P = self.world
+        if P == 1:
+            return h
+        if HW % P:
+            raise ValueError(f"{HW} pixels do not split over {P} ranks")
+        hp = HW // P
+        send = self._permute(h, (B, Fl, P, hp), (2, 0, 1, 3))   # (dest rank q, b, f_local, p')
+        recv = torch.empty_like(send)
+        self._all_to_all(recv, send)                             # (source rank r, b, f_local, p')
+        return self._permute(recv, (P, B, Fl, hp), (1, 0, 2, 3))  # (b, r*Fl + f_local, p')
+
+    def to_frames(self, h: torch.Tensor, B: int, Fl: int, HW: int) -> torch.Tensor:
+        """Inverse of to_pixels."""
+        P = self.world
+        if P == 1:
+            return h
+        hp = HW // P
+        send = self._permute(h, (B, P, Fl, hp), (1, 0, 2, 3))   # (dest rank r, b, f_local, p')
+        recv = torch.empty_like(send)
+        self._all_to_all(recv, send)                             # (source slab q, b, f_local, p')
+        return self._permute(recv, (P, B, Fl, hp), (1, 2, 0, 3))  # (b, f_local, q*hp + p')
+

@@ -29,20 +29,21 @@ def profile_launches(active: bool):
 
 
 def collect_launches():
-    """[(kind, kernel symbol or None, flops, bytes, ms)] for the launches recorded since
+    """[(kind, kernel symbol or None, flops, bytes, ms, shape)] for the launches recorded since
     profile_launches(True)."""
     torch.cuda.synchronize()
-    out = [(k, y, f, b, s.elapsed_time(e)) for k, y, f, b, s, e in (_PROF or [])]
+    out = [(k, y, f, b, s.elapsed_time(e), sh) for k, y, f, b, s, e, sh in (_PROF or [])]
     return out
 
 
 class _Rec:
-    __slots__ = ("kind", "flops", "nbytes", "s", "sym")
+    __slots__ = ("kind", "flops", "nbytes", "s", "sym", "shape")
 
-    def __init__(self, kind, flops, nbytes, sym=None):
+    def __init__(self, kind, flops, nbytes, sym=None, shape=None):
         self.kind, self.flops, self.nbytes = kind, flops, nbytes
         self.s = None
         self.sym = sym  # callable -> kernel symbol (evaluated only while profiling)
+        self.shape = shape
 
     def __enter__(self):
         if _PROF is not None:
@@ -54,7 +55,8 @@ class _Rec:
         if _PROF is not None and self.s is not None:
             e = torch.cuda.Event(enable_timing=True)
             e.record()
-            _PROF.append((self.kind, self.sym() if self.sym else None, self.flops, self.nbytes, self.s, e))
+            _PROF.append((self.kind, self.sym() if self.sym else None, self.flops, self.nbytes, self.s, e,
+                          self.shape))
 
 
 GEMM_POLICY = {"tile": 0, "splits": 0}  # 0 = library heuristic (tuning / tests may force)
@@ -131,7 +133,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
     kind = kind or ("gemm_geglu" if geglu else ("gemm_lora" if x2 is not None and alg_k2 is not None else "gemm"))
     n_alg = N if alg_n is None else alg_n
     with _Rec(kind, 2.0 * M * n_alg * k_alg, 2.0 * (M * k_alg + N * k_alg + M * n_out * (2 if residual is not None else 1)),
-              lambda: gemm_kernel_name(M, N, K, 1 if geglu else 0)):
+              lambda: gemm_kernel_name(M, N, K, 1 if geglu else 0), (M, N, K)):
         ws = _workspace(x.device)
         _lib.call("vst_gemm_ex", _p(x), _ld(x), _p(x2), 0 if x2 is None else _ld(x2), K1, _p(w), _ld(w), M, N, K,
                   _p(bias), _p(row_bias), row_bias_div, N if row_bias is not None else 0, _p(residual),
@@ -175,7 +177,7 @@ def conv3x3(x1: torch.Tensor, nimg: int, H: int, W: int, w: torch.Tensor, bias: 
         _dev(residual, BF16, "residual")
     kind = "conv3x3" if (C1 + C2) % 64 == 0 else "conv3x3_small_cin"
     with _Rec(kind, 2.0 * M * Cout * kreal, 2.0 * (nimg * H * W * (C1 + C2) + Cout * kreal + M * Cout),
-              lambda: gemm_kernel_name(M, Cout, w.shape[1], 2 if kind == "conv3x3" else 3)):
+              lambda: gemm_kernel_name(M, Cout, w.shape[1], 2 if kind == "conv3x3" else 3), (M, Cout, w.shape[1])):
         ws = _workspace(x1.device)
         _lib.call("vst_conv3x3_ex", _p(x1), C1, _p(x2), C2, nimg, H, W, stride, 1 if upsample else 0, _p(w), Cout,
                   _p(bias), _p(row_bias), row_bias_div, _p(residual), 0 if residual is None else _ld(residual),
@@ -236,6 +238,61 @@ def group_norm(x1, nsamples, rows_per_sample, groups, eps, gamma, beta, *, silu=
         _lib.call("vst_groupnorm", _p(x1), _ld(x1), x1.shape[1], _p(x2), 0 if x2 is None else _ld(x2),
                   0 if x2 is None else x2.shape[1], nsamples, rows_per_sample, groups, float(eps), _p(gamma),
                   _p(beta), 1 if silu else 0, _p(out), _ld(out), _p(ws), _stream())
+    return out
+
+
+def _gn_ws(x1, nsamples, rows_per_sample, groups, C):
+    ws_bytes = _lib.load().vst_groupnorm_workspace_bytes(nsamples, rows_per_sample, groups, C)
+    return torch.empty((ws_bytes + 3) // 4, dtype=F32, device=x1.device)
+
+
+def group_norm_sums(x1, nsamples, rows_per_sample, groups, *, x2=None, out=None):
+    """Per-(sample, group) fp64 (sum, sumsq) over this rank's rows -> [nsamples*groups*2] (frame-sharded
+    motion GroupNorm: the host all-reduces these across ranks)."""
+    _dev(x1, BF16, "x1")
+    C = x1.shape[1] + (0 if x2 is None else x2.shape[1])
+    if x2 is not None:
+        _dev(x2, BF16, "x2")
+    if x1.shape[0] != nsamples * rows_per_sample:
+        raise _lib.VstError("group_norm_sums: rows != nsamples*rows_per_sample")
+    if out is None:
+        out = torch.empty(nsamples * groups * 2, dtype=torch.float64, device=x1.device)
+    ws = _gn_ws(x1, nsamples, rows_per_sample, groups, C)
+    with _Rec("groupnorm", 0.0, 2.0 * x1.shape[0] * C):
+        _lib.call("vst_groupnorm_sums", _p(x1), _ld(x1), x1.shape[1], _p(x2), 0 if x2 is None else _ld(x2),
+                  0 if x2 is None else x2.shape[1], nsamples, rows_per_sample, groups, _p(out), _p(ws), _stream())
+    return out
+
+
+def group_norm_apply_sums(x1, nsamples, rows_per_sample, groups, eps, gamma, beta, sums, count, *, silu=False,
+                          x2=None, out=None):
+    """GroupNorm of this rank's rows with statistics from (all-reduced) `sums`; `count` = elements per
+    (sample, group) over the whole clip."""
+    _dev(x1, BF16, "x1")
+    C = x1.shape[1] + (0 if x2 is None else x2.shape[1])
+    if x2 is not None:
+        _dev(x2, BF16, "x2")
+    if sums.dtype != torch.float64 or not sums.is_cuda or sums.numel() != nsamples * groups * 2:
+        raise _lib.VstError("group_norm_apply_sums: sums must be fp64 [nsamples*groups*2] on device")
+    if out is None:
+        out = torch.empty((x1.shape[0], C), dtype=BF16, device=x1.device)
+    ws = _gn_ws(x1, nsamples, rows_per_sample, groups, C)
+    with _Rec("groupnorm", 0.0, 2.0 * 2 * x1.shape[0] * C):
+        _lib.call("vst_groupnorm_apply_sums", _p(x1), _ld(x1), x1.shape[1], _p(x2), 0 if x2 is None else _ld(x2),
+                  0 if x2 is None else x2.shape[1], nsamples, rows_per_sample, groups, _p(sums), float(count),
+                  float(eps), _p(gamma), _p(beta), 1 if silu else 0, _p(out), _ld(out), _p(ws), _stream())
+    return out
+
+
+def permute_rows(src, dims, perm, out=None):
+    """src rows indexed (i0,i1,i2,i3) over `dims`; returns rows in order (i_perm[0], .., i_perm[3])."""
+    _dev(src, BF16, "src")
+    if not src.is_contiguous() or src.shape[0] != dims[0] * dims[1] * dims[2] * dims[3]:
+        raise _lib.VstError("permute_rows: src must be contiguous with prod(dims) rows")
+    if out is None:
+        out = torch.empty_like(src)
+    with _Rec("permute", 0.0, 2.0 * 2 * src.numel()):
+        _lib.call("vst_permute_rows", _p(src), _p(out), src.shape[1], *dims, *perm, _stream())
     return out
 
 

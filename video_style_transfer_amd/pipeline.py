@@ -28,9 +28,16 @@ BF16 = torch.bfloat16
 class AnimateDiffDenoiser:
     def __init__(self, unet: UNetMotionModel, num_frames: int, height: int, width: int, *,
                  num_inference_steps: int = 50, guidance_scale: float = 7.5, device=None,
-                 scheduler: Optional[EulerDiscreteScheduler] = None, use_graph: bool = True):
+                 scheduler: Optional[EulerDiscreteScheduler] = None, use_graph: bool = True, shard=None,
+                 num_clips: int = 1):
+        """`num_clips` clips are denoised together (the reference loop is one clip, B=1).
+        `shard` (frame_shard.FrameShard): this process denoises frames [f0, f0 + F/P) of every clip and
+        exchanges with the other ranks inside every motion module."""
         self.unet = unet
-        self.F = num_frames
+        self.nclips = num_clips
+        self.shard = shard
+        self.F_total = num_frames
+        self.F, self.f0 = shard.local_frames(num_frames) if shard is not None else (num_frames, 0)
         self.h, self.w = height // 8, width // 8
         self.height, self.width = height, width
         self.guidance = guidance_scale
@@ -43,8 +50,9 @@ class AnimateDiffDenoiser:
         self.use_graph = use_graph
         cfg = unet.config
         dev = self.device
-        self.lat = torch.zeros(1, cfg.in_channels, self.F, self.h, self.w, dtype=torch.float32, device=dev)
-        self.x = torch.empty(self.ncopy * self.F * self.h * self.w, cfg.in_channels, dtype=BF16, device=dev)
+        self.lat = torch.zeros(num_clips, cfg.in_channels, self.F, self.h, self.w, dtype=torch.float32, device=dev)
+        self.x = torch.empty(self.ncopy * num_clips * self.F * self.h * self.w, cfg.in_channels, dtype=BF16,
+                             device=dev)
         self.step_idx = torch.zeros(1, dtype=torch.int32, device=dev)
         self.timesteps = self.scheduler.timesteps.to(dev, torch.float32).contiguous()
         self.sigmas = self.scheduler.sigmas.to(dev, torch.float32).contiguous()
@@ -52,8 +60,15 @@ class AnimateDiffDenoiser:
         self.graph = None
 
     def set_prompt_embeds(self, cond_embeds, cond_pooled, uncond_embeds=None, uncond_pooled=None):
-        """(1, L, D) text states and (1, P) pooled embeds per branch (encode_prompt output)."""
+        """(1 or num_clips, L, D) text states and (1 or num_clips, P) pooled embeds per branch
+        (encode_prompt output).  UNet batch order: [uncond clips..., cond clips...]."""
         dev = self.device
+        n = self.nclips
+
+        def per_clip(t):
+            return t if t is None or t.shape[0] == n else t.expand(n, *t.shape[1:])
+        cond_embeds, cond_pooled = per_clip(cond_embeds), per_clip(cond_pooled)
+        uncond_embeds, uncond_pooled = per_clip(uncond_embeds), per_clip(uncond_pooled)
         if self.cfg:
             enc = torch.cat([uncond_embeds, cond_embeds], 0)
             pooled = torch.cat([uncond_pooled, cond_pooled], 0)
@@ -63,15 +78,15 @@ class AnimateDiffDenoiser:
         self.pooled = pooled.to(dev, BF16).contiguous()
         # SDXL time ids (inference_animatediff.py:81-85)
         tid = torch.tensor([self.height, self.width, 0, 0, self.height, self.width], dtype=torch.float32)
-        self.time_ids = tid.unsqueeze(0).repeat(self.ncopy, 1).to(dev).contiguous()
+        self.time_ids = tid.unsqueeze(0).repeat(self.ncopy * n, 1).to(dev).contiguous()
         self.graph = None
 
     def _step(self):
-        B = self.ncopy
-        K.pack_latents(self.lat, self.x, sigmas=self.sigmas, step_idx=self.step_idx, ncopy=B)
+        B = self.ncopy * self.nclips
+        K.pack_latents(self.lat, self.x, sigmas=self.sigmas, step_idx=self.step_idx, ncopy=self.ncopy)
         emb = self.unet.embed(self.timesteps, self.pooled, self.time_ids, B, step_idx=self.step_idx)
-        noise = self.unet.forward_tokens(self.x, B, self.F, self.h, self.w, emb, self.enc)
-        K.euler_cfg_step(noise, self.lat, self.sigmas, self.step_idx, guidance=self.guidance, ncopy=B)
+        noise = self.unet.forward_tokens(self.x, B, self.F, self.h, self.w, emb, self.enc, shard=self.shard)
+        K.euler_cfg_step(noise, self.lat, self.sigmas, self.step_idx, guidance=self.guidance, ncopy=self.ncopy)
         K.step_advance(self.step_idx)
 
     def capture(self):
@@ -91,18 +106,27 @@ class AnimateDiffDenoiser:
         self.step_idx.zero_()
 
     def set_latents(self, latents):
-        self.lat.copy_(latents.to(self.device, torch.float32).reshape(self.lat.shape))
+        """latents: (num_clips, C, F_total, h, w) for whole clips (this rank keeps its frames) or
+        (num_clips, C, F_local, h, w)."""
+        lat = latents.to(self.device, torch.float32)
+        if lat.dim() == 5 and lat.shape[2] == self.F_total and self.F != self.F_total:
+            lat = lat[:, :, self.f0:self.f0 + self.F]
+        self.lat.copy_(lat.reshape(self.lat.shape))
         self.step_idx.zero_()
 
     def init_latents(self, seed: int = 42):
-        """randn((1,4,F,h,w), generator=seed) * init_noise_sigma (inference_animatediff.py:88-95)."""
+        """randn((1,4,F,h,w), generator=seed) * init_noise_sigma (inference_animatediff.py:88-95); with
+        frame sharding every rank draws the whole clip and keeps its frames."""
         g = torch.Generator(device="cpu").manual_seed(seed)
-        lat = torch.randn(self.lat.shape, generator=g) * self.scheduler.init_noise_sigma
+        shape = (self.nclips, self.lat.shape[1], self.F_total, self.h, self.w)
+        lat = torch.randn(shape, generator=g) * self.scheduler.init_noise_sigma
         self.set_latents(lat)
         return lat
 
     def run_steps(self, n: Optional[int] = None):
         n = self.num_steps if n is None else n
+        if self.shard is not None and not self.shard.graph_capturable:
+            self.use_graph = False
         if self.use_graph and self.graph is None:
             self.capture()
         for _ in range(n):

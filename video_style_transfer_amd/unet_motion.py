@@ -21,6 +21,7 @@ Block semantics (diffusers ~0.30, restated in oracle/unet.py with citations):
 """
 from __future__ import annotations
 
+import dataclasses
 from dataclasses import dataclass
 from typing import Optional
 
@@ -118,6 +119,7 @@ class FwdCtx:
     emb_silu: torch.Tensor  # [B, T] bf16, SiLU(time + add embedding)
     enc: Optional[torch.Tensor]  # [B, L, D] bf16 text states
     cross_kwargs: dict
+    shard: Optional[object] = None  # frame_shard.FrameShard when the clip's frames span ranks (F is per rank)
 
 
 # --------------------------------------------------------------------------------------- blocks
@@ -227,10 +229,27 @@ class MotionModule(nn.Module):
 
     def run(self, x, nimg, H, W, ctx):
         HW = H * W
-        h = self.norm.run(x, nimg // ctx.F, ctx.F * HW)  # statistics over every frame of a clip
+        shard = ctx.shard
+        if shard is None or shard.world == 1:
+            h = self.norm.run(x, nimg // ctx.F, ctx.F * HW)  # statistics over every frame of a clip
+            h = self.proj_in.run(h)
+            for blk in self.transformer_blocks:
+                h = blk.run(h, nimg, HW, ctx)
+            return self.proj_out.run(h, residual=x)
+        # frames of each clip spread over ranks (frame_shard.py): clip-wide GN statistics by
+        # all-reduce, frame-axis work on a pixel shard holding every frame
+        Fl, P = ctx.F, shard.world
+        B, G, C = nimg // Fl, self.norm.num_groups, x.shape[1]
+        sums = K.group_norm_sums(x, B, Fl * HW, G)
+        shard.all_reduce_(sums)
+        h = K.group_norm_apply_sums(x, B, Fl * HW, G, self.norm.eps, f32(self.norm.weight), f32(self.norm.bias),
+                                    sums, float(Fl * P * HW * (C // G)))
         h = self.proj_in.run(h)
+        h = shard.to_pixels(h, B, Fl, HW)
+        tctx = dataclasses.replace(ctx, F=Fl * P)
         for blk in self.transformer_blocks:
-            h = blk.run(h, nimg, HW, ctx)
+            h = blk.run(h, B * Fl * P, HW // P, tctx)
+        h = shard.to_frames(h, B, Fl, HW)
         return self.proj_out.run(h, residual=x)
 
 
@@ -432,9 +451,10 @@ class UNetMotionModel(nn.Module):
         return K.silu(emb, out=out)
 
     # ---- core (NHWC tokens) -----------------------------------------------------------------
-    def forward_tokens(self, x, B, F, h, w, emb_silu, enc, cross_kwargs=None):
-        """x: [B*F*h*w, in_channels] bf16 -> noise prediction [B*F*h*w, out_channels] bf16."""
-        ctx = FwdCtx(B, F, emb_silu, enc, cross_kwargs or {})
+    def forward_tokens(self, x, B, F, h, w, emb_silu, enc, cross_kwargs=None, shard=None):
+        """x: [B*F*h*w, in_channels] bf16 -> noise prediction [B*F*h*w, out_channels] bf16.
+        With `shard` (frame_shard.FrameShard), F is this rank's frames of each clip."""
+        ctx = FwdCtx(B, F, emb_silu, enc, cross_kwargs or {}, shard)
         nimg = B * F
         H, W = h, w
         x = self.conv_in.run(x, nimg, H, W)
@@ -449,8 +469,9 @@ class UNetMotionModel(nn.Module):
         return self.conv_out.run(x, nimg, H, W)
 
     def forward(self, sample, timestep, encoder_hidden_states, timestep_cond=None, attention_mask=None,
-                cross_attention_kwargs=None, added_cond_kwargs=None, return_dict=True, **kwargs):
-        """diffusers UNetMotionModel.forward signature (inference_animatediff.py:110-121)."""
+                cross_attention_kwargs=None, added_cond_kwargs=None, return_dict=True, frame_shard=None, **kwargs):
+        """diffusers UNetMotionModel.forward signature (inference_animatediff.py:110-121).  With
+        `frame_shard` (frame_shard.FrameShard) `sample` holds this rank's frames of each clip."""
         if not sample.is_cuda:
             raise K._lib.VstError("UNetMotionModel: sample is on CPU; the HIP path has no CPU fallback")
         B, Cin, F, h, w = sample.shape
@@ -466,6 +487,6 @@ class UNetMotionModel(nn.Module):
         enc = encoder_hidden_states.to(dev, BF16).contiguous()
         x = torch.empty(B * F * h * w, Cin, dtype=BF16, device=dev)
         K.pack_latents(sample.float().contiguous(), x)
-        y = self.forward_tokens(x, B, F, h, w, emb_silu, enc, cross_attention_kwargs)
+        y = self.forward_tokens(x, B, F, h, w, emb_silu, enc, cross_attention_kwargs, shard=frame_shard)
         out = y.view(B, F, h, w, -1).permute(0, 4, 1, 2, 3).contiguous().to(sample.dtype)
         return UNetMotionOutput(out) if return_dict else (out,)
