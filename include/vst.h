@@ -29,7 +29,8 @@ extern "C" {
 int vst_gemm(const void* A, int lda, const void* A2, int lda2, int K1, const void* W, int ldw, int M, int N, int K,
              const float* bias, const float* row_bias, int row_bias_div, int ld_row_bias, const void* R, int ldr,
              void* C, int ldc, int epilogue, void* stream);
-/* Same, with the tile (0 auto, 1 = 128x128, 2 = 128x64, 3 = 256x256, 4 = 256x128) and split-K (0 auto, >= 1 forced) choice and a
+/* Same, with the tile (0 auto, 1 = 128x128, 2 = 128x64, 3 = 256x256, 4 = 256x128, 5 = skinny N <= 64
+ * without epilogue: the UnZipLoRA down-projection) and split-K (0 auto, >= 1 forced) choice and a
  * caller-owned fp32 workspace for split-K slabs (NULL / too small disables split-K). */
 int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int K1, const void* W, int ldw, int M, int N, int K,
                 const float* bias, const float* row_bias, int row_bias_div, int ld_row_bias, const void* R, int ldr,

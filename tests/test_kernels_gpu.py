@@ -45,7 +45,21 @@ def test_gemm_bias_residual(cuda, K, M, N, Kd):
     check(out, ref, name="gemm")
 
 
-@pytest.mark.parametrize("tile,splits", [(1, 1), (2, 1), (1, 3), (2, 5), (0, 0), (3, 1), (4, 1)])
+@pytest.mark.parametrize("M,N,Kd,tile", [(8192, 32, 1280, 0), (32768, 64, 640, 0), (1030, 48, 640, 5),
+                                         (2048, 16, 2048, 0), (100, 40, 96, 5), (4099, 64, 1344, 0)])
+def test_gemm_skinny_lora_down(cuda, K, M, N, Kd, tile):
+    g = torch.Generator().manual_seed(M + N)
+    x, w = rnd(M, Kd, gen=g), rnd(N, Kd, scale=Kd ** -0.5, gen=g)
+    K.GEMM_POLICY.update(tile=tile, splits=0)
+    try:
+        assert K.gemm_kernel_name(M, N, Kd, 0) == "gemm_skinny"
+        out = K.linear(x.to(cuda), w.to(cuda), None, kind="gemm_lora_down")
+    finally:
+        K.GEMM_POLICY.update(tile=0, splits=0)
+    check(out, x.float() @ w.float().t(), name="gemm_skinny")
+
+
+@pytest.mark.parametrize("tile,splits", [(1, 1), (2, 1), (1, 3), (2, 5), (0, 0), (3, 1), (4, 1), (6, 1), (6, 3)])
 @pytest.mark.parametrize("geglu", [False, True])
 def test_gemm_tile_and_splitk_variants(cuda, K, tile, splits, geglu):
     g = torch.Generator().manual_seed(tile * 10 + splits)
@@ -74,7 +88,7 @@ def test_gemm_tile_and_splitk_variants(cuda, K, tile, splits, geglu):
     check(out, ref, name=f"gemm t{tile} s{splits} geglu={geglu}")
 
 
-@pytest.mark.parametrize("tile,splits", [(2, 1), (1, 4), (2, 3), (3, 1), (4, 1)])
+@pytest.mark.parametrize("tile,splits", [(2, 1), (1, 4), (2, 3), (3, 1), (4, 1), (6, 1), (6, 2)])
 def test_conv_tile_and_splitk_variants(cuda, K, tile, splits):
     g = torch.Generator().manual_seed(31 + splits)
     n, C1, C2, Co, H, W = 2, 128, 64, 192, 8, 8

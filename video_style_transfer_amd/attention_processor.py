@@ -118,7 +118,7 @@ class AnimateDiffAttnProcessor2_0:
             if batch % be:
                 raise ValueError(f"encoder batch {be} does not divide hidden batch {batch}")
             q = run_ops(x, build_ops([attn.to_q], s))
-            kv = run_ops(enc.reshape(be * L, D), build_ops([attn.to_k, attn.to_v], s))
+            kv = _text_kv(attn, enc, s)
             if hd != 64:
                 raise NotImplementedError("spatial cross-attention kernel is specialised for head_dim 64 (SDXL)")
             o = K.spatial_attention(q, kv[:, :inner], kv[:, inner:], batch, heads, N, L, batch // be, scale=hd ** -0.5)
@@ -128,6 +128,27 @@ class AnimateDiffAttnProcessor2_0:
         if input_ndim == 4:
             out = out.transpose(-1, -2).reshape(b4, c4, h4, w4)
         return _finish(attn, out, hidden_states)
+
+
+def _text_kv(attn, enc, s):
+    """Cross-attention K/V of the text states (to_k/to_v + LoRA on encoder_hidden_states).
+
+    They depend only on the prompt and the weights, not on the latents, so across the 50 denoise
+    steps of a clip they are projected once: cached on the module and keyed on the text tensor
+    object (weakref + in-place version) and on the projection operands (build_ops is itself keyed
+    on the parameter versions, LoRA scale and mode).  Inside a captured step graph the cached
+    buffer is simply read."""
+    import weakref
+    ops = build_ops([attn.to_k, attn.to_v], s)
+    c = attn.__dict__.get("_vst_text_kv")
+    if c is not None:
+        ref, ver, ops_c, kv = c
+        if ref() is enc and ver == enc._version and ops_c is ops:
+            return kv
+    be, L, D = enc.shape
+    kv = run_ops(enc.reshape(be * L, D), ops)
+    attn.__dict__["_vst_text_kv"] = (weakref.ref(enc), enc._version, ops, kv)
+    return kv
 
 
 def _generic_attention(qkv, batch, heads, N):

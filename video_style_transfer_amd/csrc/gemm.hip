@@ -313,6 +313,87 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
 
 // sum the split-K slabs and apply the epilogue.  geglu: slab columns are the interleaved
 // [h(64) | g(64)] blocks; each thread produces 8 output columns.
+// Skinny GEMM for the UnZipLoRA down-projection u = x · Acatᵀ (N = padded 2r·projections <= 64,
+// no epilogue): memory-bound on reading x once.  One wave owns 16 rows and all N columns; every
+// global load is fragment-shaped (lane l reads 16 B of row l&15 at k-chunk l>>4, which IS the
+// 16x16x32 MFMA operand layout), so there is no LDS stage, no split-K slab and one launch.  The
+// K loop keeps SK k-steps of loads in flight (register double buffer).  W (Acat) is small and
+// L2-resident; out-of-range rows / columns / K read as zero through the buffer range check.
+template <int NJ>
+__global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs p) {
+  constexpr int SK = 4;  // k32 steps per load group
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int m0 = blockIdx.x * 64 + w * 16;
+  const auto ra = make_rsrc(p.A1, p.a1_bytes);
+  const auto rw = make_rsrc(p.Wt, p.w_bytes);
+  const int r = lane & 15, kc = (lane >> 4) * 8;
+  const int arow = m0 + r;
+  const int abase = arow < p.M ? arow * p.lda1 * 2 : -1;
+  int wbase[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) wbase[j] = (16 * j + r) < p.N ? (16 * j + r) * p.ldw * 2 : -1;
+  f32x4 acc[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (p.K + 31) / 32;
+  u32x4 a0[SK], b0[SK][NJ], a1[SK], b1[SK][NJ];
+  auto load = [&](u32x4 (&a)[SK], u32x4 (&b)[SK][NJ], int ks) {
+#pragma unroll
+    for (int t = 0; t < SK; ++t) {
+      const int k = (ks + t) * 32 + kc;
+      const bool kin = k < p.K;
+      a[t] = buf_load16(ra, (abase >= 0 && kin) ? abase + k * 2 : kOOB);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) b[t][j] = buf_load16(rw, (wbase[j] >= 0 && kin) ? wbase[j] + k * 2 : kOOB);
+    }
+  };
+  auto compute = [&](u32x4 (&a)[SK], u32x4 (&b)[SK][NJ]) {
+#pragma unroll
+    for (int t = 0; t < SK; ++t)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8*>(&b[t][j]),
+                                                         *reinterpret_cast<bf16x8*>(&a[t]), acc[j], 0, 0, 0);
+  };
+  load(a0, b0, 0);
+  for (int ks = 0; ks < nk; ks += 2 * SK) {
+    if (ks + SK < nk) load(a1, b1, ks + SK);
+    compute(a0, b0);
+    if (ks + SK >= nk) break;
+    if (ks + 2 * SK < nk) load(a0, b0, ks + 2 * SK);
+    compute(a1, b1);
+  }
+  // acc[j][e] = C[m0 + (lane&15)][16j + 4(lane>>4) + e]
+  const int m = m0 + r;
+  if (m >= p.M) return;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int n = 16 * j + 4 * (lane >> 4);
+    if (n >= p.N) continue;
+    bf16_t* dst = p.C + (size_t)m * p.ldc + n;
+    if (n + 4 <= p.N) {
+      u32x2 v;
+      v[0] = pack2bf(acc[j][0], acc[j][1]);
+      v[1] = pack2bf(acc[j][2], acc[j][3]);
+      *reinterpret_cast<u32x2*>(dst) = v;
+    } else {
+      for (int e = 0; e < p.N - n; ++e) dst[e] = f2bf(acc[j][e]);
+    }
+  }
+}
+
+static int launch_skinny(const GemmArgs& a, hipStream_t s) {
+  const dim3 grid((a.M + 63) / 64);
+  switch ((a.N + 15) / 16) {
+    case 1: hipLaunchKernelGGL(gemm_skinny_kernel<1>, grid, dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(gemm_skinny_kernel<2>, grid, dim3(256), 0, s, a); break;
+    case 3: hipLaunchKernelGGL(gemm_skinny_kernel<3>, grid, dim3(256), 0, s, a); break;
+    case 4: hipLaunchKernelGGL(gemm_skinny_kernel<4>, grid, dim3(256), 0, s, a); break;
+    default: return VST_ERR_ARG;
+  }
+  return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+}
+
 __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(GemmArgs p, int geglu) {
   const int Nout = geglu ? p.N / 2 : p.N;
   const int CPR = (Nout + 7) / 8;
@@ -400,8 +481,9 @@ static void choose(int M, int N, int K, int geglu, int conv, size_t ws_bytes, in
     else if (!geglu && (N <= 64 || K <= 320)) tile = 2;
     else tile = 1;
   }
-  if (geglu && tile == 2) tile = 1;
-  const int tiles = tile == 1 ? t128 : tile == 2 ? t64 : tile == 3 ? t256 : t256n;
+  if (geglu && (tile == 2 || tile == 6)) tile = 1;
+  const int t160 = mb * ((N + 159) / 160);
+  const int tiles = tile == 1 ? t128 : tile == 2 ? t64 : tile == 3 ? t256 : tile == 6 ? t160 : t256n;
   if (splits == 0) {
     splits = 1;
     if (tiles < kCUs && nk32 >= 8) {
@@ -430,6 +512,7 @@ static int gemm_ablate_env() {
 
 static int run_gemm(GemmArgs& a, int amode, int geglu, int tile, int splits, hipStream_t s) {
   a.ablate = gemm_ablate_env();
+  if (tile == 5) return launch_skinny(a, s);
   if (amode == 2) {  // scalar-gather conv (conv_in): register-staged kernel, no split
     a.splits = 1;
     return launch_one<2, 0, 64>(a, s, 1);
@@ -461,15 +544,19 @@ extern "C" size_t vst_gemm_workspace_bytes(int M, int N, int K) {
 // symbol rocprofv3 reports), so per-launch timings can be attributed to kernels.  kind: 0 linear,
 // 1 GEGLU linear, 2 vectorized conv, 3 scalar-gather conv.  Returns a static string.
 extern "C" const char* vst_gemm_kernel_name(int M, int N, int K, int kind, int tile, int splits, size_t ws_bytes) {
-  static const char* names[4][3] = {
+  static const char* names[6][3] = {
       {"gemm_ring<128x128>", "gemm_ring<128x128,geglu>", "gemm_ring<128x128,conv>"},
       {"gemm_ring<128x64>", "gemm_ring<128x64,geglu>", "gemm_ring<128x64,conv>"},
       {"gemm_ring<256x256>", "gemm_ring<256x256,geglu>", "gemm_ring<256x256,conv>"},
-      {"gemm_ring<256x128>", "gemm_ring<256x128,geglu>", "gemm_ring<256x128,conv>"}};
-  static const char* split_names[4] = {"gemm_ring<128x128,splitk>", "gemm_ring<128x64,splitk>",
-                                       "gemm_ring<256x256,splitk>", "gemm_ring<256x128,splitk>"};
+      {"gemm_ring<256x128>", "gemm_ring<256x128,geglu>", "gemm_ring<256x128,conv>"},
+      {"", "", ""},
+      {"gemm_ring<256x160>", "", "gemm_ring<256x160,conv>"}};
+  static const char* split_names[6] = {"gemm_ring<128x128,splitk>", "gemm_ring<128x64,splitk>",
+                                       "gemm_ring<256x256,splitk>", "gemm_ring<256x128,splitk>", "",
+                                       "gemm_ring<256x160,splitk>"};
   if (kind == 3) return "gemm_kernel<conv_in>";
-  if (kind < 0 || kind > 3 || tile < 0 || tile > 4 || splits < 0) return "";
+  if (kind == 0 && (tile == 5 || (tile == 0 && N <= 64 && M >= 1024))) return "gemm_skinny";  // no-epilogue calls
+  if (kind < 0 || kind > 3 || tile < 0 || tile > 6 || tile == 5 || splits < 0) return "";
   choose(M, N, K, kind == 1, kind == 2, ws_bytes, tile, splits);
   if (splits > 1) return split_names[tile - 1];
   return names[tile - 1][kind == 2 ? 2 : kind];
@@ -489,7 +576,10 @@ extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int
   if (epilogue == 1 && (N % 128)) return VST_ERR_ARG;
   if (R && (ldr & 7)) return VST_ERR_ARG;
   if (row_bias && row_bias_div <= 0) return VST_ERR_ARG;
-  if (tile < 0 || tile > 4 || splits < 0) return VST_ERR_ARG;
+  if (tile < 0 || tile > 6 || splits < 0) return VST_ERR_ARG;
+  if (tile == 6 && epilogue == 1) return VST_ERR_ARG;
+  const bool skinny_ok = N <= 64 && !A2 && !bias && !row_bias && !R && epilogue == 0;
+  if (tile == 5 && !skinny_ok) return VST_ERR_ARG;
   GemmArgs a{};
   a.A1 = (const bf16_t*)A; a.A2 = (const bf16_t*)A2; a.lda1 = lda; a.lda2 = lda2; a.K1 = K1;
   a.Wt = (const bf16_t*)W; a.ldw = ldw; a.M = M; a.N = N; a.K = K;
@@ -501,6 +591,8 @@ extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int
   a.w_bytes = clamp_bytes(((size_t)(N - 1) * ldw + K) * 2);
   a.r_bytes = R ? clamp_bytes(((size_t)(M - 1) * ldr + N) * 2) : 0;
   a.C1 = 0; a.C2 = 0; a.stride = 1; a.up = 0;
+  if (tile == 0 && skinny_ok && M >= 1024) tile = 5;  // LoRA down-projection: skinny kernel
+  if (tile == 5) return run_gemm(a, 0, 0, 5, 1, (hipStream_t)stream);
   choose(M, N, K, epilogue == 1, 0, workspace ? ws_bytes : 0, tile, splits);
   return run_gemm(a, 0, epilogue == 1, tile, splits, (hipStream_t)stream);
 }
@@ -522,7 +614,7 @@ extern "C" int vst_conv3x3_ex(const void* x1, int C1, const void* x2, int C2, in
   if (!x1 || !Wt || !out || nimg <= 0 || H <= 0 || W <= 0 || Cout <= 0) return VST_ERR_ARG;
   if (stride != 1 && stride != 2) return VST_ERR_ARG;
   if (upsample && stride != 1) return VST_ERR_ARG;
-  if (tile < 0 || tile > 4 || splits < 0) return VST_ERR_ARG;
+  if (tile < 0 || tile > 6 || tile == 5 || splits < 0) return VST_ERR_ARG;
   const int Ct = C1 + (x2 ? C2 : 0);
   const bool vec = (Ct % BK == 0) && (C1 % 8 == 0);
   if (x2 && !vec) return VST_ERR_ARG;

@@ -40,17 +40,20 @@ struct RingCfg {
   static constexpr int STAGE = A_BYTES + B_BYTES;
   static constexpr int A_PIECES = A_BYTES / 1024 / NWAVES;  // per wave per tile
   static constexpr int B_PIECES = B_BYTES / 1024 / NWAVES;
-  static constexpr int DPT = A_PIECES + B_PIECES;            // DMA instructions per thread per tile
+  // B tiles whose 1-KiB pieces do not split evenly over the waves (BN = 160: 10 pieces, 8 waves):
+  // waves wid < B_EXTRA load one more piece each, so their DMA count per tile is DPT, the others'
+  // DPT - 1 (wait_tiles takes the wave's own count).
+  static constexpr int B_EXTRA = (B_BYTES / 1024) % NWAVES;
+  static constexpr int DPT = A_PIECES + B_PIECES + (B_EXTRA ? 1 : 0);  // max DMA per thread per tile
   static constexpr int EPI_BYTES = BM * (BN * 2 + 16);  // bf16 tile staged for the epilogue
   static constexpr int LDS = STAGES * STAGE > EPI_BYTES ? STAGES * STAGE : EPI_BYTES;
-  static_assert(A_BYTES % (1024 * NWAVES) == 0 && B_BYTES % (1024 * NWAVES) == 0, "piece split");
+  static_assert(A_BYTES % (1024 * NWAVES) == 0 && B_BYTES % 1024 == 0, "piece split");
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
-// wait until at most `tiles` tiles' DMA (DPT instructions each) are still outstanding
-template <class Cfg>
-__device__ __forceinline__ void wait_tiles(int tiles) {
-  constexpr int D = Cfg::DPT;
+// wait until at most `tiles` tiles' DMA (D instructions each for this wave) are still outstanding
+template <int D>
+__device__ __forceinline__ void wait_tiles_d(int tiles) {
   switch (tiles) {
     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D) : "memory"); break;
@@ -58,6 +61,16 @@ __device__ __forceinline__ void wait_tiles(int tiles) {
     case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * D) : "memory"); break;
     case 4: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * D) : "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * D) : "memory"); break;
+  }
+}
+
+template <class Cfg>
+__device__ __forceinline__ void wait_tiles(int tiles, bool full) {
+  if constexpr (Cfg::B_EXTRA == 0) {
+    wait_tiles_d<Cfg::DPT>(tiles);
+  } else {
+    if (full) wait_tiles_d<Cfg::DPT>(tiles);
+    else wait_tiles_d<Cfg::DPT - 1>(tiles);
   }
 }
 
@@ -118,12 +131,13 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
       rowA[q] = -1; oyv[q] = oxv[q] = 0;
     }
   }
-  int rowB[Cfg::B_PIECES];
+  int rowB[Cfg::B_PIECES + 1];
 #pragma unroll
-  for (int q = 0; q < Cfg::B_PIECES; ++q) {
-    const int n = n0 + 16 * (q * Cfg::NWAVES + wid) + prow;
+  for (int q = 0; q <= Cfg::B_PIECES; ++q) {
+    const int n = n0 + 16 * (q * Cfg::NWAVES + wid) + prow;  // q == B_PIECES: the extra piece
     rowB[q] = n < p.N ? n : -1;
   }
+  const bool has_extra = wid < Cfg::B_EXTRA;  // wave-uniform
   const int Ctot = p.C1 + p.C2;
   const int nk_all = (p.K + RBK - 1) / RBK;
   int kt0 = 0, kt1 = nk_all;
@@ -145,6 +159,10 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
 #pragma unroll
     for (int q = 0; q < Cfg::B_PIECES; ++q)
       offs[q] = (rowB[q] >= 0 && k < p.K) ? (rowB[q] * p.ldw + k) * 2 : kOOB;
+    if constexpr (Cfg::B_EXTRA != 0) {
+      const int q = Cfg::B_PIECES;
+      offs[Cfg::DPT - 1] = (rowB[q] >= 0 && k < p.K) ? (rowB[q] * p.ldw + k) * 2 : kOOB;
+    }
     if (AMODE == 0) {
       a_second = k0 >= p.K1;
       if (!a_second) {
@@ -182,7 +200,9 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
   };
   auto dma_piece = [&](int stage, int idx) {  // idx: compile-time after unrolling
     char* As = smem + stage * Cfg::STAGE;
-    if (idx < Cfg::B_PIECES) {
+    if (Cfg::B_EXTRA != 0 && idx == Cfg::DPT - 1) {
+      if (has_extra) dma16(rw, As + Cfg::A_BYTES + (Cfg::B_PIECES * Cfg::NWAVES + wid) * 1024, offs[idx]);
+    } else if (idx < Cfg::B_PIECES) {
       dma16(rw, As + Cfg::A_BYTES + (idx * Cfg::NWAVES + wid) * 1024, offs[idx]);
     } else {
       const int q = idx - Cfg::B_PIECES;
@@ -253,7 +273,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
 #pragma unroll
     for (int s = 0; s < S - 1; ++s)
       if (s < nk) issue(kt0 + s, s);
-    wait_tiles<Cfg>(max(0, min(nk - 1, S - 2) - 1));  // own DMA of tiles 0 and 1 landed
+    wait_tiles<Cfg>(max(0, min(nk - 1, S - 2) - 1), has_extra);  // own DMA of tiles 0 and 1 landed
     __builtin_amdgcn_s_barrier();
     if (nk > 0) load_into(fa0, fb0, 0);
     if (late) __builtin_amdgcn_s_barrier();
@@ -263,7 +283,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
       wrs = wrs + 1 == S ? 0 : wrs + 1;
       if (it + 1 < nk) load_into(na, nb, nrd);
       nrd = nrd + 1 == S ? 0 : nrd + 1;
-      if (it + 2 < nk) wait_tiles<Cfg>(no_dma ? 0 : min(nk - 1, it + S - 1) - (it + 2));
+      if (it + 2 < nk) wait_tiles<Cfg>(no_dma ? 0 : min(nk - 1, it + S - 1) - (it + 2), has_extra);
       __builtin_amdgcn_s_barrier();
       mfmas(ca, cb);
       __builtin_amdgcn_s_barrier();
@@ -278,7 +298,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
 #pragma unroll
   for (int s = 0; s < S - 1; ++s)
     if (s < nk) issue(kt0 + s, s);
-  wait_tiles<Cfg>(min(nk, S - 1) - 1);
+  wait_tiles<Cfg>(min(nk, S - 1) - 1, has_extra);
   __builtin_amdgcn_s_barrier();
 
   // fragments of the current k-tile live in registers: all MI + NJ ds_read_b128 are issued
@@ -291,7 +311,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
   int wrs = S - 1, nrd = 1 % S;  // next stage to fill / stage holding tile it+1
   auto step = [&](int it, FragA& ca, FragB& cb, FragA& na, FragB& nb) {
     if (it + 1 < nk) {
-      wait_tiles<Cfg>(no_dma ? 0 : min(nk - 1, it + S - 2) - (it + 1));
+      wait_tiles<Cfg>(no_dma ? 0 : min(nk - 1, it + S - 2) - (it + 1), has_extra);
       __builtin_amdgcn_s_barrier();
     }
     if (it + S - 1 < nk && !no_dma) issue(kt0 + it + S - 1, wrs);
@@ -365,24 +385,24 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
     const auto rr = make_rsrc(p.R ? p.R : p.Wt, p.R ? p.r_bytes : 0u);
     if constexpr (EPI == 0) {
       constexpr int CPR = BN / 8;                 // 16-B chunks per row
-      constexpr int RSTEP = Cfg::THREADS / CPR;   // rows advanced per item
-      constexpr int ITEMS = BM / RSTEP;
-      static_assert(Cfg::THREADS % CPR == 0 && BM % RSTEP == 0, "item split");
-      const int cc = tid % CPR, row0 = tid / CPR;
-      const int n = n0 + cc * 8;
-      const int nv = min(8, p.N - n);
+      constexpr int TOT = BM * CPR;
+      constexpr int ITEMS = (TOT + Cfg::THREADS - 1) / Cfg::THREADS;
       u32x4 res[ITEMS];
       if (p.R) {
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k) {
-          const int m = m0 + row0 + k * RSTEP;
-          res[k] = buf_load16(rr, (m < p.M && nv == 8) ? (m * p.ldr + n) * 2 : kOOB);
+          const int idx = tid + k * Cfg::THREADS;
+          const int row = idx / CPR, n = n0 + (idx - row * CPR) * 8, m = m0 + row;
+          res[k] = buf_load16(rr, (idx < TOT && m < p.M && n + 8 <= p.N) ? (m * p.ldr + n) * 2 : kOOB);
         }
       }
 #pragma unroll
       for (int k = 0; k < ITEMS; ++k) {
-        const int row = row0 + k * RSTEP, m = m0 + row;
-        if (m >= p.M || nv <= 0) continue;
+        const int idx = tid + k * Cfg::THREADS;
+        const int row = idx / CPR, cc = idx - row * CPR;
+        const int m = m0 + row, n = n0 + cc * 8;
+        const int nv = min(8, p.N - n);
+        if (idx >= TOT || m >= p.M || nv <= 0) continue;
         float v[8];
         unpack8(*reinterpret_cast<const u32x4*>(smem + row * LROW + cc * 16), v);
         if (p.rbias) {
@@ -440,6 +460,7 @@ using Cfg256x256 = RingCfg<256, 256, 2, 4, 5>;  // 160 KiB, 1 WG/CU
 using Cfg256x128 = RingCfg<256, 128, 4, 2, 6>;  // 144 KiB, 1 WG/CU
 using Cfg128x128 = RingCfg<128, 128, 2, 2, 5>;  //  80 KiB, 2 WG/CU
 using Cfg128x64 = RingCfg<128, 64, 2, 2, 6>;    //  72 KiB, 2 WG/CU
+using Cfg256x160 = RingCfg<256, 160, 4, 2, 5>;  // 130 KiB, 1 WG/CU: N = 320/640/960/1280/1920/3840 without waste
 
 template <class Cfg, int AMODE, int EPI>
 static int launch_ring_t(const GemmArgs& a, hipStream_t s, int splits) {
@@ -458,7 +479,10 @@ template <class Cfg>
 static int dispatch_cfg(const GemmArgs& a, int amode, int epi, hipStream_t s, int splits) {
   if (amode == 0) {
     if (epi == 0) return launch_ring_t<Cfg, 0, 0>(a, s, splits);
-    if (epi == 1) return launch_ring_t<Cfg, 0, 1>(a, s, splits);
+    if (epi == 1) {
+      if constexpr (Cfg::BN % 128 == 0) return launch_ring_t<Cfg, 0, 1>(a, s, splits);
+      return VST_ERR_ARG;  // GEGLU pairs 64 hidden + 64 gate columns per 128
+    }
     return launch_ring_t<Cfg, 0, 2>(a, s, splits);
   }
   if (epi == 0) return launch_ring_t<Cfg, 1, 0>(a, s, splits);
@@ -466,13 +490,14 @@ static int dispatch_cfg(const GemmArgs& a, int amode, int epi, hipStream_t s, in
   return VST_ERR_ARG;
 }
 
-// tile: 1 = 128x128, 2 = 128x64, 3 = 256x256, 4 = 256x128.  epi: 0 plain, 1 GEGLU, 2 split-K partial
+// tile: 1 = 128x128, 2 = 128x64, 3 = 256x256, 4 = 256x128, 6 = 256x160.  epi: 0 plain, 1 GEGLU, 2 split-K partial
 int launch_gemm_ring(const GemmArgs& a, int amode, int epi, int tile, int splits, hipStream_t s) {
   switch (tile) {
     case 1: return dispatch_cfg<Cfg128x128>(a, amode, epi, s, splits);
     case 2: return epi == 1 ? VST_ERR_ARG : dispatch_cfg<Cfg128x64>(a, amode, epi, s, splits);
     case 3: return dispatch_cfg<Cfg256x256>(a, amode, epi, s, splits);
     case 4: return dispatch_cfg<Cfg256x128>(a, amode, epi, s, splits);
+    case 6: return epi == 1 ? VST_ERR_ARG : dispatch_cfg<Cfg256x160>(a, amode, epi, s, splits);
     default: return VST_ERR_ARG;
   }
 }
