@@ -476,7 +476,8 @@ static void choose(int M, int N, int K, int geglu, int conv, size_t ws_bytes, in
   // implicit-GEMM convs (K = 9*Cin >= 2880) run best on 256x256; linears only when K is long
   // and N fills 256-wide tiles; short-K linears (K=320) want the extra parallelism of 128x64.
   if (tile == 0) {
-    if (conv && t256 >= kCUs / 2) tile = 3;
+    if (conv && N <= 64) tile = 2;  // conv_out (Cout = 4): narrow tiles, 4x less padded work
+    else if (conv && t256 >= kCUs / 2) tile = 3;
     else if (!conv && K >= 1280 && waste256 <= 0.1 && t256 >= kCUs / 2) tile = 3;
     else if (!geglu && (N <= 64 || K <= 320)) tile = 2;
     else tile = 1;

@@ -16,6 +16,8 @@
 // per 16-lane block) is bank-conflict free under CDNA4's b128 lane grouping
 // {0-3,12-15,20-27},{4-11,16-19,28-31},... .  Because the DMA image is lane-linear, the inverse
 // permutation is applied to each lane's SOURCE address (lane l fetches chunk (l&3) ^ G[(l>>4)&3]).
+#include <type_traits>
+
 #include "gemm_common.h"
 
 namespace vst {
@@ -147,55 +149,76 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
   }
   const int nk = kt1 - kt0;
 
-  // per-tile DMA plan: byte offsets of this thread's DPT pieces (B pieces first, then A) and
-  // which A source they read (wave-uniform per tile).  prep() is cheap VALU; the DMA
-  // instructions themselves are interleaved with the MFMA chain (dma_piece) so the matrix pipe
-  // never idles behind a burst of LDS-DMA issues.
+  // ---- incremental DMA addressing (keeps the load segment of each k-tile short) ----
+  // A piece's byte offset for k-tile kt is base + (k offset inside the current source run) * 2.
+  // Rows past M / N carry base kOOB: unsigned adds keep it beyond every buffer, so the hardware
+  // range check returns zeros.  Per-lane K checks are only needed when K is not a multiple of 32.
+  // Convs walk a (tap, channel) cursor one k-tile at a time (issue() is called for consecutive
+  // tiles) and recompute bases only when the tap or the concat source changes.
+  const bool ktail = (p.K & (RBK - 1)) != 0;
+  uint32_t bB[Cfg::B_PIECES + 1];
+#pragma unroll
+  for (int q = 0; q <= Cfg::B_PIECES; ++q)
+    bB[q] = rowB[q] >= 0 ? (uint32_t)(rowB[q] * p.ldw + lchunk * 8) * 2u : (uint32_t)kOOB;
+  uint32_t bA[Cfg::A_PIECES], bA2[Cfg::A_PIECES];
+  if (AMODE == 0) {
+#pragma unroll
+    for (int q = 0; q < Cfg::A_PIECES; ++q) {
+      bA[q] = rowA[q] >= 0 ? (uint32_t)(rowA[q] * p.lda1 + lchunk * 8) * 2u : (uint32_t)kOOB;
+      bA2[q] = rowA[q] >= 0 ? (uint32_t)(rowA[q] * p.lda2 + lchunk * 8) * 2u : (uint32_t)kOOB;
+    }
+  }
+  int c_tap = 0, c_ci = 0, run_ci0 = 0;  // conv cursor: next tile's tap and channel (of C1 + C2)
+  bool rebase_due = true;
+  if (AMODE == 1) {
+    const int k00 = kt0 * RBK;
+    c_tap = k00 / Ctot;
+    c_ci = k00 - c_tap * Ctot;
+  }
+  auto rebase = [&]() {
+    const int ky = c_tap / 3, kx = c_tap - 3 * (c_tap / 3);
+    const bool second = c_ci >= p.C1;
+    const int cs = second ? p.C2 : p.C1;
+    run_ci0 = second ? p.C1 : 0;
+#pragma unroll
+    for (int q = 0; q < Cfg::A_PIECES; ++q) {
+      int iy, ix;
+      bool ok = rowA[q] >= 0;
+      if (p.up) {
+        const int uy = oyv[q] + ky - 1, ux = oxv[q] + kx - 1;
+        ok = ok && uy >= 0 && uy < 2 * p.H && ux >= 0 && ux < 2 * p.W;
+        iy = uy >> 1; ix = ux >> 1;
+      } else {
+        iy = oyv[q] * p.stride + ky - 1; ix = oxv[q] * p.stride + kx - 1;
+        ok = ok && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+      }
+      bA[q] = ok ? (uint32_t)(((rowA[q] * p.H + iy) * p.W + ix) * cs + lchunk * 8) * 2u : (uint32_t)kOOB;
+    }
+  };
   int offs[Cfg::DPT];
   bool a_second = false;
   auto prep = [&](int kt) {
     const int k0 = kt * RBK;
-    const int k = k0 + lchunk * 8;
+    const uint32_t kb = (uint32_t)k0 * 2u;
+    const bool kin = !ktail || (k0 + lchunk * 8 < p.K);
 #pragma unroll
-    for (int q = 0; q < Cfg::B_PIECES; ++q)
-      offs[q] = (rowB[q] >= 0 && k < p.K) ? (rowB[q] * p.ldw + k) * 2 : kOOB;
-    if constexpr (Cfg::B_EXTRA != 0) {
-      const int q = Cfg::B_PIECES;
-      offs[Cfg::DPT - 1] = (rowB[q] >= 0 && k < p.K) ? (rowB[q] * p.ldw + k) * 2 : kOOB;
-    }
+    for (int q = 0; q < Cfg::B_PIECES; ++q) offs[q] = kin ? (int)(bB[q] + kb) : kOOB;
+    if constexpr (Cfg::B_EXTRA != 0) offs[Cfg::DPT - 1] = kin ? (int)(bB[Cfg::B_PIECES] + kb) : kOOB;
     if (AMODE == 0) {
-      a_second = k0 >= p.K1;
-      if (!a_second) {
+      a_second = k0 >= p.K1;  // K1 is a multiple of 64: a k-tile never straddles the sources
+      const uint32_t ka = a_second ? (uint32_t)(k0 - p.K1) * 2u : kb;
 #pragma unroll
-        for (int q = 0; q < Cfg::A_PIECES; ++q)
-          offs[Cfg::B_PIECES + q] = (rowA[q] >= 0 && k < p.K1) ? (rowA[q] * p.lda1 + k) * 2 : kOOB;
-      } else {
-        const int kk = k - p.K1;
-#pragma unroll
-        for (int q = 0; q < Cfg::A_PIECES; ++q)
-          offs[Cfg::B_PIECES + q] = (rowA[q] >= 0 && k < p.K) ? (rowA[q] * p.lda2 + kk) * 2 : kOOB;
-      }
+      for (int q = 0; q < Cfg::A_PIECES; ++q)
+        offs[Cfg::B_PIECES + q] = kin ? (int)((a_second ? bA2[q] : bA[q]) + ka) : kOOB;
     } else {
-      const int tap = k0 / Ctot;
-      const int ci0 = k0 - tap * Ctot;
-      const int ky = tap / 3, kx = tap - ky * 3;
-      a_second = ci0 >= p.C1;
-      const int cs = a_second ? p.C2 : p.C1;
-      const int ci = (a_second ? ci0 - p.C1 : ci0) + lchunk * 8;
+      if (rebase_due) rebase();
+      a_second = run_ci0 != 0;
+      const uint32_t kc = (uint32_t)(c_ci - run_ci0) * 2u;
 #pragma unroll
-      for (int q = 0; q < Cfg::A_PIECES; ++q) {
-        int iy, ix;
-        bool ok = rowA[q] >= 0 && tap < 9;
-        if (p.up) {
-          const int uy = oyv[q] + ky - 1, ux = oxv[q] + kx - 1;
-          ok = ok && uy >= 0 && uy < 2 * p.H && ux >= 0 && ux < 2 * p.W;
-          iy = uy >> 1; ix = ux >> 1;
-        } else {
-          iy = oyv[q] * p.stride + ky - 1; ix = oxv[q] * p.stride + kx - 1;
-          ok = ok && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
-        }
-        offs[Cfg::B_PIECES + q] = ok ? (((rowA[q] * p.H + iy) * p.W + ix) * cs + ci) * 2 : kOOB;
-      }
+      for (int q = 0; q < Cfg::A_PIECES; ++q) offs[Cfg::B_PIECES + q] = (int)(bA[q] + kc);
+      c_ci += RBK;
+      if (c_ci == Ctot) { c_ci = 0; ++c_tap; }
+      rebase_due = c_ci == 0 || (p.C2 > 0 && c_ci == p.C1);
     }
   };
   auto dma_piece = [&](int stage, int idx) {  // idx: compile-time after unrolling
@@ -279,11 +302,14 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
     if (late) __builtin_amdgcn_s_barrier();
     int wrs = S - 1, nrd = 1 % S;
     auto pp_step = [&](int it, FragA& ca, FragB& cb, FragA& na, FragB& nb) {
-      if (it + S - 1 < nk && !no_dma) issue(kt0 + it + S - 1, wrs);
+      const bool steady = it + S - 1 < nk;  // tile it+S-1 exists: issue it, keep S-3 tiles in flight
+      if (steady && !no_dma) issue(kt0 + it + S - 1, wrs);
       wrs = wrs + 1 == S ? 0 : wrs + 1;
       if (it + 1 < nk) load_into(na, nb, nrd);
       nrd = nrd + 1 == S ? 0 : nrd + 1;
-      if (it + 2 < nk) wait_tiles<Cfg>(no_dma ? 0 : min(nk - 1, it + S - 1) - (it + 2), has_extra);
+      // in the last S-1 tiles drain completely instead of counting (two wait forms, no dispatch chain)
+      if (steady && !no_dma) wait_tiles<Cfg>(S - 3, has_extra);
+      else if (it + 2 < nk) wait_tiles<Cfg>(0, has_extra);
       __builtin_amdgcn_s_barrier();
       mfmas(ca, cb);
       __builtin_amdgcn_s_barrier();
@@ -311,7 +337,9 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
   int wrs = S - 1, nrd = 1 % S;  // next stage to fill / stage holding tile it+1
   auto step = [&](int it, FragA& ca, FragB& cb, FragA& na, FragB& nb) {
     if (it + 1 < nk) {
-      wait_tiles<Cfg>(no_dma ? 0 : min(nk - 1, it + S - 2) - (it + 1), has_extra);
+      // tile it+1 must have landed: steady state leaves S-3 younger tiles in flight, the tail drains
+      if (it + S - 2 < nk && !no_dma) wait_tiles<Cfg>(S - 3, has_extra);
+      else wait_tiles<Cfg>(0, has_extra);
       __builtin_amdgcn_s_barrier();
     }
     if (it + S - 1 < nk && !no_dma) issue(kt0 + it + S - 1, wrs);
