@@ -470,16 +470,14 @@ static void choose(int M, int N, int K, int geglu, int conv, size_t ws_bytes, in
   const int nk = (K + BK - 1) / BK;
   const int mb = (M + 255) / 256;
   const int t256 = mb * ((N + 255) / 256), t256n = mb * ((N + 127) / 128);
-  const double waste256 = 1.0 - (double)N / (((N + 255) / 256) * 256);
   const int nk32 = (K + 31) / 32;  // ring kernel k-tiles
-  // Tile policy from tools/gemm_sweep.py on MI355X (UNet shapes at 16x512^2, CFG batch 2):
-  // implicit-GEMM convs (K = 9*Cin >= 2880) run best on 256x256; linears only when K is long
-  // and N fills 256-wide tiles; short-K linears (K=320) want the extra parallelism of 128x64.
+  // Tile policy from tools/gemm_sweep.py on MI355X (UNet shapes at 16x512^2, CFG batch 2): the
+  // 256x256 ping-pong ring wins every projection / FF / GEGLU / conv shape of the path that has at
+  // least a quarter-wave of tiles (it beats 128x128 and 256x160 even at 160 tiles on 256 CUs);
+  // tiny-M GEMMs (text states, temb) use 128x128 with split-K; conv_out (Cout = 4) 128x64.
   if (tile == 0) {
-    if (conv && N <= 64) tile = 2;  // conv_out (Cout = 4): narrow tiles, 4x less padded work
-    else if (conv && t256 >= kCUs / 2) tile = 3;
-    else if (!conv && K >= 1280 && waste256 <= 0.1 && t256 >= kCUs / 2) tile = 3;
-    else if (!geglu && (N <= 64 || K <= 320)) tile = 2;
+    if (conv && N <= 64) tile = 2;
+    else if (t256 >= kCUs / 4) tile = 3;
     else tile = 1;
   }
   if (geglu && (tile == 2 || tile == 6)) tile = 1;
@@ -487,7 +485,7 @@ static void choose(int M, int N, int K, int geglu, int conv, size_t ws_bytes, in
   const int tiles = tile == 1 ? t128 : tile == 2 ? t64 : tile == 3 ? t256 : tile == 6 ? t160 : t256n;
   if (splits == 0) {
     splits = 1;
-    if (tiles < kCUs && nk32 >= 8) {
+    if (tiles < kCUs / 2 && nk32 >= 8) {
       splits = std::min(std::min((2 * kCUs + tiles - 1) / tiles, nk32 / 4), 16);
       if (splits < 2) splits = 1;
     }
@@ -578,7 +576,6 @@ extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int
   if (R && (ldr & 7)) return VST_ERR_ARG;
   if (row_bias && row_bias_div <= 0) return VST_ERR_ARG;
   if (tile < 0 || tile > 6 || splits < 0) return VST_ERR_ARG;
-  if (tile == 6 && epilogue == 1) return VST_ERR_ARG;
   const bool skinny_ok = N <= 64 && !A2 && !bias && !row_bias && !R && epilogue == 0;
   if (tile == 5 && !skinny_ok) return VST_ERR_ARG;
   GemmArgs a{};
