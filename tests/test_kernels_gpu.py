@@ -59,7 +59,39 @@ def test_gemm_skinny_lora_down(cuda, K, M, N, Kd, tile):
     check(out, x.float() @ w.float().t(), name="gemm_skinny")
 
 
-@pytest.mark.parametrize("tile,splits", [(1, 1), (2, 1), (1, 3), (2, 5), (0, 0), (3, 1), (4, 1), (6, 1), (6, 3)])
+@pytest.mark.parametrize("M,N,Kd,K2", [(4096, 1280, 1280, 32), (4000, 1200, 640, 0), (8192, 1280, 2048, 64)])
+def test_gemm_underfilled_grids(cuda, K, M, N, Kd, K2):
+    """Tile counts that leave CUs idle under 256x256 (192x256 tiles; stream-K when VST_STREAMK=1)."""
+    g = torch.Generator().manual_seed(M + N + Kd)
+    x, x2 = rnd(M, Kd, gen=g), (rnd(M, K2, gen=g) if K2 else None)
+    w = rnd(N, Kd + K2, scale=(Kd + K2) ** -0.5, gen=g)
+    b = torch.randn(N, generator=g)
+    rb = torch.randn(M // 1000 + 1, N, generator=g)
+    r = rnd(M, N, gen=g)
+    name = K.gemm_kernel_name(M, N, Kd + K2, 0)
+    assert "192x256" in name or "streamk" in name, name
+    for _ in range(2):  # second launch (stream-K: flags must have been reset by the first)
+        out = K.linear(x.to(cuda), w.to(cuda), b.to(cuda), x2=None if x2 is None else x2.to(cuda),
+                       row_bias=rb.to(cuda), row_bias_div=1000, residual=r.to(cuda))
+        xx = x if x2 is None else torch.cat([x, x2], 1)
+        ref = xx.float() @ w.float().t() + b + rb.repeat_interleave(1000, 0)[:M] + r.float()
+        check(out, ref, name=f"gemm {name} {M}x{N}x{Kd + K2}")
+
+
+def test_conv_underfilled_grid(cuda, K):
+    g = torch.Generator().manual_seed(77)
+    n, Ci, Co, H, W = 16, 320, 1280, 16, 16
+    x = rnd(n, Ci, H, W, gen=g)
+    w = rnd(Co, Ci, 3, 3, scale=(9 * Ci) ** -0.5, gen=g)
+    b = torch.randn(Co, generator=g) * 0.1
+    name = K.gemm_kernel_name(n * H * W, Co, 9 * Ci, 2)
+    assert "192x256" in name or "streamk" in name, name
+    out = K.conv3x3(to_nhwc(x).to(cuda), n, H, W, wflat(w).to(cuda), b.to(cuda))
+    check(out, to_nhwc(conv_ref(x.float(), w.float(), b)), name=f"conv {name}")
+
+
+@pytest.mark.parametrize("tile,splits", [(1, 1), (2, 1), (1, 3), (2, 5), (0, 0), (3, 1), (4, 1), (6, 1), (6, 3),
+                                         (7, 1), (7, 2)])
 @pytest.mark.parametrize("geglu", [False, True])
 def test_gemm_tile_and_splitk_variants(cuda, K, tile, splits, geglu):
     g = torch.Generator().manual_seed(tile * 10 + splits)
@@ -88,7 +120,7 @@ def test_gemm_tile_and_splitk_variants(cuda, K, tile, splits, geglu):
     check(out, ref, name=f"gemm t{tile} s{splits} geglu={geglu}")
 
 
-@pytest.mark.parametrize("tile,splits", [(2, 1), (1, 4), (2, 3), (3, 1), (4, 1), (6, 1), (6, 2)])
+@pytest.mark.parametrize("tile,splits", [(2, 1), (1, 4), (2, 3), (3, 1), (4, 1), (6, 1), (6, 2), (7, 1), (7, 3)])
 def test_conv_tile_and_splitk_variants(cuda, K, tile, splits):
     g = torch.Generator().manual_seed(31 + splits)
     n, C1, C2, Co, H, W = 2, 128, 64, 192, 8, 8

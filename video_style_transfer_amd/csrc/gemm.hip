@@ -314,55 +314,58 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
 // sum the split-K slabs and apply the epilogue.  geglu: slab columns are the interleaved
 // [h(64) | g(64)] blocks; each thread produces 8 output columns.
 // Skinny GEMM for the UnZipLoRA down-projection u = x · Acatᵀ (N = padded 2r·projections <= 64,
-// no epilogue): memory-bound on reading x once.  One wave owns 16 rows and all N columns; every
-// global load is fragment-shaped (lane l reads 16 B of row l&15 at k-chunk l>>4, which IS the
-// 16x16x32 MFMA operand layout), so there is no LDS stage, no split-K slab and one launch.  The
-// K loop keeps SK k-steps of loads in flight (register double buffer).  W (Acat) is small and
-// L2-resident; out-of-range rows / columns / K read as zero through the buffer range check.
+// no epilogue): memory/latency-bound on reading x once.  A workgroup owns 16 rows and all N
+// columns; its 4 waves split K (wave w takes k-steps w, w+4, ...), issue all their fragment-shaped
+// loads of a group up front (lane l reads 16 B of row l&15 at k-chunk l>>4, which IS the 16x16x32
+// MFMA operand layout: no LDS staging), and the 4 partial accumulators are summed through LDS.
+// M/16 workgroups (512 at M = 8192) keep every CU busy; out-of-range rows / columns / K read as zero
+// through the buffer range check.
 template <int NJ>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs p) {
-  constexpr int SK = 4;  // k32 steps per load group
+  constexpr int SK = NJ <= 2 ? 12 : 8;  // k32 steps per wave per load group (all in flight at once)
+  __shared__ f32x4 red[3][NJ][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int m0 = blockIdx.x * 64 + w * 16;
+  const int m0 = blockIdx.x * 16;
   const auto ra = make_rsrc(p.A1, p.a1_bytes);
   const auto rw = make_rsrc(p.Wt, p.w_bytes);
   const int r = lane & 15, kc = (lane >> 4) * 8;
   const int arow = m0 + r;
-  const int abase = arow < p.M ? arow * p.lda1 * 2 : -1;
-  int wbase[NJ];
+  const uint32_t abase = arow < p.M ? (uint32_t)(arow * p.lda1 + kc) * 2u : (uint32_t)kOOB;
+  uint32_t wbase[NJ];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) wbase[j] = (16 * j + r) < p.N ? (16 * j + r) * p.ldw * 2 : -1;
+  for (int j = 0; j < NJ; ++j)
+    wbase[j] = (16 * j + r) < p.N ? (uint32_t)((16 * j + r) * p.ldw + kc) * 2u : (uint32_t)kOOB;
   f32x4 acc[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nk = (p.K + 31) / 32;
-  u32x4 a0[SK], b0[SK][NJ], a1[SK], b1[SK][NJ];
-  auto load = [&](u32x4 (&a)[SK], u32x4 (&b)[SK][NJ], int ks) {
+  for (int g = w; g < nk; g += 4 * SK) {
+    u32x4 a[SK], b[SK][NJ];
 #pragma unroll
     for (int t = 0; t < SK; ++t) {
-      const int k = (ks + t) * 32 + kc;
-      const bool kin = k < p.K;
-      a[t] = buf_load16(ra, (abase >= 0 && kin) ? abase + k * 2 : kOOB);
+      const int ks = g + 4 * t;
+      const bool kin = ks < nk && ks * 32 + kc < p.K;
+      a[t] = buf_load16(ra, kin ? (int)(abase + ks * 64u) : kOOB);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) b[t][j] = buf_load16(rw, (wbase[j] >= 0 && kin) ? wbase[j] + k * 2 : kOOB);
+      for (int j = 0; j < NJ; ++j) b[t][j] = buf_load16(rw, kin ? (int)(wbase[j] + ks * 64u) : kOOB);
     }
-  };
-  auto compute = [&](u32x4 (&a)[SK], u32x4 (&b)[SK][NJ]) {
+    // keep the whole group's loads in flight: one memory round trip per group, not one per k-step
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = 0; t < SK; ++t)
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8*>(&b[t][j]),
                                                          *reinterpret_cast<bf16x8*>(&a[t]), acc[j], 0, 0, 0);
-  };
-  load(a0, b0, 0);
-  for (int ks = 0; ks < nk; ks += 2 * SK) {
-    if (ks + SK < nk) load(a1, b1, ks + SK);
-    compute(a0, b0);
-    if (ks + SK >= nk) break;
-    if (ks + 2 * SK < nk) load(a0, b0, ks + 2 * SK);
-    compute(a1, b1);
   }
+  if (w > 0) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) red[w - 1][j][lane] = acc[j];
+  }
+  __syncthreads();
+  if (w > 0) return;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) acc[j] += red[0][j][lane] + red[1][j][lane] + red[2][j][lane];
   // acc[j][e] = C[m0 + (lane&15)][16j + 4(lane>>4) + e]
   const int m = m0 + r;
   if (m >= p.M) return;
@@ -383,7 +386,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs p) {
 }
 
 static int launch_skinny(const GemmArgs& a, hipStream_t s) {
-  const dim3 grid((a.M + 63) / 64);
+  const dim3 grid((a.M + 15) / 16);
   switch ((a.N + 15) / 16) {
     case 1: hipLaunchKernelGGL(gemm_skinny_kernel<1>, grid, dim3(256), 0, s, a); break;
     case 2: hipLaunchKernelGGL(gemm_skinny_kernel<2>, grid, dim3(256), 0, s, a); break;
@@ -475,14 +478,22 @@ static void choose(int M, int N, int K, int geglu, int conv, size_t ws_bytes, in
   // 256x256 ping-pong ring wins every projection / FF / GEGLU / conv shape of the path that has at
   // least a quarter-wave of tiles (it beats 128x128 and 256x160 even at 160 tiles on 256 CUs);
   // tiny-M GEMMs (text states, temb) use 128x128 with split-K; conv_out (Cout = 4) 128x64.
+  const int t192 = ((M + 191) / 192) * ((N + 255) / 256);
   if (tile == 0) {
     if (conv && N <= 64) tile = 2;
-    else if (t256 >= kCUs / 4) tile = 3;
-    else tile = 1;
+    else if (t256 >= kCUs / 4) {
+      // 192x256 when it needs fewer CU-rounds x tile area (M = 8192 x N = 1280: 215 tiles in one
+      // round vs 160 of 256x256 leaving 96 CUs idle; N = 640: exactly 2 rounds vs 1.5)
+      const double c256 = (double)((t256 + kCUs - 1) / kCUs) * 256.0;
+      const double c192 = (double)((t192 + kCUs - 1) / kCUs) * 192.0 * 1.05;
+      tile = c192 < c256 ? 7 : 3;
+    } else {
+      tile = 1;
+    }
   }
   if (geglu && (tile == 2 || tile == 6)) tile = 1;
   const int t160 = mb * ((N + 159) / 160);
-  const int tiles = tile == 1 ? t128 : tile == 2 ? t64 : tile == 3 ? t256 : tile == 6 ? t160 : t256n;
+  const int tiles = tile == 1 ? t128 : tile == 2 ? t64 : tile == 3 ? t256 : tile == 6 ? t160 : tile == 7 ? t192 : t256n;
   if (splits == 0) {
     splits = 1;
     if (tiles < kCUs / 2 && nk32 >= 8) {
@@ -499,6 +510,55 @@ static void choose(int M, int N, int K, int geglu, int conv, size_t ws_bytes, in
 }
 
 int launch_gemm_ring(const GemmArgs& a, int amode, int epi, int tile, int splits, hipStream_t s);
+// Workspace layout (caller-owned, zero-filled once): [split-K slabs | stream-K partial slots ...]
+// followed by kFlagBytes of stream-K flags at the very end (kept zero between launches).
+constexpr size_t kFlagBytes = 4096;
+
+static int device_cus() {
+  static int n = 0;
+  if (n <= 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = kCUs;
+  }
+  return n;
+}
+
+// Stream-K for the 256x256 ring (EPI 0): when the tile count leaves more than 20 % of the last
+// round's CUs idle (e.g. 160 or 384 tiles on 256 CUs), launch one workgroup per CU over equal
+// shares of the (tile, k-step) space instead.  All workgroups must be co-resident (1 per CU at
+// 160 KiB LDS), which a grid of exactly the CU count guarantees on an otherwise idle device.
+static bool plan_stream_k(int M, int N, int K, size_t ws_bytes, int& iters, int& grid) {
+  // Opt-in (VST_STREAMK=1): measured slower than the 192x256 data-parallel tile on this path —
+  // the persistent segment loop costs ~50 VGPRs on top of the 256x256 body and spills.
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("VST_STREAMK");
+    on = (e && atoi(e)) ? 1 : 0;
+  }
+  if (!on) return false;
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  const int nk = (K + 31) / 32;
+  const int cus = device_cus();
+  const int rounds = (tiles + cus - 1) / cus;
+  if ((double)tiles / ((double)rounds * cus) >= 0.8 || nk < 16 || cus > 1024) return false;
+  if (ws_bytes < (size_t)cus * 256 * 256 * sizeof(float) + kFlagBytes) return false;
+  const long long total = (long long)tiles * nk;
+  iters = (int)((total + cus - 1) / cus);
+  grid = cus;
+  return true;
+}
+
+static void apply_stream_k(GemmArgs& a, int tile, int splits, int epi, void* ws, size_t ws_bytes) {
+  if (tile != 3 || splits > 1 || epi != 0 || !ws) return;
+  int iters = 0, grid = 0;
+  if (!plan_stream_k(a.M, a.N, a.K, ws_bytes, iters, grid)) return;
+  a.sk_iters = iters;
+  a.sk_grid = grid;
+  a.sk_ws = (float*)ws;
+  a.sk_flags = (int*)((char*)ws + ws_bytes - kFlagBytes);
+}
+
 
 static int gemm_ablate_env() {
   static int v = -1;
@@ -543,21 +603,25 @@ extern "C" size_t vst_gemm_workspace_bytes(int M, int N, int K) {
 // symbol rocprofv3 reports), so per-launch timings can be attributed to kernels.  kind: 0 linear,
 // 1 GEGLU linear, 2 vectorized conv, 3 scalar-gather conv.  Returns a static string.
 extern "C" const char* vst_gemm_kernel_name(int M, int N, int K, int kind, int tile, int splits, size_t ws_bytes) {
-  static const char* names[6][3] = {
+  static const char* names[7][3] = {
       {"gemm_ring<128x128>", "gemm_ring<128x128,geglu>", "gemm_ring<128x128,conv>"},
       {"gemm_ring<128x64>", "gemm_ring<128x64,geglu>", "gemm_ring<128x64,conv>"},
       {"gemm_ring<256x256>", "gemm_ring<256x256,geglu>", "gemm_ring<256x256,conv>"},
       {"gemm_ring<256x128>", "gemm_ring<256x128,geglu>", "gemm_ring<256x128,conv>"},
       {"", "", ""},
-      {"gemm_ring<256x160>", "", "gemm_ring<256x160,conv>"}};
-  static const char* split_names[6] = {"gemm_ring<128x128,splitk>", "gemm_ring<128x64,splitk>",
+      {"gemm_ring<256x160>", "", "gemm_ring<256x160,conv>"},
+      {"gemm_ring<192x256>", "gemm_ring<192x256,geglu>", "gemm_ring<192x256,conv>"}};
+  static const char* split_names[7] = {"gemm_ring<128x128,splitk>", "gemm_ring<128x64,splitk>",
                                        "gemm_ring<256x256,splitk>", "gemm_ring<256x128,splitk>", "",
-                                       "gemm_ring<256x160,splitk>"};
+                                       "gemm_ring<256x160,splitk>", "gemm_ring<192x256,splitk>"};
   if (kind == 3) return "gemm_kernel<conv_in>";
   if (kind == 0 && (tile == 5 || (tile == 0 && N <= 64 && M >= 1024))) return "gemm_skinny";  // no-epilogue calls
-  if (kind < 0 || kind > 3 || tile < 0 || tile > 6 || tile == 5 || splits < 0) return "";
-  choose(M, N, K, kind == 1, kind == 2, ws_bytes, tile, splits);
+  if (kind < 0 || kind > 3 || tile < 0 || tile > 7 || tile == 5 || splits < 0) return "";
+  choose(M, N, K, kind == 1, kind == 2, ws_bytes > kFlagBytes ? ws_bytes - kFlagBytes : 0, tile, splits);
   if (splits > 1) return split_names[tile - 1];
+  int it = 0, gr = 0;
+  if (tile == 3 && kind != 1 && plan_stream_k(M, N, K, ws_bytes, it, gr))
+    return kind == 2 ? "gemm_ring<256x256,conv,streamk>" : "gemm_ring<256x256,streamk>";
   return names[tile - 1][kind == 2 ? 2 : kind];
 }
 
@@ -575,7 +639,7 @@ extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int
   if (epilogue == 1 && (N % 128)) return VST_ERR_ARG;
   if (R && (ldr & 7)) return VST_ERR_ARG;
   if (row_bias && row_bias_div <= 0) return VST_ERR_ARG;
-  if (tile < 0 || tile > 6 || splits < 0) return VST_ERR_ARG;
+  if (tile < 0 || tile > 7 || splits < 0) return VST_ERR_ARG;
   const bool skinny_ok = N <= 64 && !A2 && !bias && !row_bias && !R && epilogue == 0;
   if (tile == 5 && !skinny_ok) return VST_ERR_ARG;
   GemmArgs a{};
@@ -591,7 +655,9 @@ extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int
   a.C1 = 0; a.C2 = 0; a.stride = 1; a.up = 0;
   if (tile == 0 && skinny_ok && M >= 1024) tile = 5;  // LoRA down-projection: skinny kernel
   if (tile == 5) return run_gemm(a, 0, 0, 5, 1, (hipStream_t)stream);
-  choose(M, N, K, epilogue == 1, 0, workspace ? ws_bytes : 0, tile, splits);
+  const size_t slab_bytes = (workspace && ws_bytes > kFlagBytes) ? ws_bytes - kFlagBytes : 0;
+  choose(M, N, K, epilogue == 1, 0, slab_bytes, tile, splits);
+  if (slab_bytes) apply_stream_k(a, tile, splits, epilogue == 1 ? 1 : 0, workspace, ws_bytes);
   return run_gemm(a, 0, epilogue == 1, tile, splits, (hipStream_t)stream);
 }
 
@@ -612,7 +678,7 @@ extern "C" int vst_conv3x3_ex(const void* x1, int C1, const void* x2, int C2, in
   if (!x1 || !Wt || !out || nimg <= 0 || H <= 0 || W <= 0 || Cout <= 0) return VST_ERR_ARG;
   if (stride != 1 && stride != 2) return VST_ERR_ARG;
   if (upsample && stride != 1) return VST_ERR_ARG;
-  if (tile < 0 || tile > 6 || tile == 5 || splits < 0) return VST_ERR_ARG;
+  if (tile < 0 || tile > 7 || tile == 5 || splits < 0) return VST_ERR_ARG;
   const int Ct = C1 + (x2 ? C2 : 0);
   const bool vec = (Ct % BK == 0) && (C1 % 8 == 0);
   if (x2 && !vec) return VST_ERR_ARG;
@@ -634,7 +700,9 @@ extern "C" int vst_conv3x3_ex(const void* x1, int C1, const void* x2, int C2, in
   a.r_bytes = R ? clamp_bytes(((size_t)(a.M - 1) * ldr + Cout) * 2) : 0;
   if ((ldc & 7) && Cout >= 8) return VST_ERR_ARG;
   if (!vec) { tile = 2; splits = 1; }
-  choose(a.M, a.N, a.K, 0, 1, workspace ? ws_bytes : 0, tile, splits);
+  const size_t slab_bytes = (workspace && ws_bytes > kFlagBytes) ? ws_bytes - kFlagBytes : 0;
+  choose(a.M, a.N, a.K, 0, 1, slab_bytes, tile, splits);
+  if (slab_bytes && vec) apply_stream_k(a, tile, splits, 0, workspace, ws_bytes);
   return run_gemm(a, vec ? 1 : 2, 0, tile, splits, (hipStream_t)stream);
 }
 

@@ -40,16 +40,20 @@ struct RingCfg {
   static constexpr int MI = WM / 16, NJ = WN / 16;
   static constexpr int A_BYTES = BM * RBK * 2, B_BYTES = BN * RBK * 2;
   static constexpr int STAGE = A_BYTES + B_BYTES;
-  static constexpr int A_PIECES = A_BYTES / 1024 / NWAVES;  // per wave per tile
+  static constexpr int A_PIECES = A_BYTES / 1024 / NWAVES;  // per wave per tile (floor)
   static constexpr int B_PIECES = B_BYTES / 1024 / NWAVES;
-  // B tiles whose 1-KiB pieces do not split evenly over the waves (BN = 160: 10 pieces, 8 waves):
-  // waves wid < B_EXTRA load one more piece each, so their DMA count per tile is DPT, the others'
-  // DPT - 1 (wait_tiles takes the wave's own count).
+  // Tiles whose 1-KiB pieces do not split evenly over the waves (BN = 160: 10 B pieces, BM = 192:
+  // 12 A pieces, 8 waves): waves wid < B_EXTRA (A_EXTRA) load one more B (A) piece, so a wave's DMA
+  // count per tile is D_BASE + its number of extras (wait_tiles takes the wave's own count).
   static constexpr int B_EXTRA = (B_BYTES / 1024) % NWAVES;
-  static constexpr int DPT = A_PIECES + B_PIECES + (B_EXTRA ? 1 : 0);  // max DMA per thread per tile
+  static constexpr int A_EXTRA = (A_BYTES / 1024) % NWAVES;
+  static constexpr int D_BASE = A_PIECES + B_PIECES;
+  static constexpr int DPT = D_BASE + (B_EXTRA ? 1 : 0) + (A_EXTRA ? 1 : 0);  // max DMA per thread per tile
+  static constexpr int IDX_BX = D_BASE;                           // offs[] slot of the extra B piece
+  static constexpr int IDX_AX = D_BASE + (B_EXTRA ? 1 : 0);       // offs[] slot of the extra A piece
   static constexpr int EPI_BYTES = BM * (BN * 2 + 16);  // bf16 tile staged for the epilogue
   static constexpr int LDS = STAGES * STAGE > EPI_BYTES ? STAGES * STAGE : EPI_BYTES;
-  static_assert(A_BYTES % (1024 * NWAVES) == 0 && B_BYTES % 1024 == 0, "piece split");
+  static_assert(A_BYTES % 1024 == 0 && B_BYTES % 1024 == 0, "piece split");
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
@@ -67,12 +71,13 @@ __device__ __forceinline__ void wait_tiles_d(int tiles) {
 }
 
 template <class Cfg>
-__device__ __forceinline__ void wait_tiles(int tiles, bool full) {
-  if constexpr (Cfg::B_EXTRA == 0) {
-    wait_tiles_d<Cfg::DPT>(tiles);
+__device__ __forceinline__ void wait_tiles(int tiles, int n_extra) {
+  if constexpr (Cfg::DPT == Cfg::D_BASE) {
+    wait_tiles_d<Cfg::D_BASE>(tiles);
   } else {
-    if (full) wait_tiles_d<Cfg::DPT>(tiles);
-    else wait_tiles_d<Cfg::DPT - 1>(tiles);
+    if (n_extra == 0) wait_tiles_d<Cfg::D_BASE>(tiles);
+    else if (Cfg::DPT == Cfg::D_BASE + 1 || n_extra == 1) wait_tiles_d<Cfg::D_BASE + 1>(tiles);
+    else wait_tiles_d<Cfg::DPT>(tiles);
   }
 }
 
@@ -88,25 +93,31 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// Grouped tile order: GROUP_M row panels sweep the N axis together, so the A and W panels a
+// k-slice needs are shared by ~GROUP_M tiles running concurrently on one XCD (L2 hits instead of
+// repeated MALL fetches).  `t` is an XCD-contiguous logical tile index.
+__device__ __forceinline__ void tile_coords(int t, int nbm, int nbn, int& bm, int& bn) {
+  constexpr int GROUP_M = 8;
+  const int in_group = GROUP_M * nbn;
+  const int gid = t / in_group, first_m = gid * GROUP_M;
+  const int gsize = min(nbm - first_m, GROUP_M);
+  bm = first_m + (t - gid * in_group) % gsize;
+  bn = (t - gid * in_group) / gsize;
+}
+
+// One output tile's k-range [kt0, kt1): ring pipeline + epilogue.  Stream-K modes: sk_mode 0 =
+// whole tile (or a split-K slab, EPI 2); 1 = this k-range's fp32 partial goes to slot `sk_slot`
+// (accumulator register layout, 1 KiB coalesced per fragment and wave) and its flag is released;
+// 2 = the tile's head range: add the partials of slots sk_slot+1 .. sk_last (the later k-ranges,
+// which those workgroups computed FIRST in their own ranges, so they are normally ready), reset
+// their flags, then run the epilogue.
 template <class Cfg, int AMODE, int EPI>
-__global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) {
+__device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const int m0, const int n0, const int kt0,
+                                          const int kt1, const int sk_mode, const int sk_slot, const int sk_last) {
   constexpr int BM = Cfg::BM, BN = Cfg::BN;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid / Cfg::WAVES_N, wc = wid - wr * Cfg::WAVES_N;
-  const int nbn = (p.N + BN - 1) / BN, nbm = (p.M + BM - 1) / BM;
-  // XCD-contiguous tile ranges, then grouped ordering inside a range: GROUP_M row panels sweep
-  // the N axis together, so the A and W panels a k-slice needs are shared by ~GROUP_M tiles
-  // that run concurrently on one XCD (L2 hits instead of repeated MALL fetches).
-  const int wg = xcd_remap(blockIdx.x, nbn * nbm);
-  constexpr int GROUP_M = 8;
-  const int in_group = GROUP_M * nbn;
-  const int gid = wg / in_group, first_m = gid * GROUP_M;
-  const int gsize = min(nbm - first_m, GROUP_M);
-  const int bm = first_m + (wg - gid * in_group) % gsize;
-  const int bn = (wg - gid * in_group) / gsize;
-  const int m0 = bm * BM, n0 = bn * BN;
 
   const auto ra1 = make_rsrc(p.A1, p.a1_bytes);
   const auto ra2 = make_rsrc(p.A2 ? p.A2 : p.A1, p.A2 ? p.a2_bytes : 0u);
@@ -116,9 +127,10 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
   const int prow = lane >> 2;
   const int lchunk = (lane & 3) ^ gperm((lane >> 4) & 3);
 
-  int rowA[Cfg::A_PIECES], oyv[Cfg::A_PIECES], oxv[Cfg::A_PIECES];
+  constexpr int AQ = Cfg::A_PIECES + (Cfg::A_EXTRA ? 1 : 0);  // q == A_PIECES: the extra piece
+  int rowA[AQ], oyv[AQ], oxv[AQ];
 #pragma unroll
-  for (int q = 0; q < Cfg::A_PIECES; ++q) {
+  for (int q = 0; q < AQ; ++q) {
     const int m = m0 + 16 * (q * Cfg::NWAVES + wid) + prow;
     if (AMODE == 0) {
       rowA[q] = m < p.M ? m : -1;
@@ -139,14 +151,9 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
     const int n = n0 + 16 * (q * Cfg::NWAVES + wid) + prow;  // q == B_PIECES: the extra piece
     rowB[q] = n < p.N ? n : -1;
   }
-  const bool has_extra = wid < Cfg::B_EXTRA;  // wave-uniform
+  const bool has_bx = wid < Cfg::B_EXTRA, has_ax = wid < Cfg::A_EXTRA;  // wave-uniform
+  const int n_extra = (has_bx ? 1 : 0) + (has_ax ? 1 : 0);
   const int Ctot = p.C1 + p.C2;
-  const int nk_all = (p.K + RBK - 1) / RBK;
-  int kt0 = 0, kt1 = nk_all;
-  if (EPI == 2) {
-    kt0 = (int)((long long)nk_all * blockIdx.z / p.splits);
-    kt1 = (int)((long long)nk_all * (blockIdx.z + 1) / p.splits);
-  }
   const int nk = kt1 - kt0;
 
   // ---- incremental DMA addressing (keeps the load segment of each k-tile short) ----
@@ -160,10 +167,10 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
 #pragma unroll
   for (int q = 0; q <= Cfg::B_PIECES; ++q)
     bB[q] = rowB[q] >= 0 ? (uint32_t)(rowB[q] * p.ldw + lchunk * 8) * 2u : (uint32_t)kOOB;
-  uint32_t bA[Cfg::A_PIECES], bA2[Cfg::A_PIECES];
+  uint32_t bA[AQ], bA2[AQ];
   if (AMODE == 0) {
 #pragma unroll
-    for (int q = 0; q < Cfg::A_PIECES; ++q) {
+    for (int q = 0; q < AQ; ++q) {
       bA[q] = rowA[q] >= 0 ? (uint32_t)(rowA[q] * p.lda1 + lchunk * 8) * 2u : (uint32_t)kOOB;
       bA2[q] = rowA[q] >= 0 ? (uint32_t)(rowA[q] * p.lda2 + lchunk * 8) * 2u : (uint32_t)kOOB;
     }
@@ -181,7 +188,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
     const int cs = second ? p.C2 : p.C1;
     run_ci0 = second ? p.C1 : 0;
 #pragma unroll
-    for (int q = 0; q < Cfg::A_PIECES; ++q) {
+    for (int q = 0; q < AQ; ++q) {
       int iy, ix;
       bool ok = rowA[q] >= 0;
       if (p.up) {
@@ -203,19 +210,22 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
     const bool kin = !ktail || (k0 + lchunk * 8 < p.K);
 #pragma unroll
     for (int q = 0; q < Cfg::B_PIECES; ++q) offs[q] = kin ? (int)(bB[q] + kb) : kOOB;
-    if constexpr (Cfg::B_EXTRA != 0) offs[Cfg::DPT - 1] = kin ? (int)(bB[Cfg::B_PIECES] + kb) : kOOB;
+    if constexpr (Cfg::B_EXTRA != 0) offs[Cfg::IDX_BX] = kin ? (int)(bB[Cfg::B_PIECES] + kb) : kOOB;
     if (AMODE == 0) {
       a_second = k0 >= p.K1;  // K1 is a multiple of 64: a k-tile never straddles the sources
       const uint32_t ka = a_second ? (uint32_t)(k0 - p.K1) * 2u : kb;
 #pragma unroll
       for (int q = 0; q < Cfg::A_PIECES; ++q)
         offs[Cfg::B_PIECES + q] = kin ? (int)((a_second ? bA2[q] : bA[q]) + ka) : kOOB;
+      if constexpr (Cfg::A_EXTRA != 0)
+        offs[Cfg::IDX_AX] = kin ? (int)((a_second ? bA2[Cfg::A_PIECES] : bA[Cfg::A_PIECES]) + ka) : kOOB;
     } else {
       if (rebase_due) rebase();
       a_second = run_ci0 != 0;
       const uint32_t kc = (uint32_t)(c_ci - run_ci0) * 2u;
 #pragma unroll
       for (int q = 0; q < Cfg::A_PIECES; ++q) offs[Cfg::B_PIECES + q] = (int)(bA[q] + kc);
+      if constexpr (Cfg::A_EXTRA != 0) offs[Cfg::IDX_AX] = (int)(bA[Cfg::A_PIECES] + kc);
       c_ci += RBK;
       if (c_ci == Ctot) { c_ci = 0; ++c_tap; }
       rebase_due = c_ci == 0 || (p.C2 > 0 && c_ci == p.C1);
@@ -223,8 +233,10 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
   };
   auto dma_piece = [&](int stage, int idx) {  // idx: compile-time after unrolling
     char* As = smem + stage * Cfg::STAGE;
-    if (Cfg::B_EXTRA != 0 && idx == Cfg::DPT - 1) {
-      if (has_extra) dma16(rw, As + Cfg::A_BYTES + (Cfg::B_PIECES * Cfg::NWAVES + wid) * 1024, offs[idx]);
+    if (Cfg::A_EXTRA != 0 && idx == Cfg::IDX_AX) {
+      if (has_ax) dma16(a_second ? ra2 : ra1, As + (Cfg::A_PIECES * Cfg::NWAVES + wid) * 1024, offs[idx]);
+    } else if (Cfg::B_EXTRA != 0 && idx == Cfg::IDX_BX) {
+      if (has_bx) dma16(rw, As + Cfg::A_BYTES + (Cfg::B_PIECES * Cfg::NWAVES + wid) * 1024, offs[idx]);
     } else if (idx < Cfg::B_PIECES) {
       dma16(rw, As + Cfg::A_BYTES + (idx * Cfg::NWAVES + wid) * 1024, offs[idx]);
     } else {
@@ -282,41 +294,37 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
 
   if constexpr (Cfg::NWAVES == 8) {
     // ---- ping-pong schedule (8 waves; waves w and w+4 share a SIMD) ----
-    // Each k-tile is two barrier intervals: L = {LDS-DMA issue of tile it+S-1, ds_reads of tile
-    // it+1's fragments, counted wait for this wave's DMA of tile it+2} and C = {the MFMA chain of
-    // tile it}.  Waves 4-7 run one barrier behind waves 0-3 (one extra s_barrier up front, which
-    // waves 0-3 pay back after the loop), so in every interval one wave of each SIMD issues MFMAs
-    // while its partner issues loads: the load work hides under the matrix pipe.
+    // Each k-tile is two barrier intervals: L = {LDS-DMA issue of tile it+S-1, ds_reads of tile it's
+    // fragments, counted wait for this wave's DMA of tile it+1} and C = {the MFMA chain of tile it}.
+    // Waves 4-7 run one barrier behind waves 0-3 (one extra s_barrier up front, which waves 0-3 pay
+    // back after the loop), so in every interval one wave of each SIMD issues MFMAs while its
+    // partner issues loads: the load work AND its LDS latency hide under the partner's matrix
+    // work, so one register set of fragments suffices (48 VGPRs instead of 96).
     // Hazards (intervals counted globally, group g's L(it) at 2it+g, C(it) at 2it+1+g):
-    //  RAW: tile it+1 is read in L(it) (interval >= 2it); each group waited for its own DMA of
-    //       tile it+1 in L(it-1) (interval <= 2it-1), before the barrier that ends it.
-    //  WAR: L(it) refills the stage of tile it-1, whose fragments every group read in L(it-2)
-    //       and consumed in C(it-2) (interval <= 2it-2), two barriers earlier.
+    //  RAW: tile it is read in L(it) (interval >= 2it); each group waited for its own DMA of tile it
+    //       in L(it-1) (interval <= 2it-1), before the barrier that ends it.
+    //  WAR: L(it) refills the stage of tile it-1, whose fragments every group read in L(it-1) and
+    //       retired (lgkmcnt(0)) before the barrier that ended that interval (<= 2it-1).
     const bool late = wid >= 4;
 #pragma unroll
     for (int s = 0; s < S - 1; ++s)
       if (s < nk) issue(kt0 + s, s);
-    wait_tiles<Cfg>(max(0, min(nk - 1, S - 2) - 1), has_extra);  // own DMA of tiles 0 and 1 landed
+    wait_tiles<Cfg>(min(nk, S - 1) - 1, n_extra);  // own DMA of tile 0 landed
     __builtin_amdgcn_s_barrier();
-    if (nk > 0) load_into(fa0, fb0, 0);
     if (late) __builtin_amdgcn_s_barrier();
-    int wrs = S - 1, nrd = 1 % S;
-    auto pp_step = [&](int it, FragA& ca, FragB& cb, FragA& na, FragB& nb) {
-      const bool steady = it + S - 1 < nk;  // tile it+S-1 exists: issue it, keep S-3 tiles in flight
+    int wrs = S - 1, rd = 0;
+    for (int it = 0; it < nk; ++it) {
+      const bool steady = it + S - 1 < nk;  // tile it+S-1 exists: issue it, keep S-2 tiles in flight
       if (steady && !no_dma) issue(kt0 + it + S - 1, wrs);
       wrs = wrs + 1 == S ? 0 : wrs + 1;
-      if (it + 1 < nk) load_into(na, nb, nrd);
-      nrd = nrd + 1 == S ? 0 : nrd + 1;
-      // in the last S-1 tiles drain completely instead of counting (two wait forms, no dispatch chain)
-      if (steady && !no_dma) wait_tiles<Cfg>(S - 3, has_extra);
-      else if (it + 2 < nk) wait_tiles<Cfg>(0, has_extra);
+      load_into(fa0, fb0, rd);
+      rd = rd + 1 == S ? 0 : rd + 1;
+      if (steady && !no_dma) wait_tiles<Cfg>(S - 2, n_extra);
+      else if (it + 1 < nk) wait_tiles<Cfg>(0, n_extra);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      mfmas(ca, cb);
+      mfmas(fa0, fb0);
       __builtin_amdgcn_s_barrier();
-    };
-    for (int it = 0; it < nk; it += 2) {
-      pp_step(it, fa0, fb0, fa1, fb1);
-      if (it + 1 < nk) pp_step(it + 1, fa1, fb1, fa0, fb0);
     }
     if (!late) __builtin_amdgcn_s_barrier();
   } else {
@@ -324,7 +332,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
 #pragma unroll
   for (int s = 0; s < S - 1; ++s)
     if (s < nk) issue(kt0 + s, s);
-  wait_tiles<Cfg>(min(nk, S - 1) - 1, has_extra);
+  wait_tiles<Cfg>(min(nk, S - 1) - 1, n_extra);
   __builtin_amdgcn_s_barrier();
 
   // fragments of the current k-tile live in registers: all MI + NJ ds_read_b128 are issued
@@ -338,8 +346,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
   auto step = [&](int it, FragA& ca, FragB& cb, FragA& na, FragB& nb) {
     if (it + 1 < nk) {
       // tile it+1 must have landed: steady state leaves S-3 younger tiles in flight, the tail drains
-      if (it + S - 2 < nk && !no_dma) wait_tiles<Cfg>(S - 3, has_extra);
-      else wait_tiles<Cfg>(0, has_extra);
+      if (it + S - 2 < nk && !no_dma) wait_tiles<Cfg>(S - 3, n_extra);
+      else wait_tiles<Cfg>(0, n_extra);
       __builtin_amdgcn_s_barrier();
     }
     if (it + S - 1 < nk && !no_dma) issue(kt0 + it + S - 1, wrs);
@@ -355,6 +363,56 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
   }
   }
   __builtin_amdgcn_s_barrier();  // all waves done with the ring before the epilogue reuses LDS
+
+  // ---------------- stream-K partials ----------------
+  if constexpr (EPI == 0) {
+    // Partials cross XCDs: written through (sc1) and read with sc1 loads, flags stored / polled at
+    // agent scope — no L2-wide writeback or invalidate, which would also evict every other
+    // workgroup's A/W panels from the shared L2.
+    const auto rsk = make_rsrc(p.sk_ws, (uint32_t)((size_t)p.sk_grid * BM * BN * sizeof(float)));
+    if (sk_mode != 0 && (p.ablate & 4)) {  // diagnostics: segmenting cost only (wrong results)
+      if (sk_mode == 1) return;
+    } else if (sk_mode == 1) {
+      const int base = sk_slot * (BM * BN * 4);
+#pragma unroll
+      for (int i = 0; i < Cfg::MI; ++i)
+#pragma unroll
+        for (int j = 0; j < Cfg::NJ; ++j) {
+          const f32x4 v = acc[i][j];
+          buf_store16_sc1(*reinterpret_cast<const u32x4*>(&v), rsk,
+                          base + (((wid * Cfg::MI + i) * Cfg::NJ + j) * 64 + lane) * 16);
+        }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's partial is in memory
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(p.sk_flags + sk_slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    else if (sk_mode == 2) {
+      for (int sl = sk_slot + 1; sl <= sk_last; ++sl) {
+        if (tid == 0) {
+          // bounded spin (~1 s): a missing producer must not hang the GPU
+          for (int spin = 0; spin < (1 << 23); ++spin) {
+            if (__hip_atomic_load(p.sk_flags + sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1) break;
+            __builtin_amdgcn_s_sleep(2);
+          }
+        }
+        __syncthreads();
+        const int base = sl * (BM * BN * 4);
+#pragma unroll
+        for (int i = 0; i < Cfg::MI; ++i) {
+          u32x4 v[Cfg::NJ];
+#pragma unroll
+          for (int j = 0; j < Cfg::NJ; ++j)
+            v[j] = buf_load16_sc1(rsk, base + (((wid * Cfg::MI + i) * Cfg::NJ + j) * 64 + lane) * 16);
+#pragma unroll
+          for (int j = 0; j < Cfg::NJ; ++j) acc[i][j] += *reinterpret_cast<const f32x4*>(&v[j]);
+          __builtin_amdgcn_sched_barrier(0);  // NJ loads in flight at a time: no accumulator spills
+        }
+        // the next launch's producers start after this kernel completes: resetting now is race-free
+        if (tid == 0) __hip_atomic_store(p.sk_flags + sl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
 
   // ---------------- epilogue ----------------
   // Split-K partials go straight from registers to the fp32 slab (16 B per lane).  Otherwise
@@ -385,6 +443,21 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
   } else {
     constexpr int LROW = BN * 2 + 16;  // staged bf16 row (16-B pad: conflict-light b64 writes)
     static_assert(BM * LROW <= Cfg::LDS, "epilogue staging must fit in the ring's LDS");
+    constexpr int CPR = BN / 8;  // 16-B output chunks per row
+    constexpr int TOT = BM * CPR;
+    constexpr int ITEMS = (TOT + Cfg::THREADS - 1) / Cfg::THREADS;
+    const auto rr = make_rsrc(p.R ? p.R : p.Wt, p.R ? p.r_bytes : 0u);
+    // residual chunks are fetched first (the fragment registers are dead now): their HBM latency
+    // overlaps the bias add and the LDS staging below instead of stalling the store pass.
+    u32x4 res[EPI == 0 ? ITEMS : 1];
+    if (EPI == 0 && p.R) {
+#pragma unroll
+      for (int k = 0; k < ITEMS; ++k) {
+        const int idx = tid + k * Cfg::THREADS;
+        const int row = idx / CPR, n = n0 + (idx - row * CPR) * 8, m = m0 + row;
+        res[k] = buf_load16(rr, (idx < TOT && m < p.M && n + 8 <= p.N) ? (m * p.ldr + n) * 2 : kOOB);
+      }
+    }
     if (p.bias) {
 #pragma unroll
       for (int j = 0; j < Cfg::NJ; ++j) {
@@ -409,21 +482,10 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
         v[1] = pack2bf(acc[i][j][2], acc[i][j][3]);
         *reinterpret_cast<u32x2*>(smem + (lrow0 + i * 16) * LROW + (lcol0 + j * 16) * 2) = v;
       }
-    __syncthreads();
-    const auto rr = make_rsrc(p.R ? p.R : p.Wt, p.R ? p.r_bytes : 0u);
+    // publish the staged tile; a raw barrier (no vmcnt drain) keeps the residual loads in flight
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
     if constexpr (EPI == 0) {
-      constexpr int CPR = BN / 8;                 // 16-B chunks per row
-      constexpr int TOT = BM * CPR;
-      constexpr int ITEMS = (TOT + Cfg::THREADS - 1) / Cfg::THREADS;
-      u32x4 res[ITEMS];
-      if (p.R) {
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) {
-          const int idx = tid + k * Cfg::THREADS;
-          const int row = idx / CPR, n = n0 + (idx - row * CPR) * 8, m = m0 + row;
-          res[k] = buf_load16(rr, (idx < TOT && m < p.M && n + 8 <= p.N) ? (m * p.ldr + n) * 2 : kOOB);
-        }
-      }
 #pragma unroll
       for (int k = 0; k < ITEMS; ++k) {
         const int idx = tid + k * Cfg::THREADS;
@@ -461,15 +523,15 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
         }
       }
     } else {  // GEGLU: per 128 weight rows [64 hidden | 64 gate] -> 64 outputs, bias already in
-      constexpr int CPR = BN / 16;                // 8-output chunks per row
-      constexpr int RSTEP = Cfg::THREADS / CPR;
-      constexpr int ITEMS = BM / RSTEP;
-      static_assert(Cfg::THREADS % CPR == 0 && BM % RSTEP == 0, "item split");
-      const int oc = tid % CPR, row0 = tid / CPR;
+      constexpr int GPR = BN / 16;                // 8-output chunks per row
+      constexpr int RSTEP = Cfg::THREADS / GPR;
+      constexpr int GITEMS = BM / RSTEP;
+      static_assert(Cfg::THREADS % GPR == 0 && BM % RSTEP == 0, "item split");
+      const int oc = tid % GPR, row0 = tid / GPR;
       const int blk = oc >> 3, c = (oc & 7) * 8;
       const int nh = n0 + blk * 128 + c;
 #pragma unroll
-      for (int k = 0; k < ITEMS; ++k) {
+      for (int k = 0; k < GITEMS; ++k) {
         const int row = row0 + k * RSTEP, m = m0 + row;
         if (m >= p.M || nh >= p.N) continue;
         float h[8], g[8], v[8];
@@ -483,24 +545,73 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
   }
 }
 
+// Data-parallel launch: one tile per workgroup (split-K: blockIdx.z selects the k-range).
+// Stream-K launch (SK): one workgroup per CU; workgroup w (XCD-contiguous logical index) takes the
+// w-th equal share of the (tile, k-step) iteration space, so grids whose tile count leaves CUs idle
+// (160 or 384 tiles on 256 CUs) keep every CU busy; split tiles are combined through sk_ws.
+template <class Cfg, int AMODE, int EPI, bool SK>
+__global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BM = Cfg::BM, BN = Cfg::BN;
+  const int nbn = (p.N + BN - 1) / BN, nbm = (p.M + BM - 1) / BM;
+  const int nk_all = (p.K + RBK - 1) / RBK;
+  if constexpr (!SK) {
+    int bm, bn;
+    tile_coords(xcd_remap(blockIdx.x, nbn * nbm), nbm, nbn, bm, bn);
+    int kt0 = 0, kt1 = nk_all;
+    if (EPI == 2) {
+      kt0 = (int)((long long)nk_all * blockIdx.z / p.splits);
+      kt1 = (int)((long long)nk_all * (blockIdx.z + 1) / p.splits);
+    }
+    ring_tile<Cfg, AMODE, EPI>(p, smem, bm * BM, bn * BN, kt0, kt1, 0, 0, 0);
+  } else {
+    const int w = xcd_remap(blockIdx.x, gridDim.x);
+    const long long I = p.sk_iters;
+    const long long total = (long long)nbm * nbn * nk_all;
+    long long start = (long long)w * I;
+    const long long end = min(start + I, total);
+    while (start < end) {
+      const int t = (int)(start / nk_all);
+      const int kb = (int)(start - (long long)t * nk_all);
+      const int ke = (int)min((long long)nk_all, kb + (end - start));
+      const int mode = (kb == 0 && ke == nk_all) ? 0 : (kb == 0 ? 2 : 1);
+      const int last = (int)(((long long)(t + 1) * nk_all - 1) / I);  // workgroup holding the tile's last k-step
+      int bm, bn;
+      tile_coords(t, nbm, nbn, bm, bn);
+      ring_tile<Cfg, AMODE, EPI>(p, smem, bm * BM, bn * BN, kb, ke, mode, w, last);
+      start += ke - kb;
+      __syncthreads();  // LDS (staged tile / ring) is reused by the next segment
+    }
+  }
+}
+
 // stages: as many as the LDS budget allows at the intended residency (lookahead S-2 tiles)
 using Cfg256x256 = RingCfg<256, 256, 2, 4, 5>;  // 160 KiB, 1 WG/CU
 using Cfg256x128 = RingCfg<256, 128, 4, 2, 6>;  // 144 KiB, 1 WG/CU
 using Cfg128x128 = RingCfg<128, 128, 2, 2, 5>;  //  80 KiB, 2 WG/CU
 using Cfg128x64 = RingCfg<128, 64, 2, 2, 6>;    //  72 KiB, 2 WG/CU
 using Cfg256x160 = RingCfg<256, 160, 4, 2, 5>;  // 130 KiB, 1 WG/CU: N = 320/640/960/1280/1920/3840 without waste
+using Cfg192x256 = RingCfg<192, 256, 2, 4, 5>;  // 140 KiB, 1 WG/CU: 215 tiles at M = 8192, N = 1280
 
-template <class Cfg, int AMODE, int EPI>
-static int launch_ring_t(const GemmArgs& a, hipStream_t s, int splits) {
+template <class Cfg, int AMODE, int EPI, bool SK>
+static int launch_ring_k(const GemmArgs& a, hipStream_t s, dim3 grid) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_ring_kernel<Cfg, AMODE, EPI>,
+    (void)hipFuncSetAttribute((const void*)gemm_ring_kernel<Cfg, AMODE, EPI, SK>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS);
     attr = true;
   }
-  const int nwg = ((a.M + Cfg::BM - 1) / Cfg::BM) * ((a.N + Cfg::BN - 1) / Cfg::BN);
-  hipLaunchKernelGGL((gemm_ring_kernel<Cfg, AMODE, EPI>), dim3(nwg, 1, splits), dim3(Cfg::THREADS), Cfg::LDS, s, a);
+  hipLaunchKernelGGL((gemm_ring_kernel<Cfg, AMODE, EPI, SK>), grid, dim3(Cfg::THREADS), Cfg::LDS, s, a);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+}
+
+template <class Cfg, int AMODE, int EPI>
+static int launch_ring_t(const GemmArgs& a, hipStream_t s, int splits) {
+  const int nwg = ((a.M + Cfg::BM - 1) / Cfg::BM) * ((a.N + Cfg::BN - 1) / Cfg::BN);
+  if constexpr (EPI == 0 && std::is_same_v<Cfg, Cfg256x256>) {  // stream-K (opt-in, see gemm.hip)
+    if (a.sk_iters > 0) return launch_ring_k<Cfg, AMODE, EPI, true>(a, s, dim3(a.sk_grid));
+  }
+  return launch_ring_k<Cfg, AMODE, EPI, false>(a, s, dim3(nwg, 1, splits));
 }
 
 template <class Cfg>
@@ -518,7 +629,7 @@ static int dispatch_cfg(const GemmArgs& a, int amode, int epi, hipStream_t s, in
   return VST_ERR_ARG;
 }
 
-// tile: 1 = 128x128, 2 = 128x64, 3 = 256x256, 4 = 256x128, 6 = 256x160.  epi: 0 plain, 1 GEGLU, 2 split-K partial
+// tile: 1 = 128x128, 2 = 128x64, 3 = 256x256, 4 = 256x128, 6 = 256x160, 7 = 192x256.  epi: 0 plain, 1 GEGLU, 2 split-K partial
 int launch_gemm_ring(const GemmArgs& a, int amode, int epi, int tile, int splits, hipStream_t s) {
   switch (tile) {
     case 1: return dispatch_cfg<Cfg128x128>(a, amode, epi, s, splits);
@@ -526,6 +637,7 @@ int launch_gemm_ring(const GemmArgs& a, int amode, int epi, int tile, int splits
     case 3: return dispatch_cfg<Cfg256x256>(a, amode, epi, s, splits);
     case 4: return dispatch_cfg<Cfg256x128>(a, amode, epi, s, splits);
     case 6: return epi == 1 ? VST_ERR_ARG : dispatch_cfg<Cfg256x160>(a, amode, epi, s, splits);
+    case 7: return dispatch_cfg<Cfg192x256>(a, amode, epi, s, splits);
     default: return VST_ERR_ARG;
   }
 }

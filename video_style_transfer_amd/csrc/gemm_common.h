@@ -18,6 +18,11 @@ struct GemmArgs {
   float* ws;  // split-K slabs [splits][M][N] fp32
   int splits;
   int ablate;  // diagnostics only (VST_GEMM_ABLATE): bit0 skip loop DMA, bit1 skip MFMA
+  // stream-K (ring GEMM, 256x256): k-steps per workgroup (0 = data-parallel), grid, partial slots
+  // [sk_grid][BM*BN] fp32 and their flags (zero between launches; consumers reset them)
+  int sk_iters, sk_grid;
+  float* sk_ws;
+  int* sk_flags;
   uint32_t a1_bytes, a2_bytes, w_bytes, r_bytes;
 };
 

@@ -68,14 +68,15 @@ def gemm_kernel_name(M, N, K, kind):
     name = _lib.load().vst_gemm_kernel_name(M, N, K, kind, GEMM_POLICY["tile"], GEMM_POLICY["splits"], _WS_BYTES)
     return name.decode() if name else None
 _WS = {}
-_WS_BYTES = 64 << 20
+_WS_BYTES = 80 << 20  # split-K slabs / stream-K partial slots (256 x 256 KiB) + 4 KiB of flags
 
 
 def _workspace(device):
-    """Per-device fp32 split-K slab workspace (allocated once, reused stream-ordered)."""
+    """Per-device GEMM workspace (allocated once, reused stream-ordered): fp32 split-K slabs /
+    stream-K partials, and stream-K flags in its last 4 KiB, which must start (and stay) zero."""
     ws = _WS.get(device)
     if ws is None:
-        ws = torch.empty(_WS_BYTES // 4, dtype=F32, device=device)
+        ws = torch.zeros(_WS_BYTES // 4, dtype=F32, device=device)
         _WS[device] = ws
     return ws
 
