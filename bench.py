@@ -216,6 +216,7 @@ def main():
     ok = bool(torch.isfinite(den.lat).all().item())
 
     rl, table = (None, None) if args.no_roofline else roofline(den)
+    graphed = den.graph is not None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         del den, unet
@@ -238,7 +239,7 @@ def main():
                        "parallelism": (f"frame-shard x{world} ({nclips} clips, {args.frames // world} frames/clip/GPU, "
                                        f"RCCL all-to-all around each motion module)" if shard is not None else
                                        f"replicas x{world}" if world > 1 else "single"),
-                       "graph": den.graph is not None, "note": graph_note},
+                       "graph": graphed, "note": graph_note},
             "roofline": rl, "cpu_baseline": cpu, "kernels": table, "finite": ok,
             "setup_s": round(t_build, 1),
         }
