@@ -8,7 +8,9 @@ LIB := video_style_transfer_amd/libvst_hip.so
 
 all: $(LIB)
 
-build/%.o: video_style_transfer_amd/csrc/%.hip video_style_transfer_amd/csrc/vst_common.h
+HDR := $(wildcard video_style_transfer_amd/csrc/*.h) include/vst.h
+
+build/%.o: video_style_transfer_amd/csrc/%.hip $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -60,6 +60,31 @@ def parse():
     return ap.parse_args()
 
 
+def _lib_md5():
+    import hashlib
+    from video_style_transfer_amd import _lib
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.md5(f.read()).hexdigest()
+
+
+def pmc_traffic(symbol):
+    """HBM bytes per launch of `symbol` from the newest profiles/pmc_traffic_*.json (tools/pmc_traffic.py:
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes with the gfx950 corrections), only if it was measured on
+    this exact libvst_hip.so.  (bytes, source) or (None, reason)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic_*.json")), key=os.path.getmtime)
+    if not files:
+        return None, "no PMC profile"
+    with open(files[-1]) as f:
+        d = json.load(f)
+    if d.get("lib_md5") != _lib_md5():
+        return None, f"{os.path.basename(files[-1])} was measured on another build of libvst_hip.so"
+    k = d.get("kernels", {}).get(symbol)
+    if k is None:
+        return None, f"{symbol} not in {os.path.basename(files[-1])}"
+    return k["traffic_bytes"], os.path.basename(files[-1])
+
+
 def roofline(den):
     """One instrumented eager step: HIP events around every launch on its stream."""
     from video_style_transfer_amd import kernels as K
@@ -102,9 +127,11 @@ def roofline(den):
                       "share": round(d["ms"] / total_ms, 4),
                       "tflops": round(d["flops"] / (d["ms"] * 1e-3) / 1e12, 1) if d["flops"] else None,
                       "gbs": round(d["bytes"] / (d["ms"] * 1e-3) / 1e9, 1)}
+    traffic, tsrc = pmc_traffic(dom_sym)
     return {
         "bound": "mfma" if mfma else "hbm", "kernel": dom_sym, "achieved": round(achieved, 1), "peak": peak,
-        "unit": unit, "frac": round(achieved / peak, 4), "traffic": None,
+        "unit": unit, "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": tsrc,
+        "alg_bytes_per_launch": round(dom["bytes"] / dom["launches"]),
         "avg_launch_ms": round(dom["ms"] / dom["launches"], 4),
         "flops_per_launch": dom["flops"] / dom["launches"],
         "kernel_time_ms_per_step": round(total_ms, 3),

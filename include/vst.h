@@ -25,7 +25,8 @@ extern "C" {
  * UnZipLoRALinearLayerInfer.forward (unziplora_unet/unziplora_linear_layer.py:298-346), and
  * TemporalLoRALinear.forward (animatediff/temporal_lora.py:29-32).
  * epilogue 0: plain; 1: GEGLU (diffusers GEGLU feed-forward, unziplora_unet/unzip_attention.py
- * ff path) with gate/hidden rows interleaved per 64-column block, output width N/2. */
+ * ff path) with gate/hidden rows interleaved per 64-column block, output width N/2; 2: GELU(erf) after
+ * the bias, no residual / row bias (TemporalTransformerBlock.ffn, animatediff/temporal_transformer.py:53-59). */
 int vst_gemm(const void* A, int lda, const void* A2, int lda2, int K1, const void* W, int ldw, int M, int N, int K,
              const float* bias, const float* row_bias, int row_bias_div, int ld_row_bias, const void* R, int ldr,
              void* C, int ldc, int epilogue, void* stream);
@@ -94,6 +95,14 @@ int vst_layernorm(const void* x, int ldx, int C, int rows, const float* gamma, c
  * AnimateDiffTransformer3D, here across ranks). */
 int vst_permute_rows(const void* src, void* dst, int C, int d0, int d1, int d2, int d3, int p0, int p1, int p2,
                      int p3, void* stream);
+
+/* y[row] = x[row] + table[(row / div) % mod] (fp32 table [mod][C]): the reference TemporalTransformer's
+ * PositionalEncoding.forward (animatediff/temporal_transformer.py:20-27) on token rows (b*F + f)*HW + p. */
+int vst_add_row_table(const void* x, int ldx, int C, int rows, const float* table, int div, int mod, void* y, int ldy,
+                      void* stream);
+/* bf16 token rows ((b*F + f)*HW + p, C) -> fp32 (B, C, F, HW): the 5-D output layout of
+ * TemporalTransformer.forward (temporal_transformer.py:142-144) and UNetMotionModel.forward. */
+int vst_unpack_tokens(const void* src, int B, int C, int F, int HW, float* out, void* stream);
 
 /* Denoise-loop glue (inference_animatediff.py:104-131). */
 int vst_timestep_embedding(const float* t, const int* step_idx, int n, int dim, int flip_sin_to_cos,

@@ -346,3 +346,32 @@ def test_timestep_and_euler(cuda, K):
     check(latd, ref, rel_l2=1e-5, rel_max=1e-5, name="euler")
     K.step_advance(step)
     assert int(step.item()) == 1
+
+
+@pytest.mark.parametrize("M,N,Kd,tile,splits", [(700, 1280, 320, 0, 0), (4096, 2560, 640, 0, 0), (300, 384, 640, 1, 3),
+                                               (1024, 512, 256, 3, 1)])
+def test_gemm_gelu(cuda, K, M, N, Kd, tile, splits):
+    g = torch.Generator().manual_seed(M + N + 5)
+    x, w = rnd(M, Kd, gen=g), rnd(N, Kd, scale=Kd ** -0.5, gen=g)
+    b = torch.randn(N, generator=g) * 0.3
+    K.GEMM_POLICY.update(tile=tile, splits=splits)
+    try:
+        out = K.linear(x.to(cuda), w.to(cuda), b.to(cuda), act="gelu")
+    finally:
+        K.GEMM_POLICY.update(tile=0, splits=0)
+    check(out, F.gelu(x.float() @ w.float().t() + b), name="gemm+gelu")
+
+
+def test_add_row_table_and_unpack(cuda, K):
+    g = torch.Generator().manual_seed(3)
+    B, C, Fr, H, W = 2, 96, 5, 9, 7
+    x5 = torch.randn(B, C, Fr, H, W, generator=g)
+    tok = torch.empty(B * Fr * H * W, C, dtype=torch.bfloat16, device=cuda)
+    K.pack_latents(x5.to(cuda), tok)
+    pe = torch.randn(32, C, generator=g)
+    y = K.add_row_table(tok, pe.to(cuda), div=H * W, mod=Fr)
+    ref = x5.to(torch.bfloat16).float().permute(0, 2, 3, 4, 1).reshape(-1, C) + pe[(torch.arange(y.shape[0]) // (H * W)) % Fr]
+    check(y, ref, name="add_row_table")
+    out = torch.empty(B, C, Fr, H, W, device=cuda)
+    K.unpack_tokens(tok, out)
+    assert torch.equal(out.cpu(), x5.to(torch.bfloat16).float())

@@ -35,6 +35,8 @@ SIGNATURES = {
     "vst_permute_rows": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "vst_groupnorm": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _F, _P, _P, _I, _P, _I, _P, _P]),
     "vst_layernorm": (_I, [_P, _I, _I, _I, _P, _P, _F, _P, _I, _I, _P, _I, _P]),
+    "vst_add_row_table": (_I, [_P, _I, _I, _I, _P, _I, _I, _P, _I, _P]),
+    "vst_unpack_tokens": (_I, [_P, _I, _I, _I, _I, _P, _P]),
     "vst_timestep_embedding": (_I, [_P, _P, _I, _I, _I, _F, _P, _I, _I, _I, _P]),
     "vst_pack_latents": (_I, [_P, _I, _I, _I, _I, _P, _P, _F, _I, _P, _P]),
     "vst_euler_cfg_step": (_I, [_P, _I, _F, _P, _I, _I, _I, _I, _P, _P, _P]),

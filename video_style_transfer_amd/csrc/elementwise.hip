@@ -113,6 +113,53 @@ __global__ __launch_bounds__(256) void permute_rows_kernel(const bf16_t* __restr
   }
 }
 
+// y[row] = x[row] + table[(row / div) % mod]: the reference TemporalTransformer's PositionalEncoding
+// (animatediff/temporal_transformer.py:20-27) on token rows (b*F + f)*HW + p with div = HW, mod = F.
+__global__ __launch_bounds__(256) void add_row_table_kernel(const bf16_t* __restrict__ x, int ldx, int C,
+                                                            const float* __restrict__ table, int div, int mod,
+                                                            bf16_t* __restrict__ y, int ldy, size_t total_chunks) {
+  const int CH = C / 8;
+  for (size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x; idx < total_chunks; idx += (size_t)gridDim.x * 256) {
+    const size_t row = idx / CH;
+    const int c = (int)(idx - row * CH) * 8;
+    float f[8];
+    unpack8(*reinterpret_cast<const u32x4*>(x + row * ldx + c), f);
+    const f32x4* t = reinterpret_cast<const f32x4*>(table + (size_t)((row / div) % mod) * C + c);
+    const f32x4 t0 = t[0], t1 = t[1];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { f[e] += t0[e]; f[e + 4] += t1[e]; }
+    *reinterpret_cast<u32x4*>(y + row * ldy + c) = pack8(f);
+  }
+}
+
+// bf16 token rows ((b*F + f)*HW + p, C) -> fp32 (B, C, F, HW): the inverse of pack_latents (the 5-D
+// output of UNetMotionModel / TemporalTransformer).  64-pixel x 64-channel tiles transposed through
+// LDS so both the 16-B row reads and the fp32 pixel-run writes are coalesced.
+__global__ __launch_bounds__(256) void unpack_tokens_kernel(const bf16_t* __restrict__ src, int C, int F, int HW,
+                                                            float* __restrict__ out) {
+  __shared__ float tile[64][65];
+  const int img = blockIdx.z;  // b*F + f
+  const int b = img / F, f = img - b * F;
+  const int p0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int idx = tid + 256 * k;
+    const int r = idx >> 3, ch = (idx & 7) * 8;
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (p0 + r < HW && c0 + ch < C)
+      unpack8(*reinterpret_cast<const u32x4*>(src + ((size_t)img * HW + p0 + r) * C + c0 + ch), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) tile[ch + e][r] = v[e];
+  }
+  __syncthreads();
+  const int pl = tid & 63;
+  for (int cl = tid >> 6; cl < 64; cl += 4) {
+    const int c = c0 + cl, p = p0 + pl;
+    if (c < C && p < HW) out[(((size_t)b * C + c) * F + f) * HW + p] = tile[cl][pl];
+  }
+}
+
 __global__ void step_advance_kernel(int* step) {
   if (threadIdx.x == 0 && blockIdx.x == 0) *step += 1;
 }
@@ -194,6 +241,25 @@ extern "C" int vst_permute_rows(const void* src, void* dst, int C, int d0, int d
   const int grid = (int)std::min<size_t>((total + 255) / 256, 16384);
   hipLaunchKernelGGL(permute_rows_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)src,
                      (bf16_t*)dst, C, make_int4(d0, d1, d2, d3), make_int4(p0, p1, p2, p3), total);
+  return ok();
+}
+
+extern "C" int vst_add_row_table(const void* x, int ldx, int C, int rows, const float* table, int div, int mod,
+                                 void* y, int ldy, void* stream) {
+  if (!x || !y || !table || rows <= 0 || C <= 0 || (C & 7) || (ldx & 7) || (ldy & 7) || div <= 0 || mod <= 0)
+    return VST_ERR_ARG;
+  const size_t total = (size_t)rows * (C / 8);
+  const int grid = (int)std::min<size_t>((total + 255) / 256, 16384);
+  hipLaunchKernelGGL(add_row_table_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ldx, C,
+                     table, div, mod, (bf16_t*)y, ldy, total);
+  return ok();
+}
+
+extern "C" int vst_unpack_tokens(const void* src, int B, int C, int F, int HW, float* out, void* stream) {
+  if (!src || !out || B <= 0 || C <= 0 || (C & 7) || F <= 0 || HW <= 0 || B * F > 65535) return VST_ERR_ARG;
+  const dim3 grid((HW + 63) / 64, (C + 63) / 64, B * F);
+  hipLaunchKernelGGL(unpack_tokens_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)src, C, F, HW,
+                     out);
   return ok();
 }
 

@@ -425,6 +425,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(GemmArgs p, int
         if (p.bias) v[e] += p.bias[n + e];
         if (p.rbias) v[e] += p.rbias[(size_t)(m / p.rbias_div) * p.ldrb + n + e];
         if (p.R) v[e] += bf2f(p.R[(size_t)m * p.ldr + n + e]);
+        if (p.act) v[e] = gelu_erf(v[e]);
       }
     } else {
       const int blk = n / 64, c = n - blk * 64;
@@ -636,7 +637,9 @@ extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int
   } else {
     K1 = K;
   }
+  if (epilogue < 0 || epilogue > 2) return VST_ERR_ARG;
   if (epilogue == 1 && (N % 128)) return VST_ERR_ARG;
+  if (epilogue == 2 && (R || row_bias)) return VST_ERR_ARG;  // GELU: bias only
   if (R && (ldr & 7)) return VST_ERR_ARG;
   if (row_bias && row_bias_div <= 0) return VST_ERR_ARG;
   if (tile < 0 || tile > 7 || splits < 0) return VST_ERR_ARG;
@@ -653,6 +656,8 @@ extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int
   a.w_bytes = clamp_bytes(((size_t)(N - 1) * ldw + K) * 2);
   a.r_bytes = R ? clamp_bytes(((size_t)(M - 1) * ldr + N) * 2) : 0;
   a.C1 = 0; a.C2 = 0; a.stride = 1; a.up = 0;
+  a.act = epilogue == 2 ? 1 : 0;
+  if (epilogue == 2) epilogue = 0;
   if (tile == 0 && skinny_ok && M >= 1024) tile = 5;  // LoRA down-projection: skinny kernel
   if (tile == 5) return run_gemm(a, 0, 0, 5, 1, (hipStream_t)stream);
   const size_t slab_bytes = (workspace && ws_bytes > kFlagBytes) ? ws_bytes - kFlagBytes : 0;

@@ -473,6 +473,14 @@ __device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const i
         for (int i = 0; i < Cfg::MI; ++i) acc[i][j] += b4;
       }
     }
+    if (EPI == 0 && p.act) {  // GELU(erf) on the biased fp32 accumulators, before the bf16 rounding
+#pragma unroll
+      for (int i = 0; i < Cfg::MI; ++i)
+#pragma unroll
+        for (int j = 0; j < Cfg::NJ; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][e] = gelu_erf(acc[i][j][e]);
+    }
 #pragma unroll
     for (int i = 0; i < Cfg::MI; ++i)
 #pragma unroll

@@ -17,6 +17,7 @@ struct GemmArgs {
   bf16_t* C; int ldc;
   float* ws;  // split-K slabs [splits][M][N] fp32
   int splits;
+  int act;     // EPI 0 only: 1 = GELU(erf) after the bias (TemporalTransformerBlock ffn, no residual / row bias)
   int ablate;  // diagnostics only (VST_GEMM_ABLATE): bit0 skip loop DMA, bit1 skip MFMA
   // stream-K (ring GEMM, 256x256): k-steps per workgroup (0 = data-parallel), grid, partial slots
   // [sk_grid][BM*BN] fp32 and their flags (zero between launches; consumers reset them)

@@ -102,8 +102,9 @@ def _ld(t):
 def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *, x2: torch.Tensor | None = None,
            residual: torch.Tensor | None = None, row_bias: torch.Tensor | None = None, row_bias_div: int = 1,
            out: torch.Tensor | None = None, geglu: bool = False, alg_k2: int | None = None,
-           kind: str | None = None, alg_n: int | None = None) -> torch.Tensor:
-    """out[M, N'] = epilogue([x | x2] @ w^T + bias + row_bias[m // div] + residual); N' = N or N/2 (GEGLU)."""
+           kind: str | None = None, alg_n: int | None = None, act: str | None = None) -> torch.Tensor:
+    """out[M, N'] = epilogue([x | x2] @ w^T + bias + row_bias[m // div] + residual); N' = N or N/2 (GEGLU).
+    act="gelu": GELU(erf) of (x @ w^T + bias) — no residual / row bias with it."""
     _dev(x, BF16, "x")
     _dev(w, BF16, "w")
     M, K1 = x.shape
@@ -114,6 +115,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
             raise _lib.VstError(f"linear: x {tuple(x.shape)} + x2 {tuple(x2.shape)} vs w {tuple(w.shape)}")
     elif K1 != K:
         raise _lib.VstError(f"linear: x {tuple(x.shape)} vs w {tuple(w.shape)}")
+    if act not in (None, "gelu") or (act and (geglu or residual is not None or row_bias is not None)):
+        raise _lib.VstError(f"linear: act={act!r} supports only bias (no GEGLU / residual / row bias)")
     n_out = N // 2 if geglu else N
     if out is None:
         out = torch.empty((M, n_out), dtype=BF16, device=x.device)
@@ -138,7 +141,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
         ws = _workspace(x.device)
         _lib.call("vst_gemm_ex", _p(x), _ld(x), _p(x2), 0 if x2 is None else _ld(x2), K1, _p(w), _ld(w), M, N, K,
                   _p(bias), _p(row_bias), row_bias_div, N if row_bias is not None else 0, _p(residual),
-                  0 if residual is None else _ld(residual), _p(out), _ld(out), 1 if geglu else 0,
+                  0 if residual is None else _ld(residual), _p(out), _ld(out), 1 if geglu else (2 if act else 0),
                   GEMM_POLICY["tile"], GEMM_POLICY["splits"], _p(ws), _WS_BYTES, _stream())
     return out
 
@@ -294,6 +297,32 @@ def permute_rows(src, dims, perm, out=None):
         out = torch.empty_like(src)
     with _Rec("permute", 0.0, 2.0 * 2 * src.numel()):
         _lib.call("vst_permute_rows", _p(src), _p(out), src.shape[1], *dims, *perm, _stream())
+    return out
+
+
+def add_row_table(x, table, *, div=1, mod=1, out=None):
+    """out[row] = x[row] + table[(row // div) % mod]; table fp32 [>= mod, C] on device."""
+    _dev(x, BF16, "x")
+    rows, C = x.shape
+    if table.dtype != F32 or not table.is_cuda or table.dim() != 2 or table.shape[1] != C or table.shape[0] < mod:
+        raise _lib.VstError("add_row_table: table must be fp32 [>= mod, C] on device")
+    if out is None:
+        out = torch.empty((rows, C), dtype=BF16, device=x.device)
+    with _Rec("add_row_table", 0.0, 2.0 * 2 * rows * C):
+        _lib.call("vst_add_row_table", _p(x), _ld(x), C, rows, _p(table.contiguous()), div, mod, _p(out), _ld(out),
+                  _stream())
+    return out
+
+
+def unpack_tokens(src, out):
+    """bf16 token rows ((b*F + f)*HW + p, C) -> fp32 out (B, C, F, H, W) (contiguous)."""
+    _dev(src, BF16, "src")
+    if out.dtype != F32 or not out.is_cuda or not out.is_contiguous() or out.dim() != 5:
+        raise _lib.VstError("unpack_tokens: out must be a contiguous fp32 (B, C, F, H, W) device tensor")
+    B, C, F, H, W = out.shape
+    if not src.is_contiguous() or src.shape != (B * F * H * W, C):
+        raise _lib.VstError(f"unpack_tokens: src {tuple(src.shape)} vs out {tuple(out.shape)}")
+    _lib.call("vst_unpack_tokens", _p(src), B, C, F, H * W, _p(out), _stream())
     return out
 
 
