@@ -25,7 +25,7 @@ extern "C" {
  * UnZipLoRALinearLayerInfer.forward (unziplora_unet/unziplora_linear_layer.py:298-346), and
  * TemporalLoRALinear.forward (animatediff/temporal_lora.py:29-32).
  * epilogue 0: plain; 1: GEGLU (diffusers GEGLU feed-forward, unziplora_unet/unzip_attention.py
- * ff path) with gate/hidden rows interleaved per 64-column block, output width N/2; 2: GELU(erf) after
+ * ff path) with hidden/gate rows interleaved per 32-column block ([32 h | 32 g] per 64 rows), output width N/2; 2: GELU(erf) after
  * the bias, no residual / row bias (TemporalTransformerBlock.ffn, animatediff/temporal_transformer.py:53-59). */
 int vst_gemm(const void* A, int lda, const void* A2, int lda2, int K1, const void* W, int ldw, int M, int N, int K,
              const float* bias, const float* row_bias, int row_bias_div, int ld_row_bias, const void* R, int ldr,

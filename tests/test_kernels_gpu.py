@@ -112,8 +112,8 @@ def test_gemm_tile_and_splitk_variants(cuda, K, tile, splits, geglu):
         K.GEMM_POLICY.update(tile=0, splits=0)
     y = torch.cat([x, x2], 1).float() @ w.float().t() + b
     if geglu:
-        idx = torch.arange(N).view(-1, 128)
-        h, gt = y[:, idx[:, :64].reshape(-1)], y[:, idx[:, 64:].reshape(-1)]
+        idx = torch.arange(N).view(-1, 64)
+        h, gt = y[:, idx[:, :32].reshape(-1)], y[:, idx[:, 32:].reshape(-1)]
         ref = h * F.gelu(gt)
     else:
         ref = y + rb.repeat_interleave(100, 0) + r.float()
@@ -168,9 +168,9 @@ def test_gemm_geglu(cuda, K):
     x = rnd(M, C, gen=g)
     w = rnd(2 * inner, C, scale=C ** -0.5, gen=g)
     b = torch.randn(2 * inner, generator=g) * 0.1
-    # interleave rows: per 64-output block j: hidden rows [64j,64j+64) then gate rows [inner+64j, ...)
-    idx = torch.cat([torch.cat([torch.arange(64 * j, 64 * j + 64), inner + torch.arange(64 * j, 64 * j + 64)])
-                     for j in range(inner // 64)])
+    # interleave rows: per 32-output block j: hidden rows [32j,32j+32) then gate rows [inner+32j, ...)
+    idx = torch.cat([torch.cat([torch.arange(32 * j, 32 * j + 32), inner + torch.arange(32 * j, 32 * j + 32)])
+                     for j in range(inner // 32)])
     out = K.linear(x.to(cuda), w[idx].contiguous().to(cuda), b[idx].contiguous().to(cuda), geglu=True)
     y = x.float() @ w.float().t() + b
     hdn, gate = y.chunk(2, dim=-1)

@@ -11,7 +11,9 @@ from video_style_transfer_amd import kernels as K  # noqa: E402
 
 BF = torch.bfloat16
 SHAPES = [("qkv1280", 8192, 3840, 1344), ("ff2_1280", 8192, 1280, 5120), ("ff2_640", 32768, 640, 2560),
-          ("big4k", 4096, 4096, 4096)]
+          ("big4k", 4096, 4096, 4096), ("ff1_1280", 8192, 10240, 1280), ("out_lora1280", 8192, 1280, 1312),
+          ("proj320", 131072, 320, 320), ("qkv320", 131072, 960, 320), ("ff1_320", 131072, 2560, 320),
+          ("ff1_1280_geglu", 8192, 10240, 1280), ("ff1_320_geglu", 131072, 2560, 320)]
 
 
 def timeit(fn, iters=20):
@@ -33,15 +35,16 @@ def main():
     for name, M, N, Kd in SHAPES:
         x = torch.randn(M, Kd, device=dev).to(BF)
         w = (torch.randn(N, Kd, device=dev) / Kd ** 0.5).to(BF)
-        out = torch.empty(M, N, device=dev, dtype=BF)
+        geglu = name.endswith("_geglu")
+        out = torch.empty(M, N // 2 if geglu else N, device=dev, dtype=BF)
         fl = 2.0 * M * N * Kd
         row = {"ablate": ab, "shape": name}
-        for t in (1, 3, 4):
+        for t in [int(v) for v in os.environ.get("TILES", "3").split()]:
             K.GEMM_POLICY.update(tile=t, splits=1)
-            ms = timeit(lambda: K.linear(x, w, None, out=out))
+            ms = timeit(lambda: K.linear(x, w, None, out=out, geglu=geglu))
             row[f"t{t}_tf"] = round(fl / ms / 1e9, 1)
             row[f"t{t}_us"] = round(ms * 1e3, 1)
-        if ab == "0":
+        if ab == "0" and not geglu:
             ms = timeit(lambda: torch.nn.functional.linear(x, w))
             row["hipblaslt_tf"] = round(fl / ms / 1e9, 1)
         print(json.dumps(row), flush=True)

@@ -59,11 +59,14 @@ def load(path: str | None = None):
     global _lib
     if _lib is not None:
         return _lib
-    path = path or LIB_PATH
+    alt = os.environ.get("VST_LIB_AB")  # diagnostics only (tools/gemm_ablate.py A/B of two builds)
+    path = path or alt or LIB_PATH
     if not os.path.exists(path):
         raise VstError(f"libvst_hip.so not found at {path}; build it with `make` (hipcc --offload-arch=gfx950)")
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
+        if alt and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

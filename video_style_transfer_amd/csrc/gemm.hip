@@ -14,7 +14,7 @@
 //      channel concat (up-block skip connections).
 //   2  same conv with a scalar gather (tiny Cin, e.g. conv_in with 4 channels).
 // Epilogues (template EPI): 0 = +bias[n] +row_bias[m/div][n] +residual[m,n] -> bf16;
-//   1 = GEGLU (tile columns [0,64) hidden, [64,128) gate of the same 64 outputs;
+//   1 = GEGLU (per 64 columns: [0,32) hidden, [32,64) gate of the same 32 outputs;
 //   the host interleaves the weight rows accordingly); 2 = fp32 split-K partial slab
 //   (the epilogue then runs in gemm_splitk_reduce_kernel).
 //
@@ -312,7 +312,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
 }
 
 // sum the split-K slabs and apply the epilogue.  geglu: slab columns are the interleaved
-// [h(64) | g(64)] blocks; each thread produces 8 output columns.
+// [h(32) | g(32)] blocks; each thread produces 8 output columns.
 // Skinny GEMM for the UnZipLoRA down-projection u = x · Acatᵀ (N = padded 2r·projections <= 64,
 // no epilogue): memory/latency-bound on reading x once.  A workgroup owns 16 rows and all N
 // columns; its 4 waves split K (wave w takes k-steps w, w+4, ...), issue all their fragment-shaped
@@ -428,8 +428,8 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(GemmArgs p, int
         if (p.act) v[e] = gelu_erf(v[e]);
       }
     } else {
-      const int blk = n / 64, c = n - blk * 64;
-      const int hc = blk * 128 + c, gc = hc + 64;
+      const int blk = n / 32, c = n - blk * 32;
+      const int hc = blk * 64 + c, gc = hc + 32;
       float h[8], g[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) { h[e] = 0.f; g[e] = 0.f; }
@@ -587,7 +587,7 @@ static int run_gemm(GemmArgs& a, int amode, int geglu, int tile, int splits, hip
     hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(grid), dim3(256), 0, s, a, geglu);
     return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
   }
-  return launch_gemm_ring(a, amode, geglu ? 1 : 0, tile, 1, s);
+  return launch_gemm_ring(a, amode, geglu ? 1 : (a.act ? 3 : 0), tile, 1, s);
 }
 
 }  // namespace vst
@@ -638,7 +638,7 @@ extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int
     K1 = K;
   }
   if (epilogue < 0 || epilogue > 2) return VST_ERR_ARG;
-  if (epilogue == 1 && (N % 128)) return VST_ERR_ARG;
+  if (epilogue == 1 && (N % 64)) return VST_ERR_ARG;
   if (epilogue == 2 && (R || row_bias)) return VST_ERR_ARG;  // GELU: bias only
   if (R && (ldr & 7)) return VST_ERR_ARG;
   if (row_bias && row_bias_div <= 0) return VST_ERR_ARG;

@@ -258,12 +258,13 @@ __device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const i
 
   constexpr int S = Cfg::STAGES;
   const int fr = lane & 15, fq = lane >> 4;
-  const bool no_dma = p.ablate & 1, no_mfma = p.ablate & 2;
+  const bool no_dma = p.ablate & 1, no_mfma = p.ablate & 2, no_lds = p.ablate & 16;
   typedef bf16x8 FragA[Cfg::MI];
   typedef bf16x8 FragB[Cfg::NJ];
   FragA fa0, fa1;
   FragB fb0, fb1;
   auto load_into = [&](FragA& fa, FragB& fb, int stage) {
+    if (no_lds) return;  // diagnostics: no fragment reads (wrong results)
     const char* As = smem + stage * Cfg::STAGE;
     const char* Bs = As + Cfg::A_BYTES;
 #pragma unroll
@@ -363,6 +364,13 @@ __device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const i
   }
   }
   __builtin_amdgcn_s_barrier();  // all waves done with the ring before the epilogue reuses LDS
+  if (p.ablate & 8) {  // diagnostics: no epilogue (keep the accumulators alive)
+#pragma unroll
+    for (int i = 0; i < Cfg::MI; ++i)
+#pragma unroll
+      for (int j = 0; j < Cfg::NJ; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
 
   // ---------------- stream-K partials ----------------
   if constexpr (EPI == 0) {
@@ -416,7 +424,7 @@ __device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const i
 
   // ---------------- epilogue ----------------
   // Split-K partials go straight from registers to the fp32 slab (16 B per lane).  Otherwise
-  // bias is added in registers, the whole BMxBN tile is staged ONCE in LDS as bf16 (the rounding
+  // bias (and GELU for EPI 3) is applied in registers, the whole BMxBN tile is staged ONCE in LDS as bf16 (the rounding
   // point of the reference's bf16 linear/conv output), and a vectorized pass applies the per-frame
   // row bias / residual add (after that rounding, as the reference's separate add does) or GEGLU
   // and writes full 16-B chunks.  All residual loads of a thread are issued before any use.
@@ -473,27 +481,24 @@ __device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const i
         for (int i = 0; i < Cfg::MI; ++i) acc[i][j] += b4;
       }
     }
-    if (EPI == 0 && p.act) {  // GELU(erf) on the biased fp32 accumulators, before the bf16 rounding
-#pragma unroll
-      for (int i = 0; i < Cfg::MI; ++i)
-#pragma unroll
-        for (int j = 0; j < Cfg::NJ; ++j)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc[i][j][e] = gelu_erf(acc[i][j][e]);
-    }
 #pragma unroll
     for (int i = 0; i < Cfg::MI; ++i)
 #pragma unroll
       for (int j = 0; j < Cfg::NJ; ++j) {
+        f32x4 a4 = acc[i][j];
+        if constexpr (EPI == 3) {  // GELU(erf) of the biased fp32 accumulator, before the bf16 rounding
+#pragma unroll
+          for (int e = 0; e < 4; ++e) a4[e] = gelu_erf(a4[e]);
+        }
         u32x2 v;
-        v[0] = pack2bf(acc[i][j][0], acc[i][j][1]);
-        v[1] = pack2bf(acc[i][j][2], acc[i][j][3]);
+        v[0] = pack2bf(a4[0], a4[1]);
+        v[1] = pack2bf(a4[2], a4[3]);
         *reinterpret_cast<u32x2*>(smem + (lrow0 + i * 16) * LROW + (lcol0 + j * 16) * 2) = v;
       }
     // publish the staged tile; a raw barrier (no vmcnt drain) keeps the residual loads in flight
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if constexpr (EPI == 0) {
+    if constexpr (EPI == 0 || EPI == 3) {
 #pragma unroll
       for (int k = 0; k < ITEMS; ++k) {
         const int idx = tid + k * Cfg::THREADS;
@@ -503,7 +508,7 @@ __device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const i
         if (idx >= TOT || m >= p.M || nv <= 0) continue;
         float v[8];
         unpack8(*reinterpret_cast<const u32x4*>(smem + row * LROW + cc * 16), v);
-        if (p.rbias) {
+        if (EPI == 0 && p.rbias) {
           const float* rb = p.rbias + (size_t)(m / p.rbias_div) * p.ldrb + n;
           if (nv == 8) {
             const f32x4 r0 = *reinterpret_cast<const f32x4*>(rb);
@@ -515,7 +520,7 @@ __device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const i
           }
         }
         if (nv == 8) {
-          if (p.R) {
+          if (EPI == 0 && p.R) {
             float r8[8];
             unpack8(res[k], r8);
 #pragma unroll
@@ -525,29 +530,29 @@ __device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const i
         } else {
           for (int e = 0; e < nv; ++e) {
             float x = v[e];
-            if (p.R) x += bf2f(p.R[(size_t)m * p.ldr + n + e]);
+            if (EPI == 0 && p.R) x += bf2f(p.R[(size_t)m * p.ldr + n + e]);
             p.C[(size_t)m * p.ldc + n + e] = f2bf(x);
           }
         }
       }
-    } else {  // GEGLU: per 128 weight rows [64 hidden | 64 gate] -> 64 outputs, bias already in
+    } else {  // GEGLU: per 64 weight rows [32 hidden | 32 gate] -> 32 outputs, bias already in
       constexpr int GPR = BN / 16;                // 8-output chunks per row
       constexpr int RSTEP = Cfg::THREADS / GPR;
       constexpr int GITEMS = BM / RSTEP;
       static_assert(Cfg::THREADS % GPR == 0 && BM % RSTEP == 0, "item split");
       const int oc = tid % GPR, row0 = tid / GPR;
-      const int blk = oc >> 3, c = (oc & 7) * 8;
-      const int nh = n0 + blk * 128 + c;
+      const int blk = oc >> 2, c = (oc & 3) * 8;
+      const int nh = n0 + blk * 64 + c;
 #pragma unroll
       for (int k = 0; k < GITEMS; ++k) {
         const int row = row0 + k * RSTEP, m = m0 + row;
         if (m >= p.M || nh >= p.N) continue;
         float h[8], g[8], v[8];
-        unpack8(*reinterpret_cast<const u32x4*>(smem + row * LROW + (blk * 128 + c) * 2), h);
-        unpack8(*reinterpret_cast<const u32x4*>(smem + row * LROW + (blk * 128 + 64 + c) * 2), g);
+        unpack8(*reinterpret_cast<const u32x4*>(smem + row * LROW + (blk * 64 + c) * 2), h);
+        unpack8(*reinterpret_cast<const u32x4*>(smem + row * LROW + (blk * 64 + 32 + c) * 2), g);
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = h[e] * gelu_erf(g[e]);
-        *reinterpret_cast<u32x4*>(p.C + (size_t)m * p.ldc + (n0 >> 1) + blk * 64 + c) = pack8(v);
+        *reinterpret_cast<u32x4*>(p.C + (size_t)m * p.ldc + (n0 >> 1) + blk * 32 + c) = pack8(v);
       }
     }
   }
@@ -626,9 +631,10 @@ template <class Cfg>
 static int dispatch_cfg(const GemmArgs& a, int amode, int epi, hipStream_t s, int splits) {
   if (amode == 0) {
     if (epi == 0) return launch_ring_t<Cfg, 0, 0>(a, s, splits);
+    if (epi == 3) return launch_ring_t<Cfg, 0, 3>(a, s, splits);
     if (epi == 1) {
-      if constexpr (Cfg::BN % 128 == 0) return launch_ring_t<Cfg, 0, 1>(a, s, splits);
-      return VST_ERR_ARG;  // GEGLU pairs 64 hidden + 64 gate columns per 128
+      if constexpr (Cfg::NJ % 4 == 0) return launch_ring_t<Cfg, 0, 1>(a, s, splits);
+      return VST_ERR_ARG;  // GEGLU pairs 32 hidden + 32 gate columns inside one wave's 64
     }
     return launch_ring_t<Cfg, 0, 2>(a, s, splits);
   }
@@ -637,7 +643,8 @@ static int dispatch_cfg(const GemmArgs& a, int amode, int epi, hipStream_t s, in
   return VST_ERR_ARG;
 }
 
-// tile: 1 = 128x128, 2 = 128x64, 3 = 256x256, 4 = 256x128, 6 = 256x160, 7 = 192x256.  epi: 0 plain, 1 GEGLU, 2 split-K partial
+// tile: 1 = 128x128, 2 = 128x64, 3 = 256x256, 4 = 256x128, 6 = 256x160, 7 = 192x256.  epi: 0 plain, 1 GEGLU,
+// 2 split-K partial, 3 bias + GELU
 int launch_gemm_ring(const GemmArgs& a, int amode, int epi, int tile, int splits, hipStream_t s) {
   switch (tile) {
     case 1: return dispatch_cfg<Cfg128x128>(a, amode, epi, s, splits);

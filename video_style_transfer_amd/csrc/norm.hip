@@ -54,12 +54,24 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const bf16_t* __restrict_
     float a[8], q[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) { a[e] = 0.f; q[e] = 0.f; }
-    for (int r = r_beg + rph; r < r_end; r += rps) {
-      const u32x4 v = *reinterpret_cast<const u32x4*>(chan_ptr(x1, ld1, C1, x2, ld2, row0 + r, c));
-      float f[8];
-      unpack8(v, f);
+    // GN_UNROLL independent 16-B loads in flight per thread (a dependent one-at-a-time loop is
+    // latency-bound: ~40 sequential HBM round trips per thread)
+    constexpr int GN_UNROLL = 8;
+    for (int r = r_beg + rph; r < r_end; r += GN_UNROLL * rps) {
+      u32x4 v[GN_UNROLL];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { a[e] += f[e]; q[e] += f[e] * f[e]; }
+      for (int u = 0; u < GN_UNROLL; ++u) {
+        const int rr = r + u * rps;
+        v[u] = rr < r_end ? *reinterpret_cast<const u32x4*>(chan_ptr(x1, ld1, C1, x2, ld2, row0 + rr, c))
+                          : u32x4{0u, 0u, 0u, 0u};
+      }
+#pragma unroll
+      for (int u = 0; u < GN_UNROLL; ++u) {
+        float f[8];
+        unpack8(v[u], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { a[e] += f[e]; q[e] += f[e] * f[e]; }
+      }
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) { ssum[rph * C + c + e] = a[e]; ssq[rph * C + c + e] = q[e]; }
@@ -178,59 +190,80 @@ __global__ __launch_bounds__(64) void gn_finalize_sums_kernel(const double* __re
   }
 }
 
-// LayerNorm: one wave per row, up to MAXCH 8-channel chunks per lane.
-template <int MAXCH>
+// LayerNorm: each wave normalises ROWS rows (all their 16-B loads issued before any reduction, so
+// ROWS x MAXCH loads are in flight per lane), up to MAXCH 8-channel chunks per lane and row.
+template <int MAXCH, int ROWS>
 __global__ __launch_bounds__(256) void layernorm_kernel(const bf16_t* __restrict__ x, int ldx, int C, int rows,
                                                         const float* __restrict__ gamma, const float* __restrict__ beta,
                                                         float eps, const float* __restrict__ pe, int pe_div, int pe_mod,
                                                         bf16_t* __restrict__ y, int ldy) {
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * ROWS;
+  if (row0 >= rows) return;
   const int CH = C / 8;
-  float v[MAXCH][8];
-  float sum = 0.f;
+  float v[ROWS][MAXCH][8];
 #pragma unroll
-  for (int i = 0; i < MAXCH; ++i) {
-    const int cc = lane + 64 * i;
-    if (cc < CH) {
-      unpack8(*reinterpret_cast<const u32x4*>(x + (size_t)row * ldx + cc * 8), v[i]);
+  for (int r = 0; r < ROWS; ++r) {
+    const int row = row0 + r;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) sum += v[i][e];
+    for (int i = 0; i < MAXCH; ++i) {
+      const int cc = lane + 64 * i;
+      u32x4 raw = u32x4{0u, 0u, 0u, 0u};
+      if (cc < CH && row < rows) raw = *reinterpret_cast<const u32x4*>(x + (size_t)row * ldx + cc * 8);
+      unpack8(raw, v[r][i]);
     }
   }
-  const float mean = wave_sum(sum) / C;
-  float sq = 0.f;
-#pragma unroll
-  for (int i = 0; i < MAXCH; ++i) {
-    const int cc = lane + 64 * i;
-    if (cc < CH) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { const float d = v[i][e] - mean; sq += d * d; }
-    }
-  }
-  const float rstd = rsqrtf(wave_sum(sq) / C + eps);
-  const float* pr = pe ? pe + (size_t)((row / pe_div) % pe_mod) * C : nullptr;
+  float gg[MAXCH][8], bb[MAXCH][8];
 #pragma unroll
   for (int i = 0; i < MAXCH; ++i) {
     const int cc = lane + 64 * i;
     if (cc < CH) {
       const f32x4* g4 = reinterpret_cast<const f32x4*>(gamma + cc * 8);
       const f32x4* b4 = reinterpret_cast<const f32x4*>(beta + cc * 8);
-      float gg[8], bb[8];
       const f32x4 g0 = g4[0], g1 = g4[1], b0 = b4[0], b1 = b4[1];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) { gg[e] = g0[e]; gg[e + 4] = g1[e]; bb[e] = b0[e]; bb[e + 4] = b1[e]; }
-      if (pr) {
-        const f32x4* p4 = reinterpret_cast<const f32x4*>(pr + cc * 8);
-        const f32x4 p0 = p4[0], p1 = p4[1];
+      for (int e = 0; e < 4; ++e) { gg[i][e] = g0[e]; gg[i][e + 4] = g1[e]; bb[i][e] = b0[e]; bb[i][e + 4] = b1[e]; }
+    }
+  }
 #pragma unroll
-        for (int e = 0; e < 4; ++e) { bb[e] += p0[e]; bb[e + 4] += p1[e]; }
+  for (int r = 0; r < ROWS; ++r) {
+    const int row = row0 + r;
+    if (row >= rows) break;
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXCH; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sum += v[r][i][e];  // zero-filled past C
+    const float mean = wave_sum(sum) / C;
+    float sq = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXCH; ++i) {
+      if (lane + 64 * i < CH) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { const float d = v[r][i][e] - mean; sq += d * d; }
       }
-      float o[8];
+    }
+    const float rstd = rsqrtf(wave_sum(sq) / C + eps);
+    const float* pr = pe ? pe + (size_t)((row / pe_div) % pe_mod) * C : nullptr;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = (v[i][e] - mean) * (rstd * gg[e]) + bb[e];
-      *reinterpret_cast<u32x4*>(y + (size_t)row * ldy + cc * 8) = pack8(o);
+    for (int i = 0; i < MAXCH; ++i) {
+      const int cc = lane + 64 * i;
+      if (cc < CH) {
+        float o[8];
+        if (pr) {
+          const f32x4* p4 = reinterpret_cast<const f32x4*>(pr + cc * 8);
+          const f32x4 p0 = p4[0], p1 = p4[1];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            o[e] = (v[r][i][e] - mean) * (rstd * gg[i][e]) + bb[i][e] + p0[e];
+            o[e + 4] = (v[r][i][e + 4] - mean) * (rstd * gg[i][e + 4]) + bb[i][e + 4] + p1[e];
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = (v[r][i][e] - mean) * (rstd * gg[i][e]) + bb[i][e];
+        }
+        *reinterpret_cast<u32x4*>(y + (size_t)row * ldy + cc * 8) = pack8(o);
+      }
     }
   }
 }
@@ -332,16 +365,17 @@ extern "C" int vst_layernorm(const void* x, int ldx, int C, int rows, const floa
   if (pe && (pe_div <= 0 || pe_mod <= 0)) return VST_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int CH = C / 8;
-  const dim3 grid((rows + 3) / 4), blk(256);
+  const dim3 blk(256);
+#define VST_LN(MC, R)                                                                                          \
+  hipLaunchKernelGGL((layernorm_kernel<MC, R>), dim3((rows + 4 * R - 1) / (4 * R)), blk, 0, s, (const bf16_t*)x, ldx, \
+                     C, rows, gamma, beta, eps, pe, pe_div, pe_mod, (bf16_t*)y, ldy)
   if (CH <= 64)
-    hipLaunchKernelGGL(layernorm_kernel<1>, grid, blk, 0, s, (const bf16_t*)x, ldx, C, rows, gamma, beta, eps, pe,
-                       pe_div, pe_mod, (bf16_t*)y, ldy);
+    VST_LN(1, 4);
   else if (CH <= 128)
-    hipLaunchKernelGGL(layernorm_kernel<2>, grid, blk, 0, s, (const bf16_t*)x, ldx, C, rows, gamma, beta, eps, pe,
-                       pe_div, pe_mod, (bf16_t*)y, ldy);
+    VST_LN(2, 2);
   else if (CH <= 256)
-    hipLaunchKernelGGL(layernorm_kernel<4>, grid, blk, 0, s, (const bf16_t*)x, ldx, C, rows, gamma, beta, eps, pe,
-                       pe_div, pe_mod, (bf16_t*)y, ldy);
+    VST_LN(4, 2);
+#undef VST_LN
   else
     return VST_ERR_ARG;
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;

@@ -129,13 +129,13 @@ class GEGLU(nn.Module):
         self.proj = Linear(dim_in, dim_out * 2)
 
     def geglu_ops(self):
-        """proj weight with hidden/gate rows interleaved per 64-output block (GEMM GEGLU epilogue)."""
+        """proj weight with hidden/gate rows interleaved per 32-output block (GEMM GEGLU epilogue)."""
         w, b = self.proj.weight, self.proj.bias
         key = (w.data_ptr(), w._version, b.data_ptr(), b._version)
         c = self.__dict__.get("_vst_geglu")
         if c is None or c[0] != key:
             inner = w.shape[0] // 2
-            idx = torch.arange(inner, device=w.device).view(-1, 64)
+            idx = torch.arange(inner, device=w.device).view(-1, 32)
             idx = torch.cat([idx, idx + inner], 1).reshape(-1)
             c = (key, (w.detach()[idx].to(BF16).contiguous(), b.detach()[idx].float().contiguous()))
             self.__dict__["_vst_geglu"] = c
