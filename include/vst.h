@@ -51,9 +51,11 @@ const char* vst_gemm_kernel_name(int M, int N, int K, int kind, int tile, int sp
 int vst_conv3x3(const void* x1, int C1, const void* x2, int C2, int nimg, int H, int W, int stride, int upsample,
                 const void* Wt, int Cout, const float* bias, const float* row_bias, int row_bias_div, const void* R,
                 int ldr, void* out, int ldc, void* stream);
+/* _ex: + tile / split-K policy and workspace (as vst_gemm_ex) and the row stride of row_bias (0 = Cout), so
+ * the time-embedding projections of every ResnetBlock2D can come from ONE batched GEMM output. */
 int vst_conv3x3_ex(const void* x1, int C1, const void* x2, int C2, int nimg, int H, int W, int stride, int upsample,
                    const void* Wt, int Cout, const float* bias, const float* row_bias, int row_bias_div,
-                   const void* R, int ldr, void* out, int ldc, int tile, int splits, void* workspace,
+                   int ld_row_bias, const void* R, int ldr, void* out, int ldc, int tile, int splits, void* workspace,
                    size_t ws_bytes, void* stream);
 
 /* Spatial SDPA, head_dim 64: replaces F.scaled_dot_product_attention in
@@ -88,6 +90,13 @@ int vst_groupnorm_apply_sums(const void* x1, int ld1, int C1, const void* x2, in
 /* LayerNorm over C (+ sinusoidal PE row pe[(row/pe_div)%pe_mod], temporal_transformer.py:6-27). */
 int vst_layernorm(const void* x, int ldx, int C, int rows, const float* gamma, const float* beta, float eps,
                   const float* pe, int pe_div, int pe_mod, void* y, int ldy, void* stream);
+
+/* LayerNorm fused with the UnZipLoRA down-projection of the projections that consume it: y = LN(x) and
+ * u = y . A^T (A: [R, C] bf16, R <= 64, R % 16 == 0; C % 32 == 0, C <= 1280), x read once.  Replaces the
+ * BasicTransformerBlock norm1/norm2 LayerNorm (unziplora_unet/unzip_attention.py:113-239) followed by the
+ * lora_down half of UnZipLoRALinearLayerInfer.forward (unziplora_linear_layer.py:298-346) on q/k/v. */
+int vst_layernorm_lora(const void* x, int ldx, int C, int rows, const float* gamma, const float* beta, float eps,
+                       const void* A, int R, void* y, int ldy, void* u, int ldu, void* stream);
 
 /* Row-block permutation: rows of C bf16 indexed (i0,i1,i2,i3) over dims (d0..d3) in src; dst
  * axis k is src axis p_k.  Used for the frame-shard <-> pixel-shard exchange around the motion

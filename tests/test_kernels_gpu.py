@@ -375,3 +375,16 @@ def test_add_row_table_and_unpack(cuda, K):
     out = torch.empty(B, C, Fr, H, W, device=cuda)
     K.unpack_tokens(tok, out)
     assert torch.equal(out.cpu(), x5.to(torch.bfloat16).float())
+
+
+@pytest.mark.parametrize("rows,C,R", [(300, 320, 64), (1000, 1280, 32), (77, 640, 48), (64, 64, 16), (33, 1280, 64)])
+def test_layer_norm_lora(cuda, K, rows, C, R):
+    """LayerNorm + UnZipLoRA down-projection in one pass: y = LN(x) (bf16), u = y @ A^T."""
+    g = torch.Generator().manual_seed(rows + C + R)
+    x = rnd(rows, C, gen=g) + 0.3
+    gam, bet = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g) * 0.1
+    A = rnd(R, C, scale=C ** -0.5, gen=g)
+    y, u = K.layer_norm_lora(x.to(cuda), gam.to(cuda), bet.to(cuda), 1e-5, A.to(cuda))
+    ref_y = F.layer_norm(x.float(), (C,), gam, bet, 1e-5)
+    check(y, ref_y, name="ln_lora.y")
+    check(u, ref_y.to(torch.bfloat16).float() @ A.float().t(), name="ln_lora.u")

@@ -13,7 +13,9 @@ BF = torch.bfloat16
 SHAPES = [("qkv1280", 8192, 3840, 1344), ("ff2_1280", 8192, 1280, 5120), ("ff2_640", 32768, 640, 2560),
           ("big4k", 4096, 4096, 4096), ("ff1_1280", 8192, 10240, 1280), ("out_lora1280", 8192, 1280, 1312),
           ("proj320", 131072, 320, 320), ("qkv320", 131072, 960, 320), ("ff1_320", 131072, 2560, 320),
-          ("ff1_1280_geglu", 8192, 10240, 1280), ("ff1_320_geglu", 131072, 2560, 320)]
+          ("ff1_1280_geglu", 8192, 10240, 1280), ("ff1_320_geglu", 131072, 2560, 320),
+          ("down1280x32_skinny", 8192, 32, 1280), ("down1280x64_skinny", 8192, 64, 1280),
+          ("down640x32_skinny", 32768, 32, 640), ("down640x64_skinny", 32768, 64, 640)]
 
 
 def timeit(fn, iters=20):
@@ -40,11 +42,11 @@ def main():
         fl = 2.0 * M * N * Kd
         row = {"ablate": ab, "shape": name}
         for t in [int(v) for v in os.environ.get("TILES", "3").split()]:
-            K.GEMM_POLICY.update(tile=t, splits=1)
+            K.GEMM_POLICY.update(tile=5 if name.endswith("_skinny") else t, splits=1)
             ms = timeit(lambda: K.linear(x, w, None, out=out, geglu=geglu))
             row[f"t{t}_tf"] = round(fl / ms / 1e9, 1)
             row[f"t{t}_us"] = round(ms * 1e3, 1)
-        if ab == "0" and not geglu:
+        if ab == "0" and not geglu and not name.endswith("_skinny"):
             ms = timeit(lambda: torch.nn.functional.linear(x, w))
             row["hipblaslt_tf"] = round(fl / ms / 1e9, 1)
         print(json.dumps(row), flush=True)

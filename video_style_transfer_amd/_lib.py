@@ -24,8 +24,8 @@ SIGNATURES = {
     "vst_gemm_workspace_bytes": (_S, [_I, _I, _I]),
     "vst_gemm_kernel_name": (ctypes.c_char_p, [_I, _I, _I, _I, _I, _I, _S]),
     "vst_conv3x3": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P, _I, _P, _I, _P]),
-    "vst_conv3x3_ex": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P, _I, _P, _I, _I, _I, _P, _S,
-                            _P]),
+    "vst_conv3x3_ex": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _I, _P, _I, _P, _I, _I, _I, _P,
+                            _S, _P]),
     "vst_spatial_attention": (_I, [_P, _I, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _F, _P]),
     "vst_temporal_attention": (_I, [_P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _F, _P]),
     "vst_groupnorm_workspace_bytes": (_S, [_I, _I, _I, _I]),
@@ -34,6 +34,7 @@ SIGNATURES = {
                                       _I, _P, _P]),
     "vst_permute_rows": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "vst_groupnorm": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _F, _P, _P, _I, _P, _I, _P, _P]),
+    "vst_layernorm_lora": (_I, [_P, _I, _I, _I, _P, _P, _F, _P, _I, _P, _I, _P, _I, _P]),
     "vst_layernorm": (_I, [_P, _I, _I, _I, _P, _P, _F, _P, _I, _I, _P, _I, _P]),
     "vst_add_row_table": (_I, [_P, _I, _I, _I, _P, _I, _I, _P, _I, _P]),
     "vst_unpack_tokens": (_I, [_P, _I, _I, _I, _I, _P, _P]),

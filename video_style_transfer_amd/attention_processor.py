@@ -95,6 +95,7 @@ class AnimateDiffAttnProcessor2_0:
     def __call__(self, attn, hidden_states, encoder_hidden_states=None, attention_mask=None, temb=None, scale=1.0,
                  **kwargs):
         fused_residual = kwargs.pop("_vst_residual", None)
+        lora_u = kwargs.pop("_vst_lora_u", None)  # x @ Acat^T of the q(/k/v) ops, from K.layer_norm_lora
         if attn.spatial_norm is not None or attn.group_norm is not None or attn.norm_cross:
             raise NotImplementedError("spatial_norm/group_norm/norm_cross are inert for SDXL (attention_processor.py:30-60)")
         if attention_mask is not None:
@@ -109,7 +110,7 @@ class AnimateDiffAttnProcessor2_0:
         hd = inner // heads
         x = hidden_states.reshape(batch * N, C)
         if encoder_hidden_states is None:
-            qkv = run_ops(x, build_ops([attn.to_q, attn.to_k, attn.to_v], s))
+            qkv = run_ops(x, build_ops([attn.to_q, attn.to_k, attn.to_v], s), u=lora_u)
             o = K.spatial_attention(qkv[:, :inner], qkv[:, inner:2 * inner], qkv[:, 2 * inner:], batch, heads, N, N,
                                     1, scale=hd ** -0.5) if hd == 64 else _generic_attention(qkv, batch, heads, N)
         else:
@@ -117,7 +118,7 @@ class AnimateDiffAttnProcessor2_0:
             be, L, D = enc.shape
             if batch % be:
                 raise ValueError(f"encoder batch {be} does not divide hidden batch {batch}")
-            q = run_ops(x, build_ops([attn.to_q], s))
+            q = run_ops(x, build_ops([attn.to_q], s), u=lora_u)
             kv = _text_kv(attn, enc, s)
             if hd != 64:
                 raise NotImplementedError("spatial cross-attention kernel is specialised for head_dim 64 (SDXL)")
@@ -128,6 +129,16 @@ class AnimateDiffAttnProcessor2_0:
         if input_ndim == 4:
             out = out.transpose(-1, -2).reshape(b4, c4, h4, w4)
         return _finish(attn, out, hidden_states)
+
+
+def input_lora_ops(attn, self_attention: bool, scale: float = 1.0):
+    """The projection operands AnimateDiffAttnProcessor2_0 will apply to this attention's hidden states
+    (q/k/v for self-attention, q for cross-attention), or None when another processor is installed.
+    Lets the producer of the hidden states (the block's LayerNorm) emit the LoRA down-projection."""
+    if not isinstance(attn.processor, AnimateDiffAttnProcessor2_0):
+        return None
+    s = _proj_scale(attn, scale)
+    return build_ops([attn.to_q, attn.to_k, attn.to_v] if self_attention else [attn.to_q], s)
 
 
 def _text_kv(attn, enc, s):

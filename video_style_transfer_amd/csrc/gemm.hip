@@ -313,39 +313,47 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
 
 // sum the split-K slabs and apply the epilogue.  geglu: slab columns are the interleaved
 // [h(32) | g(32)] blocks; each thread produces 8 output columns.
-// Skinny GEMM for the UnZipLoRA down-projection u = x · Acatᵀ (N = padded 2r·projections <= 64,
-// no epilogue): memory/latency-bound on reading x once.  A workgroup owns 16 rows and all N
-// columns; its 4 waves split K (wave w takes k-steps w, w+4, ...), issue all their fragment-shaped
-// loads of a group up front (lane l reads 16 B of row l&15 at k-chunk l>>4, which IS the 16x16x32
-// MFMA operand layout: no LDS staging), and the 4 partial accumulators are summed through LDS.
-// M/16 workgroups (512 at M = 8192) keep every CU busy; out-of-range rows / columns / K read as zero
-// through the buffer range check.
+// Skinny GEMM for the UnZipLoRA down-projection u = x . Acat^T (N = padded 2r per projection <= 64,
+// no epilogue): HBM/MALL-bound on reading x once.  A workgroup = 8 waves owns 32 rows (two 16-row
+// MFMA fragments) and all N columns; wave w takes the k32-steps w, w+8, ..., issuing a whole group
+// of fragment-shaped loads before its MFMAs (lane l reads 16 B of row l&15 at k-chunk l>>4, which IS
+// the 16x16x32 operand layout: no LDS staging).  Each W fragment feeds two row fragments, so the W
+// bytes read per x byte are N/32 (the L2 traffic that bounded the 16-row version).  The 8 partial
+// accumulators are summed through LDS (64 KiB at N = 64).  ceil(M/32) workgroups (256 at M = 8192), 2 per CU.
 template <int NJ>
-__global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs p) {
-  constexpr int SK = NJ <= 2 ? 12 : 8;  // k32 steps per wave per load group (all in flight at once)
-  __shared__ f32x4 red[3][NJ][64];
+__global__ __launch_bounds__(512, 2) void gemm_skinny_kernel(GemmArgs p) {
+  constexpr int MI = 2, NW = 8;
+  constexpr int SK = NJ <= 2 ? 6 : 3;  // k32-steps per wave per load group (all in flight at once)
+  __shared__ f32x4 red[NW][MI][NJ][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int m0 = blockIdx.x * 16;
+  const int m0 = blockIdx.x * 16 * MI;
   const auto ra = make_rsrc(p.A1, p.a1_bytes);
   const auto rw = make_rsrc(p.Wt, p.w_bytes);
   const int r = lane & 15, kc = (lane >> 4) * 8;
-  const int arow = m0 + r;
-  const uint32_t abase = arow < p.M ? (uint32_t)(arow * p.lda1 + kc) * 2u : (uint32_t)kOOB;
+  uint32_t abase[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int arow = m0 + 16 * i + r;
+    abase[i] = arow < p.M ? (uint32_t)(arow * p.lda1 + kc) * 2u : (uint32_t)kOOB;
+  }
   uint32_t wbase[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j)
     wbase[j] = (16 * j + r) < p.N ? (uint32_t)((16 * j + r) * p.ldw + kc) * 2u : (uint32_t)kOOB;
-  f32x4 acc[NJ];
+  f32x4 acc[MI][NJ];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nk = (p.K + 31) / 32;
-  for (int g = w; g < nk; g += 4 * SK) {
-    u32x4 a[SK], b[SK][NJ];
+  for (int g = w; g < nk; g += NW * SK) {
+    u32x4 a[SK][MI], b[SK][NJ];
 #pragma unroll
     for (int t = 0; t < SK; ++t) {
-      const int ks = g + 4 * t;
+      const int ks = g + NW * t;
       const bool kin = ks < nk && ks * 32 + kc < p.K;
-      a[t] = buf_load16(ra, kin ? (int)(abase + ks * 64u) : kOOB);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) a[t][i] = buf_load16(ra, kin ? (int)(abase[i] + ks * 64u) : kOOB);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) b[t][j] = buf_load16(rw, kin ? (int)(wbase[j] + ks * 64u) : kOOB);
     }
@@ -354,20 +362,29 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs p) {
 #pragma unroll
     for (int t = 0; t < SK; ++t)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j)
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8*>(&b[t][j]),
-                                                         *reinterpret_cast<bf16x8*>(&a[t]), acc[j], 0, 0, 0);
-  }
-  if (w > 0) {
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) red[w - 1][j][lane] = acc[j];
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8*>(&b[t][j]),
+                                                              *reinterpret_cast<bf16x8*>(&a[t][i]), acc[i][j], 0, 0, 0);
   }
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) red[w][i][j][lane] = acc[i][j];
   __syncthreads();
-  if (w > 0) return;
+  if (w >= MI) return;
+  // wave i (< MI) sums row fragment i over the 8 waves and stores it
+  const int i = w;
+  f32x4 sum[NJ];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) acc[j] += red[0][j][lane] + red[1][j][lane] + red[2][j][lane];
-  // acc[j][e] = C[m0 + (lane&15)][16j + 4(lane>>4) + e]
-  const int m = m0 + r;
+  for (int j = 0; j < NJ; ++j) {
+    sum[j] = red[0][i][j][lane];
+#pragma unroll
+    for (int q = 1; q < NW; ++q) sum[j] += red[q][i][j][lane];
+  }
+  // sum[j][e] = C[m0 + 16i + (lane&15)][16j + 4(lane>>4) + e]
+  const int m = m0 + 16 * i + r;
   if (m >= p.M) return;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
@@ -376,22 +393,22 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs p) {
     bf16_t* dst = p.C + (size_t)m * p.ldc + n;
     if (n + 4 <= p.N) {
       u32x2 v;
-      v[0] = pack2bf(acc[j][0], acc[j][1]);
-      v[1] = pack2bf(acc[j][2], acc[j][3]);
+      v[0] = pack2bf(sum[j][0], sum[j][1]);
+      v[1] = pack2bf(sum[j][2], sum[j][3]);
       *reinterpret_cast<u32x2*>(dst) = v;
     } else {
-      for (int e = 0; e < p.N - n; ++e) dst[e] = f2bf(acc[j][e]);
+      for (int e = 0; e < p.N - n; ++e) dst[e] = f2bf(sum[j][e]);
     }
   }
 }
 
 static int launch_skinny(const GemmArgs& a, hipStream_t s) {
-  const dim3 grid((a.M + 15) / 16);
+  const dim3 grid((a.M + 31) / 32);
   switch ((a.N + 15) / 16) {
-    case 1: hipLaunchKernelGGL(gemm_skinny_kernel<1>, grid, dim3(256), 0, s, a); break;
-    case 2: hipLaunchKernelGGL(gemm_skinny_kernel<2>, grid, dim3(256), 0, s, a); break;
-    case 3: hipLaunchKernelGGL(gemm_skinny_kernel<3>, grid, dim3(256), 0, s, a); break;
-    case 4: hipLaunchKernelGGL(gemm_skinny_kernel<4>, grid, dim3(256), 0, s, a); break;
+    case 1: hipLaunchKernelGGL(gemm_skinny_kernel<1>, grid, dim3(512), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(gemm_skinny_kernel<2>, grid, dim3(512), 0, s, a); break;
+    case 3: hipLaunchKernelGGL(gemm_skinny_kernel<3>, grid, dim3(512), 0, s, a); break;
+    case 4: hipLaunchKernelGGL(gemm_skinny_kernel<4>, grid, dim3(512), 0, s, a); break;
     default: return VST_ERR_ARG;
   }
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
@@ -570,8 +587,18 @@ static int gemm_ablate_env() {
   return v;
 }
 
+static int gemm_group_env() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("VST_GEMM_GROUP_M");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+
 static int run_gemm(GemmArgs& a, int amode, int geglu, int tile, int splits, hipStream_t s) {
   a.ablate = gemm_ablate_env();
+  a.group_m = gemm_group_env();
   if (tile == 5) return launch_skinny(a, s);
   if (amode == 2) {  // scalar-gather conv (conv_in): register-staged kernel, no split
     a.splits = 1;
@@ -678,8 +705,8 @@ extern "C" int vst_gemm(const void* A, int lda, const void* A2, int lda2, int K1
 // the input first (output 2H x 2W).  Output [nimg, OH, OW, Cout] with row stride ldc.
 extern "C" int vst_conv3x3_ex(const void* x1, int C1, const void* x2, int C2, int nimg, int H, int W, int stride,
                               int upsample, const void* Wt, int Cout, const float* bias, const float* row_bias,
-                              int row_bias_div, const void* R, int ldr, void* out, int ldc, int tile, int splits,
-                              void* workspace, size_t ws_bytes, void* stream) {
+                              int row_bias_div, int ld_row_bias, const void* R, int ldr, void* out, int ldc, int tile,
+                              int splits, void* workspace, size_t ws_bytes, void* stream) {
   if (!x1 || !Wt || !out || nimg <= 0 || H <= 0 || W <= 0 || Cout <= 0) return VST_ERR_ARG;
   if (stride != 1 && stride != 2) return VST_ERR_ARG;
   if (upsample && stride != 1) return VST_ERR_ARG;
@@ -696,7 +723,9 @@ extern "C" int vst_conv3x3_ex(const void* x1, int C1, const void* x2, int C2, in
   a.M = nimg * a.OH * a.OW; a.N = Cout;
   if (!vec) a.K = (a.K + 7) & ~7;  // scalar gather: pad K to a chunk; weight rows padded too
   a.Wt = (const bf16_t*)Wt; a.ldw = a.K;
-  a.bias = bias; a.rbias = row_bias; a.rbias_div = row_bias_div; a.ldrb = Cout;
+  if (row_bias && (row_bias_div <= 0 || (ld_row_bias && ld_row_bias < Cout) || ((ld_row_bias ? ld_row_bias : Cout) & 3)))
+    return VST_ERR_ARG;
+  a.bias = bias; a.rbias = row_bias; a.rbias_div = row_bias_div; a.ldrb = ld_row_bias ? ld_row_bias : Cout;
   a.R = (const bf16_t*)R; a.ldr = ldr; a.C = (bf16_t*)out; a.ldc = ldc;
   a.ws = (float*)workspace;
   a.a1_bytes = clamp_bytes((size_t)nimg * H * W * C1 * 2);
@@ -714,6 +743,6 @@ extern "C" int vst_conv3x3_ex(const void* x1, int C1, const void* x2, int C2, in
 extern "C" int vst_conv3x3(const void* x1, int C1, const void* x2, int C2, int nimg, int H, int W, int stride,
                            int upsample, const void* Wt, int Cout, const float* bias, const float* row_bias,
                            int row_bias_div, const void* R, int ldr, void* out, int ldc, void* stream) {
-  return vst_conv3x3_ex(x1, C1, x2, C2, nimg, H, W, stride, upsample, Wt, Cout, bias, row_bias, row_bias_div, R, ldr,
-                        out, ldc, 0, 1, nullptr, 0, stream);
+  return vst_conv3x3_ex(x1, C1, x2, C2, nimg, H, W, stride, upsample, Wt, Cout, bias, row_bias, row_bias_div, 0, R,
+                        ldr, out, ldc, 0, 1, nullptr, 0, stream);
 }

@@ -96,8 +96,8 @@ __device__ __forceinline__ void wait_vm() {
 // Grouped tile order: GROUP_M row panels sweep the N axis together, so the A and W panels a
 // k-slice needs are shared by ~GROUP_M tiles running concurrently on one XCD (L2 hits instead of
 // repeated MALL fetches).  `t` is an XCD-contiguous logical tile index.
-__device__ __forceinline__ void tile_coords(int t, int nbm, int nbn, int& bm, int& bn) {
-  constexpr int GROUP_M = 8;
+__device__ __forceinline__ void tile_coords(int t, int nbm, int nbn, int& bm, int& bn, int group_m = 8) {
+  const int GROUP_M = group_m;
   const int in_group = GROUP_M * nbn;
   const int gid = t / in_group, first_m = gid * GROUP_M;
   const int gsize = min(nbm - first_m, GROUP_M);
@@ -570,7 +570,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
   const int nk_all = (p.K + RBK - 1) / RBK;
   if constexpr (!SK) {
     int bm, bn;
-    tile_coords(xcd_remap(blockIdx.x, nbn * nbm), nbm, nbn, bm, bn);
+    tile_coords(xcd_remap(blockIdx.x, nbn * nbm), nbm, nbn, bm, bn, p.group_m > 0 ? p.group_m : 8);
     int kt0 = 0, kt1 = nk_all;
     if (EPI == 2) {
       kt0 = (int)((long long)nk_all * blockIdx.z / p.splits);

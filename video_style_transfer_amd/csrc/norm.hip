@@ -268,6 +268,152 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const bf16_t* __restrict
   }
 }
 
+// LayerNorm fused with the UnZipLoRA down-projection of the projections that consume its output
+// (BasicTransformerBlock norm1 -> attn1 q/k/v, norm2 -> attn2 q): y = LN(x) (bf16, as the reference's
+// LayerNorm output) and u = y . Acat^T (Acat: [R, C] bf16, R <= 64 a multiple of 16), reading x once.
+// A workgroup = 8 waves owns 32 rows; wave w holds the k32-chunks w, w+8, ... of both 16-row
+// fragments in registers in the 16x16x32 MFMA operand layout (lane l: row l&15, 8 channels at
+// chunk*32 + 8*(l>>4)).  Row statistics are two-pass (mean, then sum of squared deviations) reduced
+// over the 4 lanes of a row by shuffles and over the 8 waves through LDS; the normalised bf16 values
+// are stored (16 B per lane) and fed straight to the MFMAs; the 8 partial u tiles are summed via LDS.
+template <int NJ, int MAXT>
+__global__ __launch_bounds__(512, 2) void layernorm_lora_kernel(const bf16_t* __restrict__ x, int ldx, int C, int rows,
+                                                                const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta, float eps,
+                                                                const bf16_t* __restrict__ A, int R,
+                                                                bf16_t* __restrict__ y, int ldy, bf16_t* __restrict__ u,
+                                                                int ldu) {
+  constexpr int MI = 2, NW = 8;  // MAXT = ceil(C / 256) k32-chunks per wave (C <= 256 * MAXT)
+  __shared__ f32x4 red[NW][MI][NJ][64];
+  __shared__ float st[NW][MI][16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, kc = (lane >> 4) * 8;
+  const int m0 = blockIdx.x * 16 * MI;
+  const int nk = C / 32;
+  const auto rx = make_rsrc(x, (uint32_t)min<size_t>(((size_t)(rows - 1) * ldx + C) * 2, 0x7fffffffULL));
+  u32x4 raw[MAXT][MI];  // x kept packed (bf16) in registers; unpacked per pass
+  bool rowok[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) rowok[i] = m0 + 16 * i + r < rows;
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) {
+    const int ks = w + NW * t;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int off = (ks < nk && rowok[i]) ? ((m0 + 16 * i + r) * ldx + ks * 32 + kc) * 2 : kOOB;
+      raw[t][i] = buf_load16(rx, off);
+    }
+  }
+  // ---- mean ----
+  float s[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    s[i] = 0.f;
+#pragma unroll
+    for (int t = 0; t < MAXT; ++t) {
+      float v[8];
+      unpack8(raw[t][i], v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[i] += v[e];  // zero-filled beyond C
+    }
+    s[i] += __shfl_xor(s[i], 16);
+    s[i] += __shfl_xor(s[i], 32);
+    if (lane < 16) st[w][i][lane] = s[i];
+  }
+  __syncthreads();
+  float mean[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    float a = 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) a += st[q][i][r];
+    mean[i] = a / C;
+  }
+  __syncthreads();
+  // ---- variance (deviations from the mean, only over real channels) ----
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    float q2 = 0.f;
+#pragma unroll
+    for (int t = 0; t < MAXT; ++t) {
+      if (w + NW * t < nk) {
+        float v[8];
+        unpack8(raw[t][i], v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { const float d = v[e] - mean[i]; q2 += d * d; }
+      }
+    }
+    q2 += __shfl_xor(q2, 16);
+    q2 += __shfl_xor(q2, 32);
+    if (lane < 16) st[w][i][lane] = q2;
+  }
+  __syncthreads();
+  float rstd[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    float a = 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) a += st[q][i][r];
+    rstd[i] = rsqrtf(a / C + eps);
+  }
+  // ---- normalise, store y, u partials on MFMA ----
+  const auto ra = make_rsrc(A, (uint32_t)((size_t)R * C * 2));
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) {
+    const int ks = w + NW * t;
+    if (ks >= nk) break;  // wave-uniform
+    const int c = ks * 32 + kc;
+    const f32x4* g4 = reinterpret_cast<const f32x4*>(gamma + c);
+    const f32x4* b4 = reinterpret_cast<const f32x4*>(beta + c);
+    const f32x4 g0 = g4[0], g1 = g4[1], b0 = b4[0], b1 = b4[1];
+    u32x4 wf[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) wf[j] = buf_load16(ra, (16 * j + r) < R ? ((16 * j + r) * C + c) * 2 : kOOB);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      float v[8], o[8];
+      unpack8(raw[t][i], v);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[e] = (v[e] - mean[i]) * (rstd[i] * g0[e]) + b0[e];
+        o[e + 4] = (v[e + 4] - mean[i]) * (rstd[i] * g1[e]) + b1[e];
+      }
+      const u32x4 pk = pack8(o);
+      if (rowok[i]) *reinterpret_cast<u32x4*>(y + (size_t)(m0 + 16 * i + r) * ldy + c) = pk;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(&wf[j]),
+                                                            *reinterpret_cast<const bf16x8*>(&pk), acc[i][j], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) red[w][i][j][lane] = acc[i][j];
+  __syncthreads();
+  if (w >= MI) return;
+  const int i = w;
+  const int m = m0 + 16 * i + r;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    f32x4 sum = red[0][i][j][lane];
+#pragma unroll
+    for (int q = 1; q < NW; ++q) sum += red[q][i][j][lane];
+    const int n = 16 * j + 4 * (lane >> 4);  // sum[e] = u[m][n + e]
+    if (m < rows && n < R) {
+      u32x2 pv;
+      pv[0] = pack2bf(sum[0], sum[1]);
+      pv[1] = pack2bf(sum[2], sum[3]);
+      *reinterpret_cast<u32x2*>(u + (size_t)m * ldu + n) = pv;
+    }
+  }
+}
+
 }  // namespace vst
 
 using namespace vst;
@@ -378,5 +524,30 @@ extern "C" int vst_layernorm(const void* x, int ldx, int C, int rows, const floa
 #undef VST_LN
   else
     return VST_ERR_ARG;
+  return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+}
+
+extern "C" int vst_layernorm_lora(const void* x, int ldx, int C, int rows, const float* gamma, const float* beta,
+                                  float eps, const void* A, int R, void* y, int ldy, void* u, int ldu, void* stream) {
+  if (!x || !y || !u || !A || !gamma || !beta || rows <= 0 || C <= 0 || (C & 31) || C > 1280) return VST_ERR_ARG;
+  if (R <= 0 || R > 64 || (R & 15) || (ldx & 7) || (ldy & 7) || (ldu & 3) || ldu < R) return VST_ERR_ARG;
+  const dim3 grid((rows + 31) / 32), blk(512);
+  hipStream_t s = (hipStream_t)stream;
+#define VST_LNL(NJ, MT)                                                                                         \
+  hipLaunchKernelGGL((layernorm_lora_kernel<NJ, MT>), grid, blk, 0, s, (const bf16_t*)x, ldx, C, rows, gamma, beta, \
+                     eps, (const bf16_t*)A, R, (bf16_t*)y, ldy, (bf16_t*)u, ldu)
+#define VST_LNL_T(NJ)             \
+  if (C <= 256) VST_LNL(NJ, 1);   \
+  else if (C <= 512) VST_LNL(NJ, 2); \
+  else if (C <= 768) VST_LNL(NJ, 3); \
+  else VST_LNL(NJ, 5);
+  switch (R / 16) {
+    case 1: VST_LNL_T(1); break;
+    case 2: VST_LNL_T(2); break;
+    case 3: VST_LNL_T(3); break;
+    default: VST_LNL_T(4); break;
+  }
+#undef VST_LNL_T
+#undef VST_LNL
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }

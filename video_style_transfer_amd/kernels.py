@@ -179,12 +179,15 @@ def conv3x3(x1: torch.Tensor, nimg: int, H: int, W: int, w: torch.Tensor, bias: 
         raise _lib.VstError("conv3x3: bias must be fp32 [Cout]")
     if residual is not None:
         _dev(residual, BF16, "residual")
+    if row_bias is not None and (row_bias.dtype != F32 or not row_bias.is_cuda or row_bias.dim() != 2
+                                 or row_bias.stride(1) != 1 or row_bias.shape[1] != Cout):
+        raise _lib.VstError("conv3x3: row_bias must be an fp32 [nimg/div, Cout] device view with unit column stride")
     kind = "conv3x3" if (C1 + C2) % 64 == 0 else "conv3x3_small_cin"
     with _Rec(kind, 2.0 * M * Cout * kreal, 2.0 * (nimg * H * W * (C1 + C2) + Cout * kreal + M * Cout),
               lambda: gemm_kernel_name(M, Cout, w.shape[1], 2 if kind == "conv3x3" else 3), (M, Cout, w.shape[1])):
         ws = _workspace(x1.device)
         _lib.call("vst_conv3x3_ex", _p(x1), C1, _p(x2), C2, nimg, H, W, stride, 1 if upsample else 0, _p(w), Cout,
-                  _p(bias), _p(row_bias), row_bias_div, _p(residual), 0 if residual is None else _ld(residual),
+                  _p(bias), _p(row_bias), row_bias_div, 0 if row_bias is None else _ld(row_bias), _p(residual), 0 if residual is None else _ld(residual),
                   _p(out), _ld(out) if Cout >= 8 else Cout, GEMM_POLICY["tile"], GEMM_POLICY["splits"], _p(ws),
                   _WS_BYTES, _stream())
     return out
@@ -203,7 +206,7 @@ def spatial_attention(q, k, v, nbatch, heads, Nq, Nk, kv_div=1, out=None, scale=
     _dev(out, BF16, "out")
     scale = 0.125 if scale is None else scale
     with _Rec("spatial_attention", 4.0 * nbatch * heads * Nq * Nk * 64,
-              2.0 * 64 * heads * (2 * nbatch * Nq + 2 * (nbatch // kv_div) * Nk)):
+              2.0 * 64 * heads * (2 * nbatch * Nq + 2 * (nbatch // kv_div) * Nk), None, (nbatch * heads, Nq, Nk)):
         _lib.call("vst_spatial_attention", _p(q), _ld(q), _p(k), _p(v), k.stride(0), _p(out), _ld(out), nbatch,
                   heads, Nq, Nk, kv_div, 64, float(scale), _stream())
     return out
@@ -324,6 +327,23 @@ def unpack_tokens(src, out):
         raise _lib.VstError(f"unpack_tokens: src {tuple(src.shape)} vs out {tuple(out.shape)}")
     _lib.call("vst_unpack_tokens", _p(src), B, C, F, H * W, _p(out), _stream())
     return out
+
+
+def layer_norm_lora(x, gamma, beta, eps, A, *, r_alg=None, out=None):
+    """(LN(x), LN(x) @ A^T) in one pass; A: bf16 [R, C] (R % 16 == 0, <= 64) — LayerNorm + UnZipLoRA down."""
+    _dev(x, BF16, "x")
+    _dev(A, BF16, "A")
+    rows, C = x.shape
+    R = A.shape[0]
+    if A.shape[1] != C or R % 16 or R > 64 or C % 32 or C > 1280 or not A.is_contiguous():
+        raise _lib.VstError(f"layer_norm_lora: x {tuple(x.shape)} A {tuple(A.shape)}")
+    if out is None:
+        out = torch.empty((rows, C), dtype=BF16, device=x.device)
+    u = torch.empty((rows, R), dtype=BF16, device=x.device)
+    with _Rec("layernorm_lora", 2.0 * rows * C * (r_alg or R), 2.0 * (2 * rows * C + rows * R)):
+        _lib.call("vst_layernorm_lora", _p(x), _ld(x), C, rows, _p(gamma), _p(beta), float(eps), _p(A), R, _p(out),
+                  _ld(out), _p(u), R, _stream())
+    return out, u
 
 
 def layer_norm(x, gamma, beta, eps=1e-5, *, pe=None, pe_div=1, pe_mod=1, out=None):

@@ -173,10 +173,12 @@ def build_ops(lins: Sequence[nn.Module], scale: float = 1.0, mode: Optional[str]
     return ops
 
 
-def run_ops(x2d: torch.Tensor, ops: ProjOps, residual=None, out=None, geglu=False) -> torch.Tensor:
+def run_ops(x2d: torch.Tensor, ops: ProjOps, residual=None, out=None, geglu=False, u=None) -> torch.Tensor:
+    """`u` = x2d @ ops.a^T when the producer already computed it (K.layer_norm_lora)."""
     if ops.a is None:
         return K.linear(x2d, ops.w, ops.bias, residual=residual, out=out, geglu=geglu)
-    u = K.linear(x2d, ops.a, kind="gemm_lora_down", alg_n=ops.r)
+    if u is None:
+        u = K.linear(x2d, ops.a, kind="gemm_lora_down", alg_n=ops.r)
     return K.linear(x2d, ops.w, ops.bias, x2=u, residual=residual, out=out, geglu=geglu, alg_k2=ops.r)
 
 

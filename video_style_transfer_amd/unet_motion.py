@@ -29,7 +29,7 @@ import torch
 from torch import nn
 
 from . import kernels as K
-from .attention_processor import Attention
+from .attention_processor import Attention, input_lora_ops
 from .config import UNetMotionConfig
 from .lora_linear import LoRACompatibleLinear, build_ops, run_ops
 from .weights import sinusoid_table
@@ -63,6 +63,14 @@ class LayerNorm(nn.LayerNorm):
     def run(self, x, *, pe=None, pe_div=1, pe_mod=1, out=None):
         return K.layer_norm(x, f32(self.weight), f32(self.bias), self.eps, pe=pe, pe_div=pe_div, pe_mod=pe_mod,
                             out=out)
+
+    def run_lora(self, x, ops):
+        """(LN(x), LN(x) @ ops.a^T or None): the LoRA down-projection fused into the normalisation pass when
+        the consuming projections carry one and the shapes suit the fused kernel."""
+        C = x.shape[1]
+        if ops is None or ops.a is None or ops.a.shape[0] > 64 or C % 32 or C > 1280:
+            return self.run(x), None
+        return K.layer_norm_lora(x, f32(self.weight), f32(self.bias), self.eps, ops.a, r_alg=ops.r)
 
 
 class Conv3x3(nn.Conv2d):
@@ -120,6 +128,7 @@ class FwdCtx:
     enc: Optional[torch.Tensor]  # [B, L, D] bf16 text states
     cross_kwargs: dict
     shard: Optional[object] = None  # frame_shard.FrameShard when the clip's frames span ranks (F is per rank)
+    temb: Optional[dict] = None     # ResnetBlock2D -> fp32 [B, Cout] view of the batched time_emb_proj output
 
 
 # --------------------------------------------------------------------------------------- blocks
@@ -182,10 +191,11 @@ class BasicTransformerBlock(nn.Module):
             n = self.norm2.run(x, **kw)
             x = self.attn2(n.view(nimg, N, C), num_frames=ctx.F, _vst_residual=x).view(-1, C)
         else:
-            n = self.norm1.run(x)
-            x = self.attn1(n.view(nimg, N, C), _vst_residual=x, **ctx.cross_kwargs).view(-1, C)
-            n = self.norm2.run(x)
-            x = self.attn2(n.view(nimg, N, C), encoder_hidden_states=ctx.enc, _vst_residual=x,
+            scale = ctx.cross_kwargs.get("scale", 1.0)
+            n, u = self.norm1.run_lora(x, input_lora_ops(self.attn1, True, scale))
+            x = self.attn1(n.view(nimg, N, C), _vst_residual=x, _vst_lora_u=u, **ctx.cross_kwargs).view(-1, C)
+            n, u = self.norm2.run_lora(x, input_lora_ops(self.attn2, False, scale))
+            x = self.attn2(n.view(nimg, N, C), encoder_hidden_states=ctx.enc, _vst_residual=x, _vst_lora_u=u,
                            **ctx.cross_kwargs).view(-1, C)
         n = self.norm3.run(x)
         return self.ff.run(n, residual=x)
@@ -268,7 +278,10 @@ class ResnetBlock2D(nn.Module):
     def run(self, x1, nimg, H, W, ctx, x2=None):
         HW = H * W
         h = self.norm1.run(x1, nimg, HW, silu=True, x2=x2)
-        temb = self.time_emb_proj.run(ctx.emb_silu).float()  # [B, cout]; bf16-rounded like the reference
+        if ctx.temb is not None and self in ctx.temb:
+            temb = ctx.temb[self]  # view of the one batched projection (UNetMotionModel.batched_temb)
+        else:
+            temb = self.time_emb_proj.run(ctx.emb_silu).float()  # [B, cout]; bf16-rounded like the reference
         h = self.conv1.run(h, nimg, H, W, row_bias=temb, row_bias_div=ctx.F * HW)
         h = self.norm2.run(h, nimg, HW, silu=True)
         sc = self.conv_shortcut.run(x1, x2) if self.conv_shortcut is not None else x1
@@ -450,11 +463,25 @@ class UNetMotionModel(nn.Module):
         emb = self.add_embedding.run(add_in, residual=temb)  # emb = temb + aug_emb
         return K.silu(emb, out=out)
 
+    def batched_temb(self, emb_silu):
+        """time_emb_proj(SiLU(emb)) of EVERY ResnetBlock2D as one GEMM over the concatenated weights
+        ([B, sum Cout], bf16-rounded like the reference's per-block Linear, then fp32 once): 17 M=2
+        projections become one launch.  Returns {resnet: fp32 [B, Cout] view}."""
+        res = [m for m in self.modules() if isinstance(m, ResnetBlock2D)]
+        ops = build_ops([m.time_emb_proj for m in res], 1.0)
+        allt = run_ops(emb_silu, ops).float()
+        out, o = {}, 0
+        for m in res:
+            c = m.out_channels
+            out[m] = allt[:, o:o + c]
+            o += c
+        return out
+
     # ---- core (NHWC tokens) -----------------------------------------------------------------
     def forward_tokens(self, x, B, F, h, w, emb_silu, enc, cross_kwargs=None, shard=None):
         """x: [B*F*h*w, in_channels] bf16 -> noise prediction [B*F*h*w, out_channels] bf16.
         With `shard` (frame_shard.FrameShard), F is this rank's frames of each clip."""
-        ctx = FwdCtx(B, F, emb_silu, enc, cross_kwargs or {}, shard)
+        ctx = FwdCtx(B, F, emb_silu, enc, cross_kwargs or {}, shard, self.batched_temb(emb_silu))
         nimg = B * F
         H, W = h, w
         x = self.conv_in.run(x, nimg, H, W)
