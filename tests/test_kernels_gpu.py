@@ -61,7 +61,8 @@ def test_gemm_skinny_lora_down(cuda, K, M, N, Kd, tile):
 
 @pytest.mark.parametrize("M,N,Kd,K2", [(4096, 1280, 1280, 32), (4000, 1200, 640, 0), (8192, 1280, 2048, 64)])
 def test_gemm_underfilled_grids(cuda, K, M, N, Kd, K2):
-    """Tile counts that leave CUs idle under 256x256 (192x256 tiles; stream-K when VST_STREAMK=1)."""
+    """Tile counts that leave CUs idle under 256x256 (160 tiles on 256 CUs: the policy keeps 256x256; stream-K
+    when VST_STREAMK=1), and the same GEMMs forced onto the 192x256 tile."""
     g = torch.Generator().manual_seed(M + N + Kd)
     x, x2 = rnd(M, Kd, gen=g), (rnd(M, K2, gen=g) if K2 else None)
     w = rnd(N, Kd + K2, scale=(Kd + K2) ** -0.5, gen=g)
@@ -69,10 +70,14 @@ def test_gemm_underfilled_grids(cuda, K, M, N, Kd, K2):
     rb = torch.randn(M // 1000 + 1, N, generator=g)
     r = rnd(M, N, gen=g)
     name = K.gemm_kernel_name(M, N, Kd + K2, 0)
-    assert "192x256" in name or "streamk" in name, name
-    for _ in range(2):  # second launch (stream-K: flags must have been reset by the first)
-        out = K.linear(x.to(cuda), w.to(cuda), b.to(cuda), x2=None if x2 is None else x2.to(cuda),
-                       row_bias=rb.to(cuda), row_bias_div=1000, residual=r.to(cuda))
+    assert "256x256" in name, name
+    for tile in (0, 7, 0):  # policy tile, forced 192x256, policy again (stream-K: flags reset by the first)
+        K.GEMM_POLICY.update(tile=tile, splits=0)
+        try:
+            out = K.linear(x.to(cuda), w.to(cuda), b.to(cuda), x2=None if x2 is None else x2.to(cuda),
+                           row_bias=rb.to(cuda), row_bias_div=1000, residual=r.to(cuda))
+        finally:
+            K.GEMM_POLICY.update(tile=0, splits=0)
         xx = x if x2 is None else torch.cat([x, x2], 1)
         ref = xx.float() @ w.float().t() + b + rb.repeat_interleave(1000, 0)[:M] + r.float()
         check(out, ref, name=f"gemm {name} {M}x{N}x{Kd + K2}")
@@ -85,7 +90,7 @@ def test_conv_underfilled_grid(cuda, K):
     w = rnd(Co, Ci, 3, 3, scale=(9 * Ci) ** -0.5, gen=g)
     b = torch.randn(Co, generator=g) * 0.1
     name = K.gemm_kernel_name(n * H * W, Co, 9 * Ci, 2)
-    assert "192x256" in name or "streamk" in name, name
+    assert "256x256" in name or "streamk" in name, name
     out = K.conv3x3(to_nhwc(x).to(cuda), n, H, W, wflat(w).to(cuda), b.to(cuda))
     check(out, to_nhwc(conv_ref(x.float(), w.float(), b)), name=f"conv {name}")
 

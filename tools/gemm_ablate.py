@@ -16,6 +16,8 @@ SHAPES = [("qkv1280", 8192, 3840, 1344), ("ff2_1280", 8192, 1280, 5120), ("ff2_6
           ("ff1_1280_geglu", 8192, 10240, 1280), ("ff1_320_geglu", 131072, 2560, 320),
           ("down1280x32_skinny", 8192, 32, 1280), ("down1280x64_skinny", 8192, 64, 1280),
           ("down640x32_skinny", 32768, 32, 640), ("down640x64_skinny", 32768, 64, 640)]
+if os.environ.get("SHAPES"):
+    SHAPES = [sh for sh in SHAPES if sh[0] in os.environ["SHAPES"].split()]
 
 
 def timeit(fn, iters=20):

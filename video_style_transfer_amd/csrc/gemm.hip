@@ -492,25 +492,19 @@ static void choose(int M, int N, int K, int geglu, int conv, size_t ws_bytes, in
   const int mb = (M + 255) / 256;
   const int t256 = mb * ((N + 255) / 256), t256n = mb * ((N + 127) / 128);
   const int nk32 = (K + 31) / 32;  // ring kernel k-tiles
-  // Tile policy from tools/gemm_sweep.py on MI355X (UNet shapes at 16x512^2, CFG batch 2): the
-  // 256x256 ping-pong ring wins every projection / FF / GEGLU / conv shape of the path that has at
-  // least a quarter-wave of tiles (it beats 128x128 and 256x160 even at 160 tiles on 256 CUs);
+  // Tile policy (MI355X, measured in one process per comparison: tools/gemm_ablate.py TILES=..., bench.py):
+  // the 256x256 ping-pong ring wins every projection / FF / GEGLU / conv shape of the path with at least a
+  // quarter-wave of tiles, including the under-filled M = 8192, N = 1280 grids (160 tiles on 256 CUs:
+  // 38 us vs 56 us for 192x256 at K = 1312, 116 vs 190 us at K = 5120; whole step 88.6 vs 92.9 ms);
   // tiny-M GEMMs (text states, temb) use 128x128 with split-K; conv_out (Cout = 4) 128x64.
-  const int t192 = ((M + 191) / 192) * ((N + 255) / 256);
   if (tile == 0) {
     if (conv && N <= 64) tile = 2;
-    else if (t256 >= kCUs / 4) {
-      // 192x256 when it needs fewer CU-rounds x tile area (M = 8192 x N = 1280: 215 tiles in one
-      // round vs 160 of 256x256 leaving 96 CUs idle; N = 640: exactly 2 rounds vs 1.5)
-      const double c256 = (double)((t256 + kCUs - 1) / kCUs) * 256.0;
-      const double c192 = (double)((t192 + kCUs - 1) / kCUs) * 192.0 * 1.05;
-      tile = c192 < c256 ? 7 : 3;
-    } else {
-      tile = 1;
-    }
+    else if (t256 >= kCUs / 4) tile = 3;
+    else tile = 1;
   }
   if (geglu && (tile == 2 || tile == 6)) tile = 1;
   const int t160 = mb * ((N + 159) / 160);
+  const int t192 = ((M + 191) / 192) * ((N + 255) / 256);
   const int tiles = tile == 1 ? t128 : tile == 2 ? t64 : tile == 3 ? t256 : tile == 6 ? t160 : tile == 7 ? t192 : t256n;
   if (splits == 0) {
     splits = 1;
@@ -596,9 +590,22 @@ static int gemm_group_env() {
   return v;
 }
 
+// Persistent launch: measured (tools/gemm_persist.sh) 4-10 % faster for the GEGLU epilogue and neutral for
+// the others, so it is the default for GEGLU only.  VST_GEMM_PERSIST=1 forces it on, =0 off.
+static int gemm_persist_env() {
+  static int v = -2;
+  if (v == -2) {
+    const char* e = getenv("VST_GEMM_PERSIST");
+    v = e ? atoi(e) : -1;
+  }
+  return v;
+}
+
 static int run_gemm(GemmArgs& a, int amode, int geglu, int tile, int splits, hipStream_t s) {
   a.ablate = gemm_ablate_env();
   a.group_m = gemm_group_env();
+  const int pe = gemm_persist_env();
+  a.persist = (pe > 0 || (pe < 0 && geglu)) ? device_cus() : 0;
   if (tile == 5) return launch_skinny(a, s);
   if (amode == 2) {  // scalar-gather conv (conv_in): register-staged kernel, no split
     a.splits = 1;

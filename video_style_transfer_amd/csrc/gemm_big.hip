@@ -569,6 +569,25 @@ __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) 
   const int nbn = (p.N + BN - 1) / BN, nbm = (p.M + BM - 1) / BM;
   const int nk_all = (p.K + RBK - 1) / RBK;
   if constexpr (!SK) {
+    if (EPI != 2 && p.persist) {
+      // Persistent: gridDim.x workgroups (one per resident slot) walk the tiles.  Workgroup b runs on XCD
+      // b % 8 and takes that XCD's contiguous chunk of logical tiles in rounds, so co-resident tiles share
+      // L2 panels as in the one-tile-per-workgroup launch; the next tile's ring prologue follows the
+      // previous tile's epilogue stores without a workgroup relaunch (the stores drain under its DMA).
+      const int T = nbm * nbn, G = gridDim.x;
+      const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+      const int per_xcd = (G - xcd + 7) / 8;
+      const int q = T >> 3, r = T & 7;
+      const int beg = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+      const int cnt = q + (xcd < r ? 1 : 0);
+      for (int j = loc; j < cnt; j += per_xcd) {
+        int bm, bn;
+        tile_coords(beg + j, nbm, nbn, bm, bn, p.group_m > 0 ? p.group_m : 8);
+        ring_tile<Cfg, AMODE, EPI>(p, smem, bm * BM, bn * BN, 0, nk_all, 0, 0, 0);
+        __syncthreads();  // the staged epilogue tile / ring LDS is reused by the next tile
+      }
+      return;
+    }
     int bm, bn;
     tile_coords(xcd_remap(blockIdx.x, nbn * nbm), nbm, nbn, bm, bn, p.group_m > 0 ? p.group_m : 8);
     int kt0 = 0, kt1 = nk_all;
@@ -623,6 +642,11 @@ static int launch_ring_t(const GemmArgs& a, hipStream_t s, int splits) {
   const int nwg = ((a.M + Cfg::BM - 1) / Cfg::BM) * ((a.N + Cfg::BN - 1) / Cfg::BN);
   if constexpr (EPI == 0 && std::is_same_v<Cfg, Cfg256x256>) {  // stream-K (opt-in, see gemm.hip)
     if (a.sk_iters > 0) return launch_ring_k<Cfg, AMODE, EPI, true>(a, s, dim3(a.sk_grid));
+  }
+  if (EPI != 2 && a.persist > 0) {
+    const int per_cu = Cfg::NWAVES == 8 ? 1 : 2;
+    const int slots = a.persist * per_cu;
+    if (nwg > slots) return launch_ring_k<Cfg, AMODE, EPI, false>(a, s, dim3(slots, 1, 1));
   }
   return launch_ring_k<Cfg, AMODE, EPI, false>(a, s, dim3(nwg, 1, splits));
 }

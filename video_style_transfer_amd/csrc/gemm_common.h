@@ -18,6 +18,7 @@ struct GemmArgs {
   float* ws;  // split-K slabs [splits][M][N] fp32
   int splits;
   int act;     // EPI 0 only: 1 = GELU(erf) after the bias (TemporalTransformerBlock ffn, no residual / row bias)
+  int persist;  // > 0: persistent launch over `persist` CUs (VST_GEMM_PERSIST; 0 = one workgroup per tile)
   int group_m;  // grouped tile order: row panels per group (0 = default 8; VST_GEMM_GROUP_M for tuning)
   int ablate;  // diagnostics only (VST_GEMM_ABLATE): bit0 skip loop DMA, bit1 skip MFMA
   // stream-K (ring GEMM, 256x256): k-steps per workgroup (0 = data-parallel), grid, partial slots
