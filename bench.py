@@ -113,6 +113,13 @@ def roofline(den):
     if os.environ.get("VST_BENCH_SHAPES"):
         for key, (n, ms, fl) in sorted(shapes.items(), key=lambda kv: -kv[1][1]):
             print(f"[shape] {ms:8.3f} ms {n:4d}x {fl / (ms * 1e-3) / 1e12:7.1f} TF  {key}", file=sys.stderr)
+    # north-star view: the fused base + UnZipLoRA projection GEMMs (q/k/v, out, cross q) per shape
+    lora = {}
+    for key, (n, ms, fl) in shapes.items():
+        if key.startswith("gemm_lora "):
+            lora[key.split()[1]] = {"launches": n, "ms_per_step": round(ms, 3),
+                                   "tflops": round(fl / (ms * 1e-3) / 1e12, 1),
+                                   "frac": round(fl / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4)}
     dom_sym, dom = max(by.items(), key=lambda kv: kv[1]["ms"])
     mfma = dom["flops"] > 0
     if mfma:
@@ -135,6 +142,7 @@ def roofline(den):
         "avg_launch_ms": round(dom["ms"] / dom["launches"], 4),
         "flops_per_launch": dom["flops"] / dom["launches"],
         "kernel_time_ms_per_step": round(total_ms, 3),
+        "fused_lora_gemms": lora,
     }, table
 
 
