@@ -33,7 +33,9 @@ SHAPES = [
     ("sp1280_ff2", 8192, 1280, 5120, 0, False),
     ("text_kv_lora", 154, 2560, 2048, 64, False),
     ("text_lora_down", 154, 64, 2048, 0, False),
-    ("temb", 2, 1280, 1280, 0, False),
+    ("temb", 2, 13760, 1280, 0, False),
+    ("mm640_qkv", 32768, 1920, 640, 0, False),
+    ("mm1280_qkv", 8192, 3840, 1280, 0, False),
 ]
 CONVS = [
     # (name, nimg, H, W, Cin, Cout, stride, up, C2)
@@ -62,7 +64,7 @@ def timeit(fn, iters=20):
 
 def main():
     dev = torch.device("cuda")
-    variants = [(0, 0), (1, 1), (2, 1), (3, 1), (6, 1), (3, 2), (6, 2)]
+    variants = [(0, 0), (1, 1), (2, 1), (3, 1), (4, 1), (6, 1), (7, 1), (3, 2)]
     res = []
     for name, M, N, Kd, K2, geglu in SHAPES:
         x = torch.randn(M, Kd, device=dev).to(BF)
@@ -81,7 +83,7 @@ def main():
             except Exception as ex:  # noqa
                 row[f"t{t}s{s}"] = str(ex)[:40]
         K.GEMM_POLICY.update(tile=0, splits=0)
-        if not geglu:
+        if not geglu and not os.environ.get("NO_BLAS"):
             xx = torch.cat([x, x2], 1) if x2 is not None else x
             ms = timeit(lambda: torch.nn.functional.linear(xx, w, None))
             row["hipblaslt"] = round(fl / ms / 1e9, 1)
