@@ -46,6 +46,10 @@ __device__ __forceinline__ int k_off(int row, int chunk) { return row * 128 + ((
 // V tile: [64 keys][64 d], swizzle chosen for conflict-free ds_read_b64_tr_b16 over 8-row groups
 __device__ __forceinline__ int v_off(int row, int chunk) { return row * 128 + ((chunk ^ (((row >> 1) & 3) << 1)) << 4); }
 
+// Raw v_exp_f32 (2^x): the softmax arguments are <= 0, so the denormal-range fix-up that exp2f() wraps around
+// it (v_ldexp + compares + selects, ~4 VALU per score) only decides whether a ~1e-38 weight is flushed to 0.
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 constexpr int SA_KT = 64;                         // keys per tile
 constexpr int SA_TILE = SA_KT * 64 * 2;           // 8 KiB
 constexpr int SA_LDS = 4 * SA_TILE;               // K,V double-buffered
@@ -161,7 +165,7 @@ __global__ __launch_bounds__(256, 2) void spatial_attn_kernel(
       mx = fmaxf(mx, __shfl_xor(mx, 16));
       mx = fmaxf(mx, __shfl_xor(mx, 32));
       const float mnew = fmaxf(mrun[qb], mx);
-      alpha[qb] = exp2f((mrun[qb] - mnew) * scale_log2);
+      alpha[qb] = fast_exp2((mrun[qb] - mnew) * scale_log2);
       mrun[qb] = mnew;
       const float mb = mnew * scale_log2;
       float ls = 0.f;
@@ -169,7 +173,7 @@ __global__ __launch_bounds__(256, 2) void spatial_attn_kernel(
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float pv = exp2f(s[kt][qb][i] * scale_log2 - mb);
+          const float pv = fast_exp2(s[kt][qb][i] * scale_log2 - mb);
           s[kt][qb][i] = pv;
           ls += pv;
         }
@@ -308,7 +312,7 @@ __global__ __launch_bounds__(256) void temporal_attn_kernel(
     for (int a = 0; a < NT; ++a)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float pv = exp2f(s[a][c][i] * scale_log2 - mb);
+        const float pv = fast_exp2(s[a][c][i] * scale_log2 - mb);
         s[a][c][i] = pv;
         ls += pv;
       }
