@@ -15,7 +15,8 @@ SHAPES = [("qkv1280", 8192, 3840, 1344), ("ff2_1280", 8192, 1280, 5120), ("ff2_6
           ("proj320", 131072, 320, 320), ("qkv320", 131072, 960, 320), ("ff1_320", 131072, 2560, 320),
           ("ff1_1280_geglu", 8192, 10240, 1280), ("ff1_320_geglu", 131072, 2560, 320),
           ("down1280x32_skinny", 8192, 32, 1280), ("down1280x64_skinny", 8192, 64, 1280),
-          ("down640x32_skinny", 32768, 32, 640), ("down640x64_skinny", 32768, 64, 640)]
+          ("down640x32_skinny", 32768, 32, 640), ("down640x64_skinny", 32768, 64, 640),
+          ("proj1280", 8192, 1280, 1280)]
 if os.environ.get("SHAPES"):
     SHAPES = [sh for sh in SHAPES if sh[0] in os.environ["SHAPES"].split()]
 

@@ -10,6 +10,19 @@ timeout -k 10 480 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout
   > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
 tail -3 gpurun_out/pytest_gpu_$TAG.log
 fi
+if [ -n "$PMC" ]; then
+  md5sum video_style_transfer_amd/libvst_hip.so > gpurun_out/pmc_so.md5
+  for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 240 rocprofv3 --pmc $C --kernel-trace --output-format csv -d gpurun_out/pmc_$C -o pmc -- \
+      python -u bench.py --steps 1 --warmup 1 --no-graph --no-cpu-baseline --no-roofline \
+      > gpurun_out/pmc_$C.out 2> gpurun_out/pmc_$C.err || { echo "pmc $C failed"; tail -5 gpurun_out/pmc_$C.err; exit 1; }
+  done
+  python tools/pmc_traffic.py gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE gpurun_out/pmc_so.md5 \
+    > gpurun_out/pmc_traffic_$TAG.json || exit 1
+  rm -rf gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE
+  cp gpurun_out/pmc_traffic_$TAG.json profiles/pmc_traffic_r1.json  # the bench below reads it (same .so)
+  echo pmc done
+fi
 VST_BENCH_SHAPES=1 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err \
   || { echo "bench failed"; tail -20 gpurun_out/bench_$TAG.err; exit 1; }
 cat gpurun_out/bench_$TAG.json
@@ -21,16 +34,4 @@ STATS=$(find gpurun_out/prof_$TAG -name '*kernel_stats.csv' | head -1)
 if [ -n "$STATS" ]; then python tools/prof_summary.py "$STATS" > gpurun_out/kernel_stats_$TAG.csv; fi
 rm -rf gpurun_out/prof_$TAG
 
-if [ -n "$PMC" ]; then
-  md5sum video_style_transfer_amd/libvst_hip.so > gpurun_out/pmc_so.md5
-  for C in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 240 rocprofv3 --pmc $C --kernel-trace --output-format csv -d gpurun_out/pmc_$C -o pmc -- \
-      python -u bench.py --steps 1 --warmup 1 --no-graph --no-cpu-baseline --no-roofline \
-      > gpurun_out/pmc_$C.out 2> gpurun_out/pmc_$C.err || { echo "pmc $C failed"; tail -5 gpurun_out/pmc_$C.err; exit 1; }
-  done
-  python tools/pmc_traffic.py gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE gpurun_out/pmc_so.md5 \
-    > gpurun_out/pmc_traffic_$TAG.json || exit 1
-  rm -rf gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE
-  echo pmc done
-fi
 echo all done
