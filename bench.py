@@ -177,10 +177,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # VST_BENCH_REHEARSAL=gloo: rehearse the N-rank orchestration on a one-GPU box (every rank on cuda:0, gloo
+    # transport, eager steps) -- a correctness drill for the launcher path, never a scaling number.
+    rehearsal = os.environ.get("VST_BENCH_REHEARSAL") == "gloo"
+    if rehearsal:
+        local = 0
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -207,7 +215,9 @@ def main():
     den.set_prompt_embeds(enc[1:], pooled[1:], enc[:1], pooled[:1])
     den.init_latents(seed=42 + seed_rank)
     graph_note = None
-    if not args.no_graph:
+    if shard is not None and not shard.graph_capturable:
+        graph_note = f"{shard.backend} collectives are not graph-capturable; eager steps"
+    elif not args.no_graph:
         try:
             den.capture()
         except Exception as e:  # a collective that cannot be captured: same HIP kernels, eager launches
@@ -241,7 +251,7 @@ def main():
     dt = time.perf_counter() - t0
     if world > 1:
         import torch.distributed as dist
-        tt = torch.tensor([dt], device=dev)
+        tt = torch.tensor([dt], device="cpu" if rehearsal else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     ms_step = dt / args.steps * 1e3
