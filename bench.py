@@ -55,6 +55,7 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-peaks", action="store_true", help="skip the MFMA / HBM ceiling probes")
     ap.add_argument("--cpu-sample-frames", type=int, default=2)
     ap.add_argument("--seed", type=int, default=0)
     return ap.parse_args()
@@ -135,6 +136,7 @@ def roofline(den):
                       "tflops": round(d["flops"] / (d["ms"] * 1e-3) / 1e12, 1) if d["flops"] else None,
                       "gbs": round(d["bytes"] / (d["ms"] * 1e-3) / 1e9, 1)}
     traffic, tsrc = pmc_traffic(dom_sym)
+    step_flops = sum(d["flops"] for d in by.values())
     return {
         "bound": "mfma" if mfma else "hbm", "kernel": dom_sym, "achieved": round(achieved, 1), "peak": peak,
         "unit": unit, "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": tsrc,
@@ -143,7 +145,21 @@ def roofline(den):
         "flops_per_launch": dom["flops"] / dom["launches"],
         "kernel_time_ms_per_step": round(total_ms, 3),
         "fused_lora_gemms": lora,
+        "step_flops": step_flops,
     }, table
+
+
+def measured_peaks(dev, rl):
+    """Measured ceilings (vst_probe_mfma / vst_probe_hbm_read) next to the vendor peaks, and the dominant
+    kernel's fraction of the measured one (report both)."""
+    from video_style_transfer_amd import kernels as K
+    mf = K.probe_mfma_tflops(dev)
+    hb = K.probe_hbm_read_gbs(dev)
+    meas = mf if rl["bound"] == "mfma" else hb
+    return {"mfma_bf16_tflops": round(mf, 1), "hbm_read_gbs": round(hb, 1),
+            "frac_of_measured": round(rl["achieved"] / meas, 4),
+            "probes": "vst_probe_mfma: 1024 WGs x 8 waves x 16 independent 16x16x32 bf16 chains; "
+                      "vst_probe_hbm_read: 4 GiB streamed with 16-B non-temporal loads"}
 
 
 def cpu_baseline(args, cfg):
@@ -261,6 +277,16 @@ def main():
     ok = bool(torch.isfinite(den.lat).all().item())
 
     rl, table = (None, None) if args.no_roofline else roofline(den)
+    step = None
+    if rl is not None:
+        # whole denoise step against the chip: algorithmic flops of every launch (table in DESIGN.md 3) per
+        # graph-replayed step time
+        fl = rl.pop("step_flops")
+        step = {"alg_tflop": round(fl / 1e12, 2), "achieved_tflops": round(fl / (ms_step * 1e-3) / 1e12, 1),
+                "frac": round(fl / (ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4)}
+        if rank == 0 and not rehearsal and not args.no_peaks:
+            rl["peak_measured"] = measured_peaks(dev, rl)
+            step["frac_of_measured"] = round(step["achieved_tflops"] / rl["peak_measured"]["mfma_bf16_tflops"], 4)
     graphed = den.graph is not None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -285,7 +311,7 @@ def main():
                                        f"RCCL all-to-all around each motion module)" if shard is not None else
                                        f"replicas x{world}" if world > 1 else "single"),
                        "graph": graphed, "note": graph_note},
-            "roofline": rl, "cpu_baseline": cpu, "kernels": table, "finite": ok,
+            "roofline": rl, "step_roofline": step, "cpu_baseline": cpu, "kernels": table, "finite": ok,
             "setup_s": round(t_build, 1),
         }
         print(json.dumps(out))

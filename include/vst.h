@@ -124,6 +124,12 @@ int vst_step_advance(int* step_idx, void* stream);
 int vst_silu(const void* x, void* y, size_t n, void* stream);
 int vst_add(const void* a, const void* b, void* y, size_t n, void* stream);
 int vst_copy2d(const void* x, int ldx, void* y, int ldy, int rows, int cols, void* stream);
+/* Ceiling probes (no reference counterpart; bench.py's measured peaks next to the vendor figures,
+ * SURVEY §8(d)).  vst_probe_mfma: `grid` workgroups x 8 waves, each wave `iters` x 16 independent
+ * 16x16x32 bf16 MFMAs (flops = grid*8*iters*16*16384).  vst_probe_hbm_read: streams `bytes` of `src`
+ * with 16-B loads.  `out` receives nothing in practice (anti-dead-code sink, >= grid elements). */
+int vst_probe_mfma(int grid, int iters, float* out, void* stream);
+int vst_probe_hbm_read(const void* src, size_t bytes, int grid, unsigned* out, void* stream);
 const char* vst_version(void);
 
 #ifdef __cplusplus

@@ -393,3 +393,12 @@ def test_layer_norm_lora(cuda, K, rows, C, R):
     ref_y = F.layer_norm(x.float(), (C,), gam, bet, 1e-5)
     check(y, ref_y, name="ln_lora.y")
     check(u, ref_y.to(torch.bfloat16).float() @ A.float().t(), name="ln_lora.u")
+
+
+def test_ceiling_probes(cuda, K):
+    """The measured-peak probes bench.py reports: plausible MI355X magnitudes (well above any
+    kernel of the path, at or below the vendor peaks with some slack for clocks)."""
+    tf = K.probe_mfma_tflops(cuda, grid=512, iters=4000, reps=1)
+    gbs = K.probe_hbm_read_gbs(cuda, nbytes=1 << 30, reps=1)
+    assert 500.0 < tf < 3000.0, tf
+    assert 1000.0 < gbs < 9000.0, gbs

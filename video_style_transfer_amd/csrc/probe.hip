@@ -1,0 +1,65 @@
+// Ceiling probes: the measured counterparts of the vendor peaks bench.py divides by (SURVEY §8(d)
+// "use the vendor figures and a measured microbenchmark ceiling; report both").
+//
+//  * vst_probe_mfma: every wave issues `iters` rounds of 16 independent v_mfma_f32_16x16x32_bf16
+//    (16 accumulator chains, so the dependent-issue latency never stalls the pipe), 8 waves per
+//    workgroup (2 per SIMD), `grid` workgroups.  flops = grid * 8 * iters * 16 * 16384.
+//  * vst_probe_hbm_read: a grid-stride stream of 16-B non-temporal global loads over `bytes` (folded into one
+//    word per thread so nothing is dead), 4 loads in flight per thread.
+// Neither touches anything outside the caller's buffers; both return 0 / VST_ERR_*.
+#include "vst_common.h"
+
+namespace vst {
+
+__global__ __launch_bounds__(512) void probe_mfma_kernel(int iters, float* out) {
+  const int lane = threadIdx.x & 63;
+  bf16x8 a, b;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    a[i] = (__bf16)(1e-3f * (lane + i));
+    b[i] = (__bf16)(1e-3f * (lane - i));
+  }
+  f32x4 acc[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[j], 0, 0, 0);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) s += acc[j][0] + acc[j][1] + acc[j][2] + acc[j][3];
+  if (s == 1234.5f) out[blockIdx.x] = s;  // never true in practice; keeps the chain alive
+}
+
+__global__ __launch_bounds__(256) void probe_hbm_read_kernel(const void* src, size_t bytes, unsigned* out) {
+  const size_t nchunk = bytes / 16;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  const u32x4* p = reinterpret_cast<const u32x4*>(src);
+  u32x4 x = {0u, 0u, 0u, 0u};
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < nchunk; i += 4 * stride) {
+    const u32x4 v0 = __builtin_nontemporal_load(p + i);
+    const u32x4 v1 = __builtin_nontemporal_load(p + i + stride);
+    const u32x4 v2 = __builtin_nontemporal_load(p + i + 2 * stride);
+    const u32x4 v3 = __builtin_nontemporal_load(p + i + 3 * stride);
+    x ^= v0 ^ v1 ^ v2 ^ v3;
+  }
+  for (; i < nchunk; i += stride) x ^= p[i];
+  const unsigned r = x[0] ^ x[1] ^ x[2] ^ x[3];
+  if (r == 0x9e3779b9u) out[blockIdx.x] = r;  // data-dependent, practically never taken
+}
+
+}  // namespace vst
+
+extern "C" int vst_probe_mfma(int grid, int iters, float* out, void* stream) {
+  if (grid <= 0 || iters <= 0 || !out) return VST_ERR_ARG;
+  hipLaunchKernelGGL(vst::probe_mfma_kernel, dim3(grid), dim3(512), 0, (hipStream_t)stream, iters, out);
+  return hipGetLastError() == hipSuccess ? 0 : VST_ERR_LAUNCH;
+}
+
+extern "C" int vst_probe_hbm_read(const void* src, size_t bytes, int grid, unsigned* out, void* stream) {
+  if (!src || bytes < 16 || grid <= 0 || !out) return VST_ERR_ARG;
+  hipLaunchKernelGGL(vst::probe_hbm_read_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, src, bytes, out);
+  return hipGetLastError() == hipSuccess ? 0 : VST_ERR_LAUNCH;
+}

@@ -400,3 +400,36 @@ def euler_cfg_step(noise, lat, sigmas, step_idx, *, guidance=7.5, ncopy=2):
 
 def step_advance(step_idx):
     _lib.call("vst_step_advance", _p(step_idx), _stream())
+
+
+# ---- ceiling probes (bench.py: measured peaks next to the vendor figures) ----
+def probe_mfma_tflops(device, grid=1024, iters=20000, reps=3):
+    """Best-of-`reps` bf16 MFMA rate of vst_probe_mfma (16 independent 16x16x32 chains per wave)."""
+    sink = torch.empty(grid, dtype=F32, device=device)
+    flops = float(grid) * 8 * iters * 16 * 16384
+    best = 0.0
+    for _ in range(reps + 1):  # first launch warms the clocks
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        _lib.call("vst_probe_mfma", grid, iters, sink.data_ptr(), _stream())
+        e.record()
+        e.synchronize()
+        best = max(best, flops / (s.elapsed_time(e) * 1e-3) / 1e12)
+    return best
+
+
+def probe_hbm_read_gbs(device, nbytes=4 << 30, grid=4096, reps=3):
+    """Best-of-`reps` streaming read rate of vst_probe_hbm_read over an `nbytes` buffer (>> the 256 MB
+    Infinity Cache, so it is HBM)."""
+    buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    sink = torch.empty(grid, dtype=torch.int32, device=device)
+    best = 0.0
+    for _ in range(reps + 1):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        _lib.call("vst_probe_hbm_read", buf.data_ptr(), nbytes, grid, sink.data_ptr(), _stream())
+        e.record()
+        e.synchronize()
+        best = max(best, nbytes / (s.elapsed_time(e) * 1e-3) / 1e9)
+    del buf
+    return best
