@@ -264,7 +264,9 @@ def test_temporal_attention(cuda, K, nclip, Fr, HW, C):
 
 
 @pytest.mark.parametrize("ns,rps,C1,C2,silu", [(4, 64, 320, 0, True), (2, 1000, 640, 0, False),
-                                               (3, 64, 128, 64, True), (1, 16 * 256, 1280, 0, False)])
+                                               (3, 64, 128, 64, True), (1, 16 * 256, 1280, 0, False),
+                                               (32, 256, 1280, 1280, True), (5, 77, 640, 320, True),
+                                               (2, 9, 64, 0, False), (3, 700, 4096, 0, False)])
 def test_group_norm(cuda, K, ns, rps, C1, C2, silu):
     g = torch.Generator().manual_seed(ns * rps + C1)
     x1 = rnd(ns * rps, C1, gen=g) + 0.5

@@ -19,72 +19,84 @@
 
 namespace vst {
 
-constexpr int GN_ROWS = 256;  // rows per stats chunk
+// Launch geometry shared by the stats and apply passes: grid (nchunk, nsamples), each workgroup owns
+// `rpc` consecutive rows of one sample and has rps x CH threads (CH = C/8 16-B channel chunks per row,
+// rps = 512 / CH rows in flight per step), so no lane idles whatever C is, and `rpc` is chosen by the
+// host so that every launch has >= ~256 workgroups (the 16x16-latent GroupNorms have only 256 rows
+// per frame: one 256-row chunk per sample gave 32 workgroups and 0.7 TB/s).
+__host__ __device__ inline int gn_rps(int C) { return max(1, 512 / (C / 8)); }
 
-// x1: [rows, C1] (ld1), x2: [rows, C2] (ld2) ; channel c of the concat
-__device__ __forceinline__ const bf16_t* chan_ptr(const bf16_t* x1, int ld1, int C1, const bf16_t* x2, int ld2,
-                                                  size_t row, int c) {
-  return c < C1 ? x1 + row * ld1 + c : x2 + row * ld2 + (c - C1);
+// x1: [rows, C1] (ld1), x2: [rows, C2] (ld2): base pointer / stride of the source holding channel c
+__device__ __forceinline__ void gn_src(const bf16_t* x1, int ld1, int C1, const bf16_t* x2, int ld2, int c,
+                                       const bf16_t*& base, int& ld) {
+  if (c < C1) { base = x1 + c; ld = ld1; }
+  else { base = x2 + (c - C1); ld = ld2; }
 }
 
-__global__ __launch_bounds__(256) void gn_stats_kernel(const bf16_t* __restrict__ x1, int ld1, int C1,
+__global__ __launch_bounds__(512) void gn_stats_kernel(const bf16_t* __restrict__ x1, int ld1, int C1,
                                                        const bf16_t* __restrict__ x2, int ld2, int C2,
-                                                       int rows_per_sample, int groups, float* __restrict__ part) {
+                                                       int rows_per_sample, int rpc, int groups,
+                                                       float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) float gsm[];  // [rps][C] sums then sumsqs
   const int C = C1 + C2;
   const int CH = C / 8;
+  const int rps = blockDim.x / CH;
   const int s = blockIdx.y, chunk = blockIdx.x;
   const int nchunk = gridDim.x;
-  const int r_beg = chunk * GN_ROWS;
-  const int r_end = min(rows_per_sample, r_beg + GN_ROWS);
-  const size_t row0 = (size_t)s * rows_per_sample;
+  const int r_beg = chunk * rpc;
+  const int r_end = min(rows_per_sample, r_beg + rpc);
   const int tid = threadIdx.x;
-  // layout: each thread owns channel chunks {cch, cch+256, ...} and a row phase
-  const int rps = CH >= 256 ? 1 : 256 / CH;  // rows per step
-  float* ssum = gsm;
-  float* ssq = gsm + rps * C;
-  for (int i = tid; i < 2 * rps * C; i += 256) gsm[i] = 0.f;
-  __syncthreads();
-  for (int cbase = 0; cbase < CH; cbase += 256) {
-    int cch, rph;
-    if (CH >= 256) { cch = cbase + tid; rph = 0; }
-    else { cch = tid % CH; rph = tid / CH; }
-    if (cch >= CH || rph >= rps) continue;
-    const int c = cch * 8;
-    float a[8], q[8];
+  const int cch = tid % CH, rph = tid / CH, c = cch * 8;
+  const bf16_t* base;
+  int ld;
+  gn_src(x1, ld1, C1, x2, ld2, c, base, ld);
+  base += (size_t)s * rows_per_sample * ld;
+  float a[8], q[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { a[e] = 0.f; q[e] = 0.f; }
-    // GN_UNROLL independent 16-B loads in flight per thread (a dependent one-at-a-time loop is
-    // latency-bound: ~40 sequential HBM round trips per thread)
-    constexpr int GN_UNROLL = 8;
-    for (int r = r_beg + rph; r < r_end; r += GN_UNROLL * rps) {
-      u32x4 v[GN_UNROLL];
+  for (int e = 0; e < 8; ++e) { a[e] = 0.f; q[e] = 0.f; }
+  // GN_UNROLL independent 16-B loads in flight per thread
+  constexpr int GN_UNROLL = 8;
+  for (int r = r_beg + rph; r < r_end; r += GN_UNROLL * rps) {
+    u32x4 v[GN_UNROLL];
 #pragma unroll
-      for (int u = 0; u < GN_UNROLL; ++u) {
-        const int rr = r + u * rps;
-        v[u] = rr < r_end ? *reinterpret_cast<const u32x4*>(chan_ptr(x1, ld1, C1, x2, ld2, row0 + rr, c))
-                          : u32x4{0u, 0u, 0u, 0u};
-      }
-#pragma unroll
-      for (int u = 0; u < GN_UNROLL; ++u) {
-        float f[8];
-        unpack8(v[u], f);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) { a[e] += f[e]; q[e] += f[e] * f[e]; }
-      }
+    for (int u = 0; u < GN_UNROLL; ++u) {
+      const int rr = r + u * rps;
+      v[u] = rr < r_end ? *reinterpret_cast<const u32x4*>(base + (size_t)rr * ld) : u32x4{0u, 0u, 0u, 0u};
     }
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { ssum[rph * C + c + e] = a[e]; ssq[rph * C + c + e] = q[e]; }
+    for (int u = 0; u < GN_UNROLL; ++u) {
+      float f[8];
+      unpack8(v[u], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { a[e] += f[e]; q[e] += f[e] * f[e]; }
+    }
+  }
+  float* ssum = gsm;
+  float* ssq = gsm + rps * C;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { ssum[rph * C + c + e] = a[e]; ssq[rph * C + c + e] = q[e]; }
+  __syncthreads();
+  // fold the row phases column-parallel into row 0, then one wave per group sums its Cg columns by
+  // shuffles (a serial per-group loop over rps x Cg LDS reads was ~10 us of latency per workgroup)
+  for (int cc = tid; cc < C; cc += blockDim.x) {
+    float sa = ssum[cc], sq = ssq[cc];
+    for (int rr = 1; rr < rps; ++rr) { sa += ssum[rr * C + cc]; sq += ssq[rr * C + cc]; }
+    ssum[cc] = sa;
+    ssq[cc] = sq;
   }
   __syncthreads();
   const int Cg = C / groups;
-  for (int gi = tid; gi < groups; gi += 256) {
-    float a = 0.f, q = 0.f;
-    for (int rr = 0; rr < rps; ++rr)
-      for (int c = gi * Cg; c < (gi + 1) * Cg; ++c) { a += ssum[rr * C + c]; q += ssq[rr * C + c]; }
-    float* o = part + (((size_t)s * nchunk + chunk) * groups + gi) * 2;
-    o[0] = a;
-    o[1] = q;
+  const int lane = tid & 63, wave = tid >> 6, nwave = blockDim.x >> 6;  // full waves only
+  for (int gi = wave; wave < nwave && gi < groups; gi += nwave) {
+    float sa = 0.f, sq = 0.f;
+    for (int cc = lane; cc < Cg; cc += 64) { sa += ssum[gi * Cg + cc]; sq += ssq[gi * Cg + cc]; }
+    sa = wave_sum(sa);
+    sq = wave_sum(sq);
+    if (lane == 0) {
+      float* o = part + (((size_t)s * nchunk + chunk) * groups + gi) * 2;
+      o[0] = sa;
+      o[1] = sq;
+    }
   }
 }
 
@@ -120,32 +132,53 @@ __global__ __launch_bounds__(64) void gn_finalize_kernel(const float* __restrict
   }
 }
 
-__global__ __launch_bounds__(256) void gn_apply_kernel(const bf16_t* __restrict__ x1, int ld1, int C1,
+__global__ __launch_bounds__(512) void gn_apply_kernel(const bf16_t* __restrict__ x1, int ld1, int C1,
                                                        const bf16_t* __restrict__ x2, int ld2, int C2,
-                                                       int rows_per_sample, const float* __restrict__ scale,
+                                                       int rows_per_sample, int rpc, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, int act,
-                                                       bf16_t* __restrict__ y, int ldy, size_t total_chunks) {
+                                                       bf16_t* __restrict__ y, int ldy) {
   const int C = C1 + C2;
   const int CH = C / 8;
-  for (size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x; idx < total_chunks; idx += (size_t)gridDim.x * 256) {
-    const size_t row = idx / CH;
-    const int c = (int)(idx - row * CH) * 8;
-    const int s = (int)(row / rows_per_sample);
-    float f[8];
-    unpack8(*reinterpret_cast<const u32x4*>(chan_ptr(x1, ld1, C1, x2, ld2, row, c)), f);
-    const f32x4* sc = reinterpret_cast<const f32x4*>(scale + (size_t)s * C + c);
-    const f32x4* sh = reinterpret_cast<const f32x4*>(shift + (size_t)s * C + c);
-    const f32x4 a0 = sc[0], a1 = sc[1], b0 = sh[0], b1 = sh[1];
+  const int rps = blockDim.x / CH;
+  const int s = blockIdx.y;
+  const int r_beg = blockIdx.x * rpc;
+  const int r_end = min(rows_per_sample, r_beg + rpc);
+  const int cch = threadIdx.x % CH, rph = threadIdx.x / CH, c = cch * 8;
+  const bf16_t* base;
+  int ld;
+  gn_src(x1, ld1, C1, x2, ld2, c, base, ld);
+  const size_t row0 = (size_t)s * rows_per_sample;
+  base += row0 * ld;
+  bf16_t* yb = y + row0 * ldy + c;
+  // this thread's 8 channels of one sample: the affine is loaded once
+  const f32x4* sc = reinterpret_cast<const f32x4*>(scale + (size_t)s * C + c);
+  const f32x4* sh = reinterpret_cast<const f32x4*>(shift + (size_t)s * C + c);
+  const f32x4 a0 = sc[0], a1 = sc[1], b0 = sh[0], b1 = sh[1];
+  constexpr int U = 4;  // loads in flight per thread
+  for (int r = r_beg + rph; r < r_end; r += U * rps) {
+    u32x4 v[U];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      f[e] = f[e] * a0[e] + b0[e];
-      f[e + 4] = f[e + 4] * a1[e] + b1[e];
+    for (int u = 0; u < U; ++u) {
+      const int rr = r + u * rps;
+      v[u] = rr < r_end ? *reinterpret_cast<const u32x4*>(base + (size_t)rr * ld) : u32x4{0u, 0u, 0u, 0u};
     }
-    if (act) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] = silu(f[e]);
+    for (int u = 0; u < U; ++u) {
+      const int rr = r + u * rps;
+      if (rr >= r_end) break;
+      float f[8];
+      unpack8(v[u], f);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        f[e] = f[e] * a0[e] + b0[e];
+        f[e + 4] = f[e + 4] * a1[e] + b1[e];
+      }
+      if (act) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = silu(f[e]);
+      }
+      *reinterpret_cast<u32x4*>(yb + (size_t)rr * ldy) = pack8(f);
     }
-    *reinterpret_cast<u32x4*>(y + row * ldy + c) = pack8(f);
   }
 }
 
@@ -418,8 +451,21 @@ __global__ __launch_bounds__(512, 2) void layernorm_lora_kernel(const bf16_t* __
 
 using namespace vst;
 
+// rows per workgroup: >= ~256 workgroups (swept 256..4096 with tools/norm_bench.py), 8..256 rows each
+static inline int gn_rpc(int nsamples, int rows_per_sample) {
+  static const long long target = [] {
+    const char* e = getenv("VST_GN_TARGET");  // tuning only (tools/norm_bench.py)
+    return e ? std::max(1LL, atoll(e)) : 256LL;
+  }();
+  const long long total = (long long)nsamples * rows_per_sample;
+  return (int)std::max<long long>(8, std::min<long long>(256, (total + target - 1) / target));
+}
+static inline int gn_nchunk(int nsamples, int rows_per_sample) {
+  const int rpc = gn_rpc(nsamples, rows_per_sample);
+  return (rows_per_sample + rpc - 1) / rpc;
+}
 static inline size_t gn_part_floats(int nsamples, int rows_per_sample, int groups) {
-  const int nchunk = (rows_per_sample + GN_ROWS - 1) / GN_ROWS;
+  const int nchunk = gn_nchunk(nsamples, rows_per_sample);
   return ((size_t)nsamples * nchunk * groups * 2 + 3) & ~(size_t)3;  // keep scale/shift 16-B aligned
 }
 
@@ -437,22 +483,20 @@ extern "C" int vst_groupnorm(const void* x1, int ld1, int C1, const void* x2, in
   if (C > 4096) return VST_ERR_ARG;
   if (!x2) C2 = 0;
   hipStream_t s = (hipStream_t)stream;
-  const int nchunk = (rows_per_sample + GN_ROWS - 1) / GN_ROWS;
+  const int rpc = gn_rpc(nsamples, rows_per_sample);
+  const int nchunk = gn_nchunk(nsamples, rows_per_sample);
   float* part = (float*)workspace;
   float* scale = part + gn_part_floats(nsamples, rows_per_sample, groups);
   float* shift = scale + (size_t)nsamples * C;
   const int CH = C / 8;
-  const int rps = CH >= 256 ? 1 : 256 / CH;
+  const int rps = gn_rps(C);
   const size_t lds = (size_t)2 * rps * C * sizeof(float);
-  if (lds > 64 * 1024) return VST_ERR_ARG;
-  hipLaunchKernelGGL(gn_stats_kernel, dim3(nchunk, nsamples), dim3(256), lds, s, (const bf16_t*)x1, ld1, C1,
-                     (const bf16_t*)x2, ld2, C2, rows_per_sample, groups, part);
+  hipLaunchKernelGGL(gn_stats_kernel, dim3(nchunk, nsamples), dim3(rps * CH), lds, s, (const bf16_t*)x1, ld1, C1,
+                     (const bf16_t*)x2, ld2, C2, rows_per_sample, rpc, groups, part);
   hipLaunchKernelGGL(gn_finalize_kernel, dim3(nsamples * groups), dim3(64), 0, s, part, nchunk, rows_per_sample,
                      groups, C / groups, eps, gamma, beta, scale, shift, C);
-  const size_t total = (size_t)nsamples * rows_per_sample * CH;
-  const int grid = (int)std::min<size_t>((total + 255) / 256, 16384);
-  hipLaunchKernelGGL(gn_apply_kernel, dim3(grid), dim3(256), 0, s, (const bf16_t*)x1, ld1, C1, (const bf16_t*)x2,
-                     ld2, C2, rows_per_sample, scale, shift, silu_act, (bf16_t*)y, ldy, total);
+  hipLaunchKernelGGL(gn_apply_kernel, dim3(nchunk, nsamples), dim3(rps * CH), 0, s, (const bf16_t*)x1, ld1, C1,
+                     (const bf16_t*)x2, ld2, C2, rows_per_sample, rpc, scale, shift, silu_act, (bf16_t*)y, ldy);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 
@@ -472,14 +516,14 @@ extern "C" int vst_groupnorm_sums(const void* x1, int ld1, int C1, const void* x
   if (!x2) C2 = 0;
   const int C = C1 + C2;
   hipStream_t s = (hipStream_t)stream;
-  const int nchunk = (rows_per_sample + GN_ROWS - 1) / GN_ROWS;
+  const int rpc = gn_rpc(nsamples, rows_per_sample);
+  const int nchunk = gn_nchunk(nsamples, rows_per_sample);
   const int CH = C / 8;
-  const int rps = CH >= 256 ? 1 : 256 / CH;
+  const int rps = gn_rps(C);
   const size_t lds = (size_t)2 * rps * C * sizeof(float);
-  if (lds > 64 * 1024) return VST_ERR_ARG;
   float* part = (float*)workspace;
-  hipLaunchKernelGGL(gn_stats_kernel, dim3(nchunk, nsamples), dim3(256), lds, s, (const bf16_t*)x1, ld1, C1,
-                     (const bf16_t*)x2, ld2, C2, rows_per_sample, groups, part);
+  hipLaunchKernelGGL(gn_stats_kernel, dim3(nchunk, nsamples), dim3(rps * CH), lds, s, (const bf16_t*)x1, ld1, C1,
+                     (const bf16_t*)x2, ld2, C2, rows_per_sample, rpc, groups, part);
   hipLaunchKernelGGL(gn_sums_kernel, dim3(nsamples * groups), dim3(64), 0, s, part, nchunk, groups, sums);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
@@ -498,10 +542,11 @@ extern "C" int vst_groupnorm_apply_sums(const void* x1, int ld1, int C1, const v
   float* shift = scale + (size_t)nsamples * C;
   hipLaunchKernelGGL(gn_finalize_sums_kernel, dim3(nsamples * groups), dim3(64), 0, s, sums, count, groups,
                      C / groups, eps, gamma, beta, scale, shift, C);
-  const size_t total = (size_t)nsamples * rows_per_sample * (C / 8);
-  const int grid = (int)std::min<size_t>((total + 255) / 256, 16384);
-  hipLaunchKernelGGL(gn_apply_kernel, dim3(grid), dim3(256), 0, s, (const bf16_t*)x1, ld1, C1, (const bf16_t*)x2,
-                     ld2, C2, rows_per_sample, scale, shift, silu_act, (bf16_t*)y, ldy, total);
+  const int rpc = gn_rpc(nsamples, rows_per_sample);
+  const int nchunk = gn_nchunk(nsamples, rows_per_sample);
+  hipLaunchKernelGGL(gn_apply_kernel, dim3(nchunk, nsamples), dim3(gn_rps(C) * (C / 8)), 0, s, (const bf16_t*)x1,
+                     ld1, C1, (const bf16_t*)x2, ld2, C2, rows_per_sample, rpc, scale, shift, silu_act, (bf16_t*)y,
+                     ldy);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 
