@@ -4,12 +4,15 @@ insert_unziplora_to_unet (unziplora_unet/utils.py:388-484), unziplora_set_forwar
 get_lora_weights (:131-160; safetensors only, local path — no hub download offline),
 use_lora_weights_for_inference / use_lora_mergers_for_inference (:347-387),
 _make_lora_compatible (:712-725), freeze_spatial_layers / save_checkpoint /
-_extract_merger_state_dicts (animatediff/utils.py:66-163), synthetic UNet construction.
+_extract_merger_state_dicts (animatediff/utils.py:66-163), load_unet_with_motion / _find_pth
+(animatediff/utils.py:13-63: a diffusers SDXL `unet/` snapshot + a MotionAdapter snapshot or a trained
+motion_modules.pth, read offline with loaders that execute nothing), synthetic UNet construction.
 """
 from __future__ import annotations
 
+import json
 import os
-from typing import Dict, Optional, Union
+from typing import Dict, Optional, Tuple, Union
 
 import torch
 
@@ -135,7 +138,7 @@ def attach_unziplora_layers(unet, rank: int):
 
 
 def build_unet(cfg: Optional[UNetMotionConfig] = None, *, state_dict=None, seed: int = 0, lora_rank: Optional[int] = 8,
-               device="cuda", dtype=torch.bfloat16) -> UNetMotionModel:
+               device="cuda", dtype=torch.bfloat16, strict: bool = True) -> UNetMotionModel:
     """UNetMotionModel with UnZipLoRA layers, weights from `state_dict` or seeded synthetic ones."""
     cfg = cfg or UNetMotionConfig.sdxl()
     with torch.device("meta"):
@@ -153,7 +156,20 @@ def build_unet(cfg: Optional[UNetMotionConfig] = None, *, state_dict=None, seed:
     unet = unet.to_empty(device="cpu")
     if lora_rank:
         attach_unziplora_layers(unet, lora_rank)
-    unet.load_state_dict(state_dict, strict=True)
+    if not strict:
+        # the only keys a checkpoint may omit are the sinusoidal PE tables (diffusers rebuilds them too);
+        # UnZipLoRA factors come from insert_unziplora_to_unet (lora_rank=None here); anything else is an error
+        from .weights import sinusoid_table
+        for name, buf in unet.named_buffers():
+            if name.endswith("pos_embed.pe") or name.endswith("pos_encoding.pe"):
+                buf.copy_(sinusoid_table(buf.shape[-1], buf.shape[-2]).view_as(buf))
+        missing, unexpected = unet.load_state_dict(state_dict, strict=False)
+        missing = [k for k in missing if not k.endswith(".pe")]
+        if missing or unexpected:
+            raise KeyError(f"checkpoint does not match the architecture: missing {missing[:5]} "
+                           f"({len(missing)}), unexpected {unexpected[:5]} ({len(unexpected)})")
+    else:
+        unet.load_state_dict(state_dict, strict=True)
     unet.requires_grad_(False)
     # UNet weights in the compute dtype; UnZipLoRA params stay fp32 like the reference (dtype=None)
     for name, p in unet.named_parameters():
@@ -201,3 +217,98 @@ def save_checkpoint(unet, output_dir: str, step, save_mergers: bool = False):
         torch.save(mc, os.path.join(path, "merger_content_stage2.pth"))
         torch.save(ms, os.path.join(path, "merger_style_stage2.pth"))
     return path
+
+
+# ---------------------------------------------------------------------------------------------------------
+# Offline checkpoint formats: diffusers snapshots and the reference's motion_modules.pth
+# ---------------------------------------------------------------------------------------------------------
+def _load_tensor_file(path: str) -> Dict[str, torch.Tensor]:
+    """safetensors, or a torch pickle read with weights_only=True (nothing in the file is executed)."""
+    if path.endswith(".safetensors"):
+        from safetensors.torch import load_file
+        return load_file(path, device="cpu")
+    return torch.load(path, map_location="cpu", weights_only=True)
+
+
+def load_diffusers_weights(path: str, stem: str = "diffusion_pytorch_model") -> Dict[str, torch.Tensor]:
+    """State dict of a diffusers model folder (single file, fp16 variant, or a sharded index), or of a file."""
+    if os.path.isfile(path):
+        return _load_tensor_file(path)
+    for name in (f"{stem}.safetensors", f"{stem}.fp16.safetensors", f"{stem}.bin", f"{stem}.fp16.bin"):
+        p = os.path.join(path, name)
+        if os.path.isfile(p):
+            return _load_tensor_file(p)
+    for name in (f"{stem}.safetensors.index.json", f"{stem}.safetensors.index.fp16.json", f"{stem}.bin.index.json"):
+        p = os.path.join(path, name)
+        if os.path.isfile(p):
+            with open(p) as f:
+                shards = sorted(set(json.load(f)["weight_map"].values()))
+            sd = {}
+            for sh in shards:
+                sd.update(_load_tensor_file(os.path.join(path, sh)))
+            return sd
+    raise FileNotFoundError(f"no {stem} weights under {path}")
+
+
+def unet_config_from_diffusers(unet_cfg: dict, adapter_cfg: Optional[dict] = None) -> UNetMotionConfig:
+    """UNetMotionConfig from a diffusers UNet2DConditionModel config.json (+ MotionAdapter config.json).
+    diffusers' SDXL config names the per-block head COUNT `attention_head_dim` ([5, 10, 20]); a
+    `num_attention_heads` entry, when present, takes precedence (diffusers does the same)."""
+    heads = unet_cfg.get("num_attention_heads") or unet_cfg.get("attention_head_dim")
+    nb = len(unet_cfg["block_out_channels"])
+    as_tuple = lambda v: tuple(v) if isinstance(v, (list, tuple)) else (v,) * nb  # noqa: E731
+    motion = lambda t: t.replace("2D", "Motion")  # noqa: E731
+    add_dim = unet_cfg.get("addition_time_embed_dim") or 256
+    proj_in = unet_cfg.get("projection_class_embeddings_input_dim") or (1280 + 6 * add_dim)
+    kw = dict(in_channels=unet_cfg.get("in_channels", 4), out_channels=unet_cfg.get("out_channels", 4),
+              block_out_channels=tuple(unet_cfg["block_out_channels"]),
+              down_block_types=tuple(motion(t) for t in unet_cfg["down_block_types"]),
+              up_block_types=tuple(motion(t) for t in unet_cfg["up_block_types"]),
+              layers_per_block=unet_cfg.get("layers_per_block", 2),
+              transformer_layers_per_block=as_tuple(unet_cfg.get("transformer_layers_per_block", 1)),
+              num_attention_heads=as_tuple(heads), cross_attention_dim=unet_cfg.get("cross_attention_dim", 2048),
+              norm_num_groups=unet_cfg.get("norm_num_groups", 32), norm_eps=unet_cfg.get("norm_eps", 1e-5),
+              addition_time_embed_dim=add_dim, num_time_ids=6, text_embed_dim=proj_in - 6 * add_dim)
+    if adapter_cfg:
+        kw.update(motion_num_attention_heads=adapter_cfg.get("motion_num_attention_heads", 8),
+                  motion_max_seq_length=adapter_cfg.get("motion_max_seq_length", 32),
+                  motion_norm_num_groups=adapter_cfg.get("motion_norm_num_groups", 32),
+                  use_motion_mid_block=bool(adapter_cfg.get("use_motion_mid_block", False)))
+    return UNetMotionConfig(**kw)
+
+
+def _find_pth(path: str) -> Optional[str]:
+    """animatediff/utils.py:56-63: a trained motion_modules.pth given directly or inside a directory."""
+    if path.endswith(".pth") and os.path.isfile(path):
+        return path
+    if os.path.isdir(path):
+        cand = os.path.join(path, "motion_modules.pth")
+        if os.path.isfile(cand):
+            return cand
+    return None
+
+
+def load_unet_with_motion(pretrained_model_name_or_path: str, motion_adapter_path: str,
+                          torch_dtype: torch.dtype = torch.bfloat16, device: str = "cuda",
+                          lora_rank: Optional[int] = None) -> Tuple[UNetMotionModel, Optional[int]]:
+    """animatediff/utils.py:13-45 offline: SDXL `unet/` (config.json + weights) + the motion adapter folder,
+    or a trained `motion_modules.pth` (then the architecture's default adapter config applies, as the reference's
+    from_unet2d(base, None) does).  Returns (unet, motion_max_seq_length or None), like the reference."""
+    base = os.path.join(pretrained_model_name_or_path, "unet")
+    if not os.path.isdir(base):
+        base = pretrained_model_name_or_path
+    with open(os.path.join(base, "config.json")) as f:
+        unet_cfg = json.load(f)
+    pth = _find_pth(motion_adapter_path)
+    adapter_cfg = None
+    if pth is not None:
+        motion_sd = _load_tensor_file(pth)
+    else:
+        with open(os.path.join(motion_adapter_path, "config.json")) as f:
+            adapter_cfg = json.load(f)
+        motion_sd = load_diffusers_weights(motion_adapter_path)
+    cfg = unet_config_from_diffusers(unet_cfg, adapter_cfg)
+    sd = load_diffusers_weights(base)
+    sd.update({k: v for k, v in motion_sd.items() if "motion_modules" in k})
+    unet = build_unet(cfg, state_dict=sd, lora_rank=lora_rank, device=device, dtype=torch_dtype, strict=False)
+    return unet, (adapter_cfg.get("motion_max_seq_length") if adapter_cfg else None)
