@@ -245,7 +245,7 @@ def test_spatial_attention(cuda, K, nb, heads, Nq, Nk, kv_div):
     check(out, ref.transpose(1, 2).reshape(nb * Nq, C), name="sdpa")
 
 
-@pytest.mark.parametrize("nclip,Fr,HW,C", [(2, 16, 64, 320), (1, 32, 16, 640), (1, 16, 8, 1280), (3, 5, 7, 64),
+@pytest.mark.parametrize("nclip,Fr,HW,C", [(2, 16, 64, 320), (1, 32, 16, 640), (1, 16, 8, 1280), (1, 32, 4, 1280), (3, 5, 7, 64),
                                            (2, 16, 1, 128)])
 def test_temporal_attention(cuda, K, nclip, Fr, HW, C):
     g = torch.Generator().manual_seed(nclip * Fr + C)

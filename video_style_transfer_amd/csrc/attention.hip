@@ -232,17 +232,20 @@ __global__ __launch_bounds__(256, 2) void spatial_attn_kernel(
 
 // ---------------------------------------------------------------------------------
 // Temporal attention.  NT = number of 16-frame tiles (1: F<=16, 2: F<=32); D = head dim.
+// A workgroup holds `blockDim.x / 64` consecutive units, i.e. all heads of one (clip, pixel) when they fit: the
+// heads' 16-B q/k/v/o segments of a token row then meet in one CU's L1 instead of splitting cache lines
+// between workgroups on two XCDs.
 template <int NT, int D>
-__global__ __launch_bounds__(256) void temporal_attn_kernel(
+__global__ __launch_bounds__(512) void temporal_attn_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V, int ldqkv,
     bf16_t* __restrict__ O, int ldo, int nclip, int F, int HW, int heads, float scale_log2, uint32_t qkv_bytes) {
   constexpr int KS = (D + 31) / 32;  // 32-deep k-steps for S
   constexpr int DB = (D + 15) / 16;  // 16-wide d blocks for O
   constexpr int NF = 16 * NT;
   constexpr int VROW = DB * 32;      // bytes per V row in LDS
-  __shared__ __attribute__((aligned(16))) char vsm[4][NF * VROW];
+  extern __shared__ __attribute__((aligned(16))) char vsm[];  // [waves][NF * VROW]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int unit = blockIdx.x * 4 + wid;
+  const int unit = blockIdx.x * (blockDim.x >> 6) + wid;
   const int nunits = nclip * HW * heads;
   if (unit >= nunits) return;  // whole wave exits (unit is wave-uniform)
   const int h = unit % heads;
@@ -256,7 +259,7 @@ __global__ __launch_bounds__(256) void temporal_attn_kernel(
   auto row_of = [&](int f) { return (b * F + f) * HW + p; };
 
   // ---- stage V rows (zero rows >= F and columns >= D) ----
-  char* vs = vsm[wid];
+  char* vs = vsm + wid * (NF * VROW);
   constexpr int CPR = VROW / 16;  // 16-B chunks per LDS row
   for (int idx = lane; idx < NF * CPR; idx += 64) {
     const int f = idx / CPR, c = idx - f * CPR;
@@ -362,8 +365,11 @@ template <int NT, int D>
 static int launch_temporal(const bf16_t* Q, const bf16_t* K, const bf16_t* V, int ld, bf16_t* O, int ldo,
                            int nclip, int F, int HW, int heads, float sl2, uint32_t bytes, hipStream_t s) {
   const int units = nclip * HW * heads;
-  hipLaunchKernelGGL((temporal_attn_kernel<NT, D>), dim3((units + 3) / 4), dim3(256), 0, s, Q, K, V, ld, O, ldo,
-                     nclip, F, HW, heads, sl2, bytes);
+  constexpr int VBYTES = 16 * NT * ((D + 15) / 16) * 32;  // one wave's V tile
+  // all heads of a (clip, pixel) in one workgroup when they fit (<= 8 waves, <= 64 KiB of V tiles), else 4 units
+  const int wpg = (heads <= 8 && heads * VBYTES <= 64 * 1024) ? heads : 4;
+  hipLaunchKernelGGL((temporal_attn_kernel<NT, D>), dim3((units + wpg - 1) / wpg), dim3(64 * wpg), wpg * VBYTES, s,
+                     Q, K, V, ld, O, ldo, nclip, F, HW, heads, sl2, bytes);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 
