@@ -27,7 +27,7 @@ VST_BENCH_SHAPES=1 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > 
   || { echo "bench failed"; tail -20 gpurun_out/bench_$TAG.err; exit 1; }
 cat gpurun_out/bench_$TAG.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- \
-  python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/bench_prof_$TAG.json 2> gpurun_out/prof_$TAG.err \
+  python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-peaks > gpurun_out/bench_prof_$TAG.json 2> gpurun_out/prof_$TAG.err \
   || { echo "rocprof failed"; tail -20 gpurun_out/prof_$TAG.err; exit 1; }
 # keep only the stats summary (the raw traces overflow gpurun_out's copy-back limit)
 STATS=$(find gpurun_out/prof_$TAG -name '*kernel_stats.csv' | head -1)
