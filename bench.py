@@ -51,7 +51,8 @@ def parse():
                          "motion module, frame_shard.py); 'replicas' runs an independent clip per rank")
     ap.add_argument("--clips", type=int, default=0,
                     help="frames mode: clips denoised together (default N: per-GPU work fixed at one clip's "
-                         "frames = weak scaling; 1 = one clip split N ways = strong scaling)")
+                         "frames = weak scaling; 1 = one clip split N ways = strong scaling); N=1 or replicas: "
+                         "clips batched per GPU (throughput mode, not the headline)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
@@ -217,7 +218,7 @@ def main():
     set_lora_mode(args.lora_mode)
     t_build = time.perf_counter()
     unet = build_unet(cfg, seed=args.seed, lora_rank=args.lora_rank or None, device=dev)
-    shard, nclips = None, 1
+    shard, nclips = None, max(1, args.clips)
     if world > 1 and args.parallel == "frames":
         from video_style_transfer_amd.frame_shard import FrameShard
         shard = FrameShard()
@@ -272,7 +273,7 @@ def main():
         dt = float(tt.item())
     ms_step = dt / args.steps * 1e3
     # frames mode: nclips whole clips spread over all ranks; replicas: every rank denoises its own clip
-    frames_total = args.frames * nclips if shard is not None else args.frames * world
+    frames_total = args.frames * nclips if shard is not None else args.frames * nclips * world
     value = frames_total / (args.num_inference_steps * ms_step * 1e-3)
     ok = bool(torch.isfinite(den.lat).all().item())
 
@@ -305,11 +306,12 @@ def main():
                                    f"rank-{args.lora_rank} ({args.lora_mode}) on all 560 spatial q/k/v/out, "
                                    f"{args.num_inference_steps}-step Euler, CFG {args.guidance} batched (B=2)",
                        "model": "SDXL UNet + AnimateDiff-SDXL motion modules (synthetic weights)",
-                       "global_batch": nclips if shard is not None else world, "frames": args.frames,
+                       "global_batch": nclips if shard is not None else nclips * world, "frames": args.frames,
                        "resolution": args.size,
                        "parallelism": (f"frame-shard x{world} ({nclips} clips, {args.frames // world} frames/clip/GPU, "
                                        f"RCCL all-to-all around each motion module)" if shard is not None else
-                                       f"replicas x{world}" if world > 1 else "single"),
+                                       f"replicas x{world}" if world > 1 else "single") + (
+                                       f", {nclips} clips batched per GPU" if shard is None and nclips > 1 else ""),
                        "graph": graphed, "note": graph_note},
             "roofline": rl, "step_roofline": step, "cpu_baseline": cpu, "kernels": table, "finite": ok,
             "setup_s": round(t_build, 1),
