@@ -48,6 +48,35 @@ def lora_compatible_linear(x, W, b=None, delta=None, scale=1.0):
     return out
 
 
+def lora_unzip_linear(x, W, b=None, x1=None, x2=None, lora=None, forward_type="both", scale=1.0):
+    """lora_unzip.LoRACompatibleLinear.forward (unziplora_unet/lora_unzip.py:66-75): F.linear(x) + scale *
+    lora_layer(x1, x2) — base on the joint-prompt states x, the content LoRA on x1, the style LoRA on x2 (the
+    UnZipLoRALinearLayerInfer two-input forward, unziplora_linear_layer.py:298-346).  lora = (A_c, B_c, m_c,
+    A_s, B_s, m_s) or None."""
+    d = None if lora is None else unziplora_delta(x1, *lora, forward_type=forward_type, x_style=x2)
+    return lora_compatible_linear(x, W, b, d, scale)
+
+
+def unzip_attn_processor(hidden_states, encoder_hidden_states, enc_content, enc_style, heads, proj):
+    """AttnProcessor2_0.__call__ of the image path (unziplora_unet/unzip_attention_processor.py:671-759), 3-D
+    input, no mask: q = to_q(x | x, x); k, v = to_{k,v}(enc | enc_content, enc_style); SDPA; to_out(o | o, o).
+    proj(name, x, x1, x2) applies the projection.  Missing content/style states fall back to the joint ones
+    (the reference passes None through, which its LoRA layer cannot take)."""
+    enc = hidden_states if encoder_hidden_states is None else encoder_hidden_states
+    enc_c = enc if enc_content is None else enc_content
+    enc_s = enc if enc_style is None else enc_style
+    batch = hidden_states.shape[0]
+    q = proj("to_q", hidden_states, hidden_states, hidden_states)
+    k = proj("to_k", enc, enc_c, enc_s)
+    v = proj("to_v", enc, enc_c, enc_s)
+    hd = k.shape[-1] // heads
+    q = q.view(batch, -1, heads, hd).transpose(1, 2)
+    k = k.view(batch, -1, heads, hd).transpose(1, 2)
+    v = v.view(batch, -1, heads, hd).transpose(1, 2)
+    o = sdpa(q, k, v).transpose(1, 2).reshape(batch, -1, heads * hd)
+    return proj("to_out", o, o, o)
+
+
 # ----------------------------------------------------------------------------- attention
 def sdpa(q, k, v, scale=None):
     """F.scaled_dot_product_attention without mask/dropout (attention_processor.py:78-80), fp32."""

@@ -10,6 +10,7 @@ outputs).  Modules exercised:
                                        get_merged_motion_state_dict
   unziplora_unet/unziplora_linear_layer.py  UnZipLoRALinearLayerInfer (both/content/style, masked)
   unziplora_unet/lora_linear.py        LoRACompatibleLinear (+ UnZipLoRA layer)
+  unziplora_unet/lora_unzip.py         LoRACompatibleLinear, image-path dual-prompt variant (x, x_content, x_style)
 """
 import json
 import os
@@ -30,6 +31,7 @@ from animatediff.temporal_lora import (TemporalLoRALinear, build_spatial_lora_in
                                        compute_orth_loss, get_merged_motion_state_dict, inject_temporal_lora)
 from animatediff.temporal_transformer import PositionalEncoding, TemporalTransformer  # noqa: E402
 from unziplora_unet.lora_linear import LoRACompatibleLinear  # noqa: E402
+from unziplora_unet.lora_unzip import LoRACompatibleLinear as UnzipLoRACompatibleLinear  # noqa: E402
 from unziplora_unet.unziplora_linear_layer import UnZipLoRALinearLayerInfer  # noqa: E402
 
 torch.set_grad_enabled(False)
@@ -123,6 +125,31 @@ def gen_lora_linear():
     lin.set_lora_layer(None)
     T["out_nolora"] = lin(x)
     save("lora_linear", T, {"in": in_f, "out": out_f, "rank": 8})
+
+
+# --------------------------------------------------------------------------- 2b. lora_unzip dual-prompt linear
+def gen_lora_unzip():
+    """lora_unzip.py:66-75: base on x (joint prompt), content LoRA on x_1, style LoRA on x_2.
+    Text-token-shaped inputs (77 tokens, 2048 -> 640), as the K/V projections of cross-attention see them."""
+    gen = torch.Generator().manual_seed(9)
+    T = {}
+    in_f, out_f, r = 2048, 640, 8
+    lin = UnzipLoRACompatibleLinear(in_f, out_f, bias=False)
+    wf = S.make(out_f, in_f, 8, gen)
+    lin.weight.copy_(S.rebuild(wf, out_f, in_f))
+    layer = make_unziplora(gen, in_f, out_f, r)
+    lin.set_lora_layer(layer)
+    x, x1, x2 = (bf(torch.randn(1, 77, in_f, generator=gen)) for _ in range(3))
+    S.store("W", wf, T)
+    T["x"], T["x1"], T["x2"] = x, x1, x2
+    dump_unziplora(layer, "lora.", T)
+    for mode in ("both", "content", "style"):
+        layer.set_forward(mode)
+        T[f"out_{mode}_s1"] = lin(x, 1.0, x1, x2)
+        T[f"out_{mode}_s07"] = lin(x, 0.7, x1, x2)
+    lin.set_lora_layer(None)
+    T["out_nolora"] = lin(x)
+    save("lora_unzip", T, {"in": in_f, "out": out_f, "rank": r})
 
 
 # --------------------------------------------------------------------------- 3/4. attention processor
@@ -309,6 +336,7 @@ def gen_temporal_lora():
 if __name__ == "__main__":
     gen_unziplora()
     gen_lora_linear()
+    gen_lora_unzip()
     gen_processor()
     gen_temporal_core()
     gen_temporal_transformer()

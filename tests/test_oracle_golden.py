@@ -53,6 +53,17 @@ def test_lora_compatible_linear():
     close(R.lora_compatible_linear(T["x"], W, T["b"]), T["out_nolora"])
 
 
+def test_lora_unzip_dual_prompt_linear():
+    """a4: the image-path LoRACompatibleLinear (lora_unzip.py:66-75) with x, x_content, x_style all distinct."""
+    T, meta = load("lora_unzip")
+    W = S.rebuild(S.load("W", T), meta["out"], meta["in"])
+    lora = [T["lora." + k] for k in ("A_c", "B_c", "m_c", "A_s", "B_s", "m_s")]
+    for mode in ("both", "content", "style"):
+        for sc, tag in ((1.0, "s1"), (0.7, "s07")):
+            close(R.lora_unzip_linear(T["x"], W, None, T["x1"], T["x2"], lora, mode, sc), T[f"out_{mode}_{tag}"])
+    close(R.lora_unzip_linear(T["x"], W), T["out_nolora"])
+
+
 def _proj_fn(T, prefix, mode="both", scale=1.0, lora=True):
     def proj(name, x):
         key = "to_out.0" if name == "to_out" else name
