@@ -124,6 +124,11 @@ int vst_step_advance(int* step_idx, void* stream);
 int vst_silu(const void* x, void* y, size_t n, void* stream);
 int vst_add(const void* a, const void* b, void* y, size_t n, void* stream);
 int vst_copy2d(const void* x, int ldx, void* y, int ldy, int rows, int cols, void* stream);
+/* bf16 transpose y[c][r] = x[r][c] (x: rows x cols, row stride ldx; y: cols x rows, row stride ldy).  Backward-pass
+ * operand layout for dW = dY^T X and the temporal-LoRA factor gradients (no reference counterpart: torch.autograd
+ * of train_animatediff.py:265-319 does it implicitly). */
+int vst_transpose(const void* x, int ldx, int rows, int cols, void* y, int ldy, void* stream);
+
 /* Ceiling probes (no reference counterpart; bench.py's measured peaks next to the vendor figures,
  * SURVEY §8(d)).  vst_probe_mfma: `grid` workgroups x 8 waves, each wave `iters` x 16 independent
  * 16x16x32 bf16 MFMAs (flops = grid*8*iters*16*16384).  vst_probe_hbm_read: streams `bytes` of `src`

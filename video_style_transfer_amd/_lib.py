@@ -45,6 +45,7 @@ SIGNATURES = {
     "vst_silu": (_I, [_P, _P, _S, _P]),
     "vst_add": (_I, [_P, _P, _P, _S, _P]),
     "vst_copy2d": (_I, [_P, _I, _P, _I, _I, _I, _P]),
+    "vst_transpose": (_I, [_P, _I, _I, _I, _P, _I, _P]),
     "vst_probe_mfma": (_I, [_I, _I, _P, _P]),
     "vst_probe_hbm_read": (_I, [_P, _S, _I, _P, _P]),
     "vst_version": (ctypes.c_char_p, []),

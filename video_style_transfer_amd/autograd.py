@@ -1,0 +1,107 @@
+"""Training path, first piece: autograd Functions whose forward AND backward run on the HIP
+kernels, for the projections `train_animatediff.py` trains (train_animatediff.py:212-319).
+
+`LoRALinearFn`: y = x W^T + b + s (x A^T) B^T — `TemporalLoRALinear` (animatediff/temporal_lora.py:10-41, W frozen,
+A/B trainable) and the motion-module linears whose W/b are trainable (animatediff/utils.py:79-85 leaves FF and
+proj_in/out unfrozen).  With g = dL/dy (bf16, tokens x out):
+    forward   u = x A^T (skinny GEMM)            y = [x | u] . [W | s B]^T + b      (one fused GEMM)
+    backward  v = g B                            dX = [g | v] . [W^T | s A^T]^T     (one fused GEMM)
+              dA = s v^T x,  dB = s g^T u,  db = g^T 1 (a ones row appended to u^T),  dW = g^T x
+The weight-side products contract over the token axis, so g, x, u, v are transposed once (vst_transpose) into
+[features, tokens] operands for the ring GEMM; W^T is cached per weight version when W is frozen.
+Gradients come out of bf16 MFMA GEMMs with fp32 accumulation (as under the reference's bf16 autocast) and are
+cast to the parameters' dtypes.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import kernels as K
+from .lora_linear import pad32
+
+BF16 = torch.bfloat16
+
+
+def _wt(W: torch.Tensor) -> torch.Tensor:
+    """W^T (bf16, [in, out]); cached on the parameter while it is not being trained."""
+    if W.requires_grad:
+        return K.transpose(W.detach().to(BF16).contiguous())
+    key = (W.data_ptr(), W._version)
+    c = W.__dict__.get("_vst_wt")
+    if c is None or c[0] != key:
+        c = (key, K.transpose(W.detach().to(BF16).contiguous()))
+        W.__dict__["_vst_wt"] = c
+    return c[1]
+
+
+class LoRALinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x2d, W, b, A, B, s: float):
+        if x2d.shape[1] % 64 or W.shape[0] % 64:
+            raise ValueError("LoRALinearFn: in/out features must be multiples of 64 (two-source GEMM K split)")
+        r = A.shape[0]
+        P = pad32(max(r, 1))  # r = 0: a plain trainable linear (u stays zero)
+        dev = x2d.device
+        x2d = x2d.to(BF16).contiguous()
+        Wb = W.detach().to(BF16)
+        A_pad = torch.zeros(P, A.shape[1], device=dev, dtype=BF16)
+        A_pad[:r] = A.detach().to(BF16)
+        W_aug = torch.zeros(W.shape[0], W.shape[1] + P, device=dev, dtype=BF16)
+        W_aug[:, :W.shape[1]] = Wb
+        W_aug[:, W.shape[1]:W.shape[1] + r] = (B.detach().float() * s).to(BF16)
+        bias = None if b is None else b.detach().float().contiguous()
+        u = K.linear(x2d, A_pad, kind="gemm_lora_down", alg_n=r)
+        y = K.linear(x2d, W_aug, bias, x2=u, alg_k2=r)
+        ctx.save_for_backward(x2d, W, A, B, u, A_pad)
+        ctx.s = s
+        ctx.b_dtype = None if b is None else b.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x2d, W, A, B, u, A_pad = ctx.saved_tensors
+        s = ctx.s
+        g = g.to(BF16).contiguous()
+        M, N = g.shape
+        r = A.shape[0]
+        P = pad32(max(r, 1))
+        dev = g.device
+        BT = torch.zeros(P, N, device=dev, dtype=BF16)
+        BT[:r] = B.detach().t().to(BF16)
+        v = K.linear(g, BT, kind="gemm_lora_down", alg_n=r)                    # [M, P] = g B
+        need_x, need_w, need_b, need_a, need_bb = ctx.needs_input_grad[:5]
+        dX = dW = db = dA = dB = None
+        if need_x:
+            WT = _wt(W)                                                          # [in, N]
+            WT_aug = torch.zeros(WT.shape[0], N + P, device=dev, dtype=BF16)
+            WT_aug[:, :N] = WT
+            WT_aug[:, N:] = (A_pad.float().t() * s).to(BF16)
+            dX = K.linear(g, WT_aug, x2=v, alg_k2=r)                             # [M, in]
+        if need_w or need_b or need_a or need_bb:
+            gT = K.transpose(g)                                                  # [N, M]
+            if need_w or need_a:
+                xT = K.transpose(x2d)                                            # [in, M]
+            if need_w:
+                dW = K.linear(gT, xT).to(W.dtype)                                # [N, in] = g^T x
+            if need_a:
+                vT = K.transpose(v)                                              # [P, M]
+                dA = (K.linear(vT, xT)[:r].float() * s).to(A.dtype)             # [r, in] = s v^T x
+            if need_bb or need_b:
+                P1 = pad32(r + 1)
+                U1 = torch.zeros(P1, M, device=dev, dtype=BF16)
+                if r:
+                    K.transpose(u[:, :r], out=U1[:r])                            # u^T
+                U1[r].fill_(1.0)                                                 # ones row -> db
+                gu = K.linear(gT, U1)                                            # [N, P1]
+                if need_bb:
+                    dB = (gu[:, :r].float() * s).to(B.dtype)                     # [N, r] = s g^T u
+                if need_b:
+                    db = gu[:, r].float().to(ctx.b_dtype)
+        return dX, dW, db, dA, dB, None
+
+
+def lora_linear(x, W, b, A, B, s: float):
+    """y[..., out] = x W^T + b + s (x A^T) B^T with the HIP forward/backward (any leading shape)."""
+    x2 = x.reshape(-1, x.shape[-1])
+    y = LoRALinearFn.apply(x2, W, b, A, B, s)
+    return y.view(x.shape[:-1] + (W.shape[0],))

@@ -160,6 +160,56 @@ __global__ __launch_bounds__(256) void unpack_tokens_kernel(const bf16_t* __rest
   }
 }
 
+// bf16 transpose y[c][r] = x[r][c] through a 64x64 LDS tile (backward-pass operand layouts: dW = dY^T X needs
+// the token axis as the GEMM's K, i.e. row-major [features, tokens] copies of dY and X).
+__global__ __launch_bounds__(256) void transpose_kernel(const bf16_t* __restrict__ x, int ldx, int rows, int cols,
+                                                        bf16_t* __restrict__ y, int ldy) {
+  __shared__ uint16_t tile[64][66];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tid = threadIdx.x;
+  const bool vec_in = (cols & 7) == 0 && (ldx & 7) == 0;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int idx = tid + 256 * k;
+    const int r = idx >> 3, ch = (idx & 7) * 8;
+    const int gr = r0 + r, gc = c0 + ch;
+    uint16_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (gr < rows) {
+      if (vec_in && gc + 8 <= cols) {
+        const u32x4 w = *reinterpret_cast<const u32x4*>(x + (size_t)gr * ldx + gc);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { v[2 * e] = (uint16_t)(w[e] & 0xffffu); v[2 * e + 1] = (uint16_t)(w[e] >> 16); }
+      } else {
+        for (int e = 0; e < 8; ++e)
+          if (gc + e < cols) v[e] = x[(size_t)gr * ldx + gc + e];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) tile[r][ch + e] = v[e];
+  }
+  __syncthreads();
+  const bool vec_out = (rows & 7) == 0 && (ldy & 7) == 0;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int idx = tid + 256 * k;
+    const int c = idx >> 3, rr = (idx & 7) * 8;  // output row c0 + c, output columns r0 + rr .. +7
+    const int gc = c0 + c, gr = r0 + rr;
+    if (gc >= cols) continue;
+    uint16_t v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = tile[rr + e][c];
+    if (vec_out && gr + 8 <= rows) {
+      u32x4 w;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w[e] = (uint32_t)v[2 * e] | ((uint32_t)v[2 * e + 1] << 16);
+      *reinterpret_cast<u32x4*>(y + (size_t)gc * ldy + gr) = w;
+    } else {
+      for (int e = 0; e < 8; ++e)
+        if (gr + e < rows) y[(size_t)gc * ldy + gr + e] = v[e];
+    }
+  }
+}
+
 __global__ void step_advance_kernel(int* step) {
   if (threadIdx.x == 0 && blockIdx.x == 0) *step += 1;
 }
@@ -260,6 +310,15 @@ extern "C" int vst_unpack_tokens(const void* src, int B, int C, int F, int HW, f
   const dim3 grid((HW + 63) / 64, (C + 63) / 64, B * F);
   hipLaunchKernelGGL(unpack_tokens_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)src, C, F, HW,
                      out);
+  return ok();
+}
+
+extern "C" int vst_transpose(const void* x, int ldx, int rows, int cols, void* y, int ldy, void* stream) {
+  if (!x || !y || rows <= 0 || cols <= 0 || ldx < cols || ldy < rows) return VST_ERR_ARG;
+  const dim3 grid((cols + 63) / 64, (rows + 63) / 64);
+  if (grid.y > 65535) return VST_ERR_ARG;
+  hipLaunchKernelGGL(transpose_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ldx, rows, cols,
+                     (bf16_t*)y, ldy);
   return ok();
 }
 

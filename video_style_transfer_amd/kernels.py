@@ -378,6 +378,17 @@ def add(a, b, out=None):
     return out
 
 
+def transpose(x, out=None):
+    """bf16 [rows, cols] (row-major view) -> [cols, rows]."""
+    _dev(x, BF16, "x")
+    rows, cols = x.shape
+    if out is None:
+        out = torch.empty((cols, rows), dtype=BF16, device=x.device)
+    with _Rec("transpose", 0.0, 2.0 * 2 * rows * cols):
+        _lib.call("vst_transpose", _p(x), _ld(x), rows, cols, _p(out), _ld(out), _stream())
+    return out
+
+
 def copy2d(x, out):
     _lib.call("vst_copy2d", _p(x), _ld(x), _p(out), _ld(out), x.shape[0], x.shape[1], _stream())
     return out

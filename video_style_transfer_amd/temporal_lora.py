@@ -41,6 +41,11 @@ class TemporalLoRALinear(nn.Module):
         return self.lora_A.float(), self.lora_B.float() * self.scale
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if torch.is_grad_enabled() and (self.lora_A.requires_grad or self.lora_B.requires_grad
+                                        or self.base.weight.requires_grad):
+            # training (train_animatediff.py:265-319): HIP forward + backward through autograd.LoRALinearFn
+            from .autograd import lora_linear
+            return lora_linear(x, self.base.weight, self.base.bias, self.lora_A, self.lora_B, self.scale)
         x2 = x.reshape(-1, self.in_features)
         out = run_ops(x2, build_ops([self], 1.0))
         return out.view(x.shape[:-1] + (self.out_features,))
