@@ -129,6 +129,15 @@ int vst_copy2d(const void* x, int ldx, void* y, int ldy, int rows, int cols, voi
  * of train_animatediff.py:265-319 does it implicitly). */
 int vst_transpose(const void* x, int ldx, int rows, int cols, void* y, int ldy, void* stream);
 
+/* Training path (torch.autograd of train_animatediff.py:265-319 in the reference).
+ * vst_layernorm_bwd: dx and (dgamma, dbeta) of BasicTransformerBlock LayerNorm (x, g = dL/dy: rows x C bf16), stats
+ * recomputed; workspace of vst_layernorm_bwd_workspace_bytes(C, rows).  vst_geglu_bwd: dp of the GEGLU projection output
+ * p (32-interleaved [h | gate] blocks, as the fused GEMM stores them) from g = dL/d(h * gelu(gate)) (M x Nh). */
+size_t vst_layernorm_bwd_workspace_bytes(int C, int rows);
+int vst_layernorm_bwd(const void* x, int ldx, const void* g, int ldg, int C, int rows, const float* gamma, float eps,
+                      void* dx, int lddx, float* dgamma, float* dbeta, void* workspace, void* stream);
+int vst_geglu_bwd(const void* p, int ldp, const void* g, int ldg, int M, int Nh, void* dp, int lddp, void* stream);
+
 /* Ceiling probes (no reference counterpart; bench.py's measured peaks next to the vendor figures,
  * SURVEY §8(d)).  vst_probe_mfma: `grid` workgroups x 8 waves, each wave `iters` x 16 independent
  * 16x16x32 bf16 MFMAs (flops = grid*8*iters*16*16384).  vst_probe_hbm_read: streams `bytes` of `src`

@@ -98,3 +98,43 @@ def test_temporal_lora_linear_trains_on_hip(cuda):
         m.lora_B -= 50.0 * m.lora_B.grad
     loss2 = ((m(x).float() - target) ** 2).mean()
     assert loss2.item() < loss.item()
+
+
+@pytest.mark.parametrize("rows,C", [(512, 320), (300, 640), (1024, 1280), (64, 64)])
+def test_layer_norm_fn_grads(cuda, rows, C):
+    from video_style_transfer_amd.autograd import LayerNormFn
+    g = torch.Generator().manual_seed(rows + C)
+    xb = (torch.randn(rows, C, generator=g) + 0.3).to(BF)
+    gam, bet = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g) * 0.1
+    gy = torch.randn(rows, C, generator=g).to(BF)
+    xr, gr, br = xb.float().requires_grad_(True), gam.clone().requires_grad_(True), bet.clone().requires_grad_(True)
+    torch.nn.functional.layer_norm(xr, (C,), gr, br, 1e-5).backward(gy.float())
+    x = xb.to(cuda).requires_grad_(True)
+    gd, bd = gam.to(cuda).requires_grad_(True), bet.to(cuda).requires_grad_(True)
+    LayerNormFn.apply(x, gd, bd, 1e-5).backward(gy.to(cuda))
+    for name, got, ref in (("dx", x.grad, xr.grad), ("dgamma", gd.grad, gr.grad), ("dbeta", bd.grad, br.grad)):
+        e = rel(got, ref)
+        print(f"[train] LN {rows}x{C} {name}: rel_l2={e:.2e}")
+        assert e < 2e-2, (name, e)
+
+
+@pytest.mark.parametrize("M,C,Nh", [(512, 320, 1280), (256, 640, 2560), (96, 128, 64)])
+def test_geglu_fn_grads(cuda, M, C, Nh):
+    from video_style_transfer_amd.autograd import GEGLUFn
+    g = torch.Generator().manual_seed(M + C + Nh)
+    xb = torch.randn(M, C, generator=g).to(BF)
+    W = (torch.randn(2 * Nh, C, generator=g) * C ** -0.5).to(BF)
+    b = torch.randn(2 * Nh, generator=g) * 0.1
+    gy = torch.randn(M, Nh, generator=g).to(BF)
+    xr, Wr, br = xb.float().requires_grad_(True), W.float().requires_grad_(True), b.clone().requires_grad_(True)
+    h, gate = (xr @ Wr.t() + br).chunk(2, dim=-1)
+    (h * torch.nn.functional.gelu(gate)).backward(gy.float())
+    x, Wd, bd = xb.to(cuda).requires_grad_(True), W.to(cuda).requires_grad_(True), b.to(cuda).requires_grad_(True)
+    y = GEGLUFn.apply(x, Wd, bd)
+    y.backward(gy.to(cuda))
+    hr, gr = (xb.float() @ W.float().t() + b).chunk(2, dim=-1)
+    for name, got, ref in (("y", y, hr * torch.nn.functional.gelu(gr)), ("dX", x.grad, xr.grad),
+                           ("dW", Wd.grad, Wr.grad), ("db", bd.grad, br.grad)):
+        e = rel(got, ref)
+        print(f"[train] GEGLU {M}x{C}->{Nh} {name}: rel_l2={e:.2e}")
+        assert e < 2e-2, (name, e)

@@ -105,3 +105,73 @@ def lora_linear(x, W, b, A, B, s: float):
     x2 = x.reshape(-1, x.shape[-1])
     y = LoRALinearFn.apply(x2, W, b, A, B, s)
     return y.view(x.shape[:-1] + (W.shape[0],))
+
+
+class LayerNormFn(torch.autograd.Function):
+    """BasicTransformerBlock LayerNorm (unziplora_unet/unzip_attention.py:113-239; diffusers nn.LayerNorm) with the
+    HIP forward (vst_layernorm) and backward (vst_layernorm_bwd: dx, dgamma, dbeta; statistics recomputed)."""
+
+    @staticmethod
+    def forward(ctx, x2d, gamma, beta, eps: float):
+        x2d = x2d.to(BF16).contiguous()
+        g32 = gamma.detach().float().contiguous()
+        y = K.layer_norm(x2d, g32, beta.detach().float().contiguous(), eps)
+        ctx.save_for_backward(x2d, gamma)
+        ctx.eps = eps
+        ctx.beta_dtype = beta.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x2d, gamma = ctx.saved_tensors
+        dx, dgam, dbet = K.layer_norm_bwd(x2d, g.to(BF16).contiguous(), gamma.detach().float().contiguous(), ctx.eps)
+        return dx, dgam.to(gamma.dtype), dbet.to(ctx.beta_dtype), None
+
+
+def _interleave32(t: torch.Tensor) -> torch.Tensor:
+    """diffusers GEGLU proj rows [h; gate] -> the fused epilogue's [h_b (32) | gate_b (32)] blocks."""
+    two_nh = t.shape[0]
+    return t.reshape(2, two_nh // 64, 32, *t.shape[1:]).transpose(0, 1).reshape(t.shape)
+
+
+def _deinterleave32(t: torch.Tensor) -> torch.Tensor:
+    two_nh = t.shape[0]
+    return t.reshape(two_nh // 64, 2, 32, *t.shape[1:]).transpose(0, 1).reshape(t.shape)
+
+
+class GEGLUFn(torch.autograd.Function):
+    """diffusers GEGLU (proj = Linear(C, 2 Nh); out = h * gelu(gate)) of the motion / spatial FF: forward is the
+    fused GEGLU GEMM; backward recomputes p = x W^T + b, then vst_geglu_bwd -> dp, dX = dp W, dW = dp^T x,
+    db = dp^T 1, all in the 32-interleaved column order (de-interleaved for the parameters)."""
+
+    @staticmethod
+    def forward(ctx, x2d, W, b):
+        if W.shape[0] % 64 or x2d.shape[1] % 8:
+            raise ValueError("GEGLUFn: 2*Nh must be a multiple of 64")
+        x2d = x2d.to(BF16).contiguous()
+        Wi = _interleave32(W.detach().to(BF16)).contiguous()
+        bi = _interleave32(b.detach().float()).contiguous()
+        y = K.linear(x2d, Wi, bi, geglu=True)
+        ctx.save_for_backward(x2d, Wi, bi)
+        ctx.w_dtype, ctx.b_dtype = W.dtype, b.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x2d, Wi, bi = ctx.saved_tensors
+        M = x2d.shape[0]
+        p = K.linear(x2d, Wi, bi)                                              # [M, 2Nh] pre-activation
+        dp = K.geglu_bwd(p, g.to(BF16).contiguous())
+        need_x, need_w, need_b = ctx.needs_input_grad[:3]
+        dX = dW = db = None
+        if need_x:
+            dX = K.linear(dp, K.transpose(Wi))                                  # [M, C] = dp W
+        if need_w or need_b:
+            dpT = K.transpose(dp)                                              # [2Nh, M]
+            if need_w:
+                dW = _deinterleave32(K.linear(dpT, K.transpose(x2d))).to(ctx.w_dtype)
+            if need_b:
+                ones = torch.zeros(32, M, device=dp.device, dtype=BF16)
+                ones[0].fill_(1.0)
+                db = _deinterleave32(K.linear(dpT, ones)[:, 0].float()).to(ctx.b_dtype)
+        return dX, dW, db

@@ -210,6 +210,38 @@ __global__ __launch_bounds__(256) void transpose_kernel(const bf16_t* __restrict
   }
 }
 
+// GEGLU backward (training path): the FF projection output p is stored in the GEMM's 32-interleaved layout —
+// block b = [32 hidden | 32 gate] columns 64b.., producing output columns 32b.. (diffusers GEGLU:
+// out = h * gelu(gate)).  Given g = dL/dout:  dh = g * gelu(gate),  dgate = g * h * gelu'(gate),
+// gelu'(z) = Phi(z) + z * phi(z).  dp is written in the same interleaved layout (the dX / dW GEMMs use the
+// interleaved weights as they are).
+__global__ __launch_bounds__(256) void geglu_bwd_kernel(const bf16_t* __restrict__ p, int ldp,
+                                                        const bf16_t* __restrict__ g, int ldg, int M, int Nh,
+                                                        bf16_t* __restrict__ dp, int lddp) {
+  const int cpr = Nh / 8;  // 8-column chunks of g per row
+  const size_t total = (size_t)M * cpr;
+  for (size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (size_t)gridDim.x * 256) {
+    const int m = (int)(idx / cpr);
+    const int oc = (int)(idx - (size_t)m * cpr) * 8;
+    const int blk = oc >> 5, c = oc & 31;
+    const int hcol = blk * 64 + c, gcol = hcol + 32;
+    float gv[8], hv[8], zv[8], dh[8], dz[8];
+    unpack8(*reinterpret_cast<const u32x4*>(g + (size_t)m * ldg + oc), gv);
+    unpack8(*reinterpret_cast<const u32x4*>(p + (size_t)m * ldp + hcol), hv);
+    unpack8(*reinterpret_cast<const u32x4*>(p + (size_t)m * ldp + gcol), zv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float z = zv[e];
+      const float cdf = 0.5f * (1.0f + erf_fast(z * 0.70710678118654752f));
+      const float pdf = 0.3989422804014327f * __builtin_amdgcn_exp2f(-0.5f * z * z * 1.4426950408889634f);
+      dh[e] = gv[e] * z * cdf;
+      dz[e] = gv[e] * hv[e] * (cdf + z * pdf);
+    }
+    *reinterpret_cast<u32x4*>(dp + (size_t)m * lddp + hcol) = pack8(dh);
+    *reinterpret_cast<u32x4*>(dp + (size_t)m * lddp + gcol) = pack8(dz);
+  }
+}
+
 __global__ void step_advance_kernel(int* step) {
   if (threadIdx.x == 0 && blockIdx.x == 0) *step += 1;
 }
@@ -319,6 +351,18 @@ extern "C" int vst_transpose(const void* x, int ldx, int rows, int cols, void* y
   if (grid.y > 65535) return VST_ERR_ARG;
   hipLaunchKernelGGL(transpose_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ldx, rows, cols,
                      (bf16_t*)y, ldy);
+  return ok();
+}
+
+extern "C" int vst_geglu_bwd(const void* p, int ldp, const void* g, int ldg, int M, int Nh, void* dp, int lddp,
+                             void* stream) {
+  if (!p || !g || !dp || M <= 0 || Nh <= 0 || Nh % 32 || (ldp & 7) || (ldg & 7) || (lddp & 7) || ldp < 2 * Nh ||
+      lddp < 2 * Nh)
+    return VST_ERR_ARG;
+  const size_t total = (size_t)M * (Nh / 8);
+  const int grid = (int)std::min<size_t>((total + 255) / 256, 16384);
+  hipLaunchKernelGGL(geglu_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)p, ldp,
+                     (const bf16_t*)g, ldg, M, Nh, (bf16_t*)dp, lddp);
   return ok();
 }
 

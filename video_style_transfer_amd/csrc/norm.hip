@@ -447,6 +447,106 @@ __global__ __launch_bounds__(512, 2) void layernorm_lora_kernel(const bf16_t* __
   }
 }
 
+
+// LayerNorm backward (training path): one wave per row, grid-stride over rows.
+//   x^ = (x - mean) * rstd (recomputed, two-pass), gg = g * gamma,
+//   dx = rstd * (gg - mean(gg) - x^ * mean(gg * x^)),  dgamma += g * x^,  dbeta += g.
+// The per-channel sums are kept per lane, folded over the 4 waves in LDS and written as one [2][C] partial per
+// workgroup; layernorm_bwd_reduce_kernel sums the partials in a fixed order (deterministic).
+template <int MAXCH>
+__global__ __launch_bounds__(256) void layernorm_bwd_kernel(const bf16_t* __restrict__ x, int ldx,
+                                                            const bf16_t* __restrict__ g, int ldg, int C, int rows,
+                                                            const float* __restrict__ gamma, float eps,
+                                                            bf16_t* __restrict__ dx, int lddx, float* __restrict__ part) {
+  __shared__ float red[4][2][MAXCH * 512];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int CH = C / 8;
+  float gm[MAXCH][8], dg[MAXCH][8], db[MAXCH][8];
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int cc = lane + 64 * i;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { gm[i][e] = cc < CH ? gamma[cc * 8 + e] : 0.f; dg[i][e] = 0.f; db[i][e] = 0.f; }
+  }
+  for (int row = blockIdx.x * 4 + w; row < rows; row += gridDim.x * 4) {
+    float xv[MAXCH][8], gv[MAXCH][8];
+#pragma unroll
+    for (int i = 0; i < MAXCH; ++i) {
+      const int cc = lane + 64 * i;
+      u32x4 rx = u32x4{0u, 0u, 0u, 0u}, rg = u32x4{0u, 0u, 0u, 0u};
+      if (cc < CH) {
+        rx = *reinterpret_cast<const u32x4*>(x + (size_t)row * ldx + cc * 8);
+        rg = *reinterpret_cast<const u32x4*>(g + (size_t)row * ldg + cc * 8);
+      }
+      unpack8(rx, xv[i]);
+      unpack8(rg, gv[i]);
+    }
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXCH; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sum += xv[i][e];
+    const float mean = wave_sum(sum) / C;
+    float sq = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXCH; ++i)
+      if (lane + 64 * i < CH) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { const float d = xv[i][e] - mean; sq += d * d; }
+      }
+    const float rstd = rsqrtf(wave_sum(sq) / C + eps);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXCH; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xh = (xv[i][e] - mean) * rstd;
+        const float gg = gv[i][e] * gm[i][e];
+        xv[i][e] = xh;
+        s1 += gg;
+        s2 += gg * xh;
+        dg[i][e] += gv[i][e] * xh;
+        db[i][e] += gv[i][e];
+      }
+    s1 = wave_sum(s1) / C;
+    s2 = wave_sum(s2) / C;
+#pragma unroll
+    for (int i = 0; i < MAXCH; ++i) {
+      const int cc = lane + 64 * i;
+      if (cc < CH) {
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = rstd * (gv[i][e] * gm[i][e] - s1 - xv[i][e] * s2);
+        *reinterpret_cast<u32x4*>(dx + (size_t)row * lddx + cc * 8) = pack8(o);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int cc = lane + 64 * i;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { red[w][0][cc * 8 + e] = dg[i][e]; red[w][1][cc * 8 + e] = db[i][e]; }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { a += red[q][0][c]; b += red[q][1][c]; }
+    part[((size_t)blockIdx.x * 2) * C + c] = a;
+    part[((size_t)blockIdx.x * 2 + 1) * C + c] = b;
+  }
+}
+
+__global__ __launch_bounds__(256) void layernorm_bwd_reduce_kernel(const float* __restrict__ part, int nblk, int C,
+                                                                   float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= 2 * C) return;
+  const int which = c / C, cc = c - which * C;
+  float a = 0.f;
+  for (int b = 0; b < nblk; ++b) a += part[((size_t)b * 2 + which) * C + cc];
+  (which ? dbeta : dgamma)[cc] = a;
+}
+
 }  // namespace vst
 
 using namespace vst;
@@ -594,5 +694,34 @@ extern "C" int vst_layernorm_lora(const void* x, int ldx, int C, int rows, const
   }
 #undef VST_LNL_T
 #undef VST_LNL
+  return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+}
+
+// ---- LayerNorm backward (training path) ----
+static inline int lnb_grid(int rows) { return std::max(1, std::min(1024, (rows + 3) / 4)); }
+
+extern "C" size_t vst_layernorm_bwd_workspace_bytes(int C, int rows) {
+  return (size_t)lnb_grid(rows) * 2 * C * sizeof(float);
+}
+
+extern "C" int vst_layernorm_bwd(const void* x, int ldx, const void* g, int ldg, int C, int rows, const float* gamma,
+                                 float eps, void* dx, int lddx, float* dgamma, float* dbeta, void* workspace,
+                                 void* stream) {
+  if (!x || !g || !dx || !gamma || !dgamma || !dbeta || !workspace || rows <= 0 || C <= 0 || C % 8 ||
+      (ldx & 7) || (ldg & 7) || (lddx & 7) || C > 2048)
+    return VST_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = lnb_grid(rows);
+  float* part = (float*)workspace;
+  const int CH = C / 8;
+#define VST_LNB(MC)                                                                                            \
+  hipLaunchKernelGGL((layernorm_bwd_kernel<MC>), dim3(grid), dim3(256), 0, s, (const bf16_t*)x, ldx, (const bf16_t*)g, \
+                     ldg, C, rows, gamma, eps, (bf16_t*)dx, lddx, part)
+  if (CH <= 64) VST_LNB(1);
+  else if (CH <= 128) VST_LNB(2);
+  else VST_LNB(4);
+#undef VST_LNB
+  hipLaunchKernelGGL(layernorm_bwd_reduce_kernel, dim3((2 * C + 255) / 256), dim3(256), 0, s, part, grid, C, dgamma,
+                     dbeta);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }

@@ -389,6 +389,35 @@ def transpose(x, out=None):
     return out
 
 
+def layer_norm_bwd(x, g, gamma, eps=1e-5):
+    """LayerNorm backward: (dx bf16 [rows, C], dgamma fp32 [C], dbeta fp32 [C])."""
+    _dev(x, BF16, "x")
+    _dev(g, BF16, "g")
+    rows, C = x.shape
+    dx = torch.empty((rows, C), dtype=BF16, device=x.device)
+    dgamma = torch.empty(C, dtype=F32, device=x.device)
+    dbeta = torch.empty(C, dtype=F32, device=x.device)
+    ws = torch.empty((_lib.load().vst_layernorm_bwd_workspace_bytes(C, rows) + 3) // 4, dtype=F32, device=x.device)
+    with _Rec("layernorm_bwd", 0.0, 2.0 * 3 * rows * C):
+        _lib.call("vst_layernorm_bwd", _p(x), _ld(x), _p(g), _ld(g), C, rows, _p(gamma), float(eps), _p(dx), _ld(dx),
+                  _p(dgamma), _p(dbeta), _p(ws), _stream())
+    return dx, dgamma, dbeta
+
+
+def geglu_bwd(p, g, out=None):
+    """dp (32-interleaved like p) from p = the GEGLU projection output and g = dL/d(h * gelu(gate))."""
+    _dev(p, BF16, "p")
+    _dev(g, BF16, "g")
+    M, Nh = g.shape
+    if p.shape != (M, 2 * Nh):
+        raise _lib.VstError(f"geglu_bwd: p {tuple(p.shape)} vs g {tuple(g.shape)}")
+    if out is None:
+        out = torch.empty((M, 2 * Nh), dtype=BF16, device=p.device)
+    with _Rec("geglu_bwd", 0.0, 2.0 * 5 * M * Nh):
+        _lib.call("vst_geglu_bwd", _p(p), _ld(p), _p(g), _ld(g), M, Nh, _p(out), _ld(out), _stream())
+    return out
+
+
 def copy2d(x, out):
     _lib.call("vst_copy2d", _p(x), _ld(x), _p(out), _ld(out), x.shape[0], x.shape[1], _stream())
     return out
