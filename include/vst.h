@@ -136,6 +136,11 @@ int vst_transpose(const void* x, int ldx, int rows, int cols, void* y, int ldy, 
 size_t vst_layernorm_bwd_workspace_bytes(int C, int rows);
 int vst_layernorm_bwd(const void* x, int ldx, const void* g, int ldg, int C, int rows, const float* gamma, float eps,
                       void* dx, int lddx, float* dgamma, float* dbeta, void* workspace, void* stream);
+/* vst_temporal_attention_bwd: gradients of vst_temporal_attention (same token layout and q/k/v views) from dO; dq/dk/dv
+ * are written with row stride lddqkv (e.g. column views of one [tokens, 3C] buffer).  F <= 32, head_dim <= 256. */
+int vst_temporal_attention_bwd(const void* q, const void* k, const void* v, int ldqkv, const void* dout, int lddo,
+                               void* dq, void* dk, void* dv, int lddqkv, int nclip, int F, int HW, int heads,
+                               int head_dim, float scale, void* stream);
 int vst_geglu_bwd(const void* p, int ldp, const void* g, int ldg, int M, int Nh, void* dp, int lddp, void* stream);
 
 /* Ceiling probes (no reference counterpart; bench.py's measured peaks next to the vendor figures,

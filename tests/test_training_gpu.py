@@ -138,3 +138,30 @@ def test_geglu_fn_grads(cuda, M, C, Nh):
         e = rel(got, ref)
         print(f"[train] GEGLU {M}x{C}->{Nh} {name}: rel_l2={e:.2e}")
         assert e < 2e-2, (name, e)
+
+
+@pytest.mark.parametrize("nclip,Fr,HW,C", [(2, 16, 8, 320), (1, 32, 4, 640), (1, 16, 2, 1280), (3, 5, 7, 64)])
+def test_temporal_attention_fn_grads(cuda, nclip, Fr, HW, C):
+    import math
+    from video_style_transfer_amd.autograd import TemporalAttentionFn
+    heads, d = 8, C // 8
+    g = torch.Generator().manual_seed(nclip * Fr + C)
+    qkv = torch.randn(nclip * Fr * HW, 3 * C, generator=g).to(BF)
+    gy = torch.randn(nclip * Fr * HW, C, generator=g).to(BF)
+
+    def seq(t):  # rows (b*F+f)*HW+p -> (b*HW+p, heads, F, d)
+        return t.view(nclip, Fr, HW, heads, d).permute(0, 2, 3, 1, 4).reshape(nclip * HW, heads, Fr, d)
+
+    qr = qkv.float().requires_grad_(True)
+    q, k, v = seq(qr[:, :C]), seq(qr[:, C:2 * C]), seq(qr[:, 2 * C:])
+    o = torch.softmax(q @ k.transpose(-1, -2) / math.sqrt(d), -1) @ v
+    ref = o.view(nclip, HW, heads, Fr, d).permute(0, 3, 1, 2, 4).reshape(nclip * Fr * HW, C)
+    ref.backward(gy.float())
+    x = qkv.to(cuda).requires_grad_(True)
+    out = TemporalAttentionFn.apply(x, nclip, Fr, HW, heads)
+    out.backward(gy.to(cuda))
+    for name, got, want in (("o", out, ref), ("dq", x.grad[:, :C], qr.grad[:, :C]),
+                            ("dk", x.grad[:, C:2 * C], qr.grad[:, C:2 * C]), ("dv", x.grad[:, 2 * C:], qr.grad[:, 2 * C:])):
+        e = rel(got, want)
+        print(f"[train] temporal attn {nclip}x{Fr}x{HW} C={C} {name}: rel_l2={e:.2e}")
+        assert e < 2e-2, (name, e)

@@ -175,3 +175,29 @@ class GEGLUFn(torch.autograd.Function):
                 ones[0].fill_(1.0)
                 db = _deinterleave32(K.linear(dpT, ones)[:, 0].float()).to(ctx.b_dtype)
         return dX, dW, db
+
+
+class TemporalAttentionFn(torch.autograd.Function):
+    """Motion-module attention core over the frame axis (the diffusers AnimateDiffTransformer3D attention as
+    restated in animatediff/attention_processor.py; tokens [(b*F + f)*HW + p, C]).  Input: the fused q/k/v
+    projection output [tokens, 3C]; its gradient comes back as one [tokens, 3C] buffer (vst_temporal_attention_bwd),
+    which is what the fused projection's backward consumes."""
+
+    @staticmethod
+    def forward(ctx, qkv, nclip: int, F: int, HW: int, heads: int):
+        qkv = qkv.to(BF16).contiguous()
+        C = qkv.shape[1] // 3
+        o = K.temporal_attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], nclip, F, HW, heads, C // heads)
+        ctx.save_for_backward(qkv)
+        ctx.dims = (nclip, F, HW, heads)
+        return o
+
+    @staticmethod
+    def backward(ctx, g):
+        (qkv,) = ctx.saved_tensors
+        nclip, F, HW, heads = ctx.dims
+        C = qkv.shape[1] // 3
+        dqkv = torch.empty_like(qkv)
+        K.temporal_attention_bwd(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], g.to(BF16).contiguous(), nclip, F, HW,
+                                 heads, C // heads, out=dqkv)
+        return dqkv, None, None, None, None

@@ -359,6 +359,80 @@ __global__ __launch_bounds__(512) void temporal_attn_kernel(
   }
 }
 
+
+// Temporal attention backward (training path): one wave per (clip, pixel, head), F <= 32.
+// q/k/v/dO rows are staged in LDS (fp32), then with P = softmax(scale Q K^T) recomputed:
+//   dP = dO V^T,  D_i = sum_j P_ij dP_ij,  dS = P * (dP - D),  dQ = scale dS K,  dK = scale dS^T Q,  dV = P^T dO.
+// Scalar VALU (the F x F x d work per unit is small; the kernel is HBM-bound on q/k/v/dO in, dq/dk/dv out).
+__global__ __launch_bounds__(64) void temporal_attn_bwd_kernel(
+    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V, int ldqkv,
+    const bf16_t* __restrict__ dO, int lddo, bf16_t* __restrict__ dQ, bf16_t* __restrict__ dK,
+    bf16_t* __restrict__ dV, int lddqkv, int nclip, int F, int HW, int heads, int D, float scale) {
+  extern __shared__ float tsm[];
+  float* qs = tsm;                 // [F][D]
+  float* ks = qs + F * D;
+  float* vs = ks + F * D;
+  float* os = vs + F * D;          // dO
+  float* P = os + F * D;           // [F][F]
+  float* dS = P + F * F;           // [F][F]
+  float* Dv = dS + F * F;          // [F]
+  const int lane = threadIdx.x;
+  const int unit = blockIdx.x;
+  const int h = unit % heads, bp = unit / heads;
+  const int b = bp / HW, p = bp - b * HW;
+  auto row = [&](int f) { return (size_t)((b * F + f) * HW + p); };
+  for (int idx = lane; idx < F * D; idx += 64) {
+    const int f = idx / D, d = idx - f * D;
+    const size_t o = row(f) * ldqkv + h * D + d;
+    qs[idx] = bf2f(Q[o]);
+    ks[idx] = bf2f(K[o]);
+    vs[idx] = bf2f(V[o]);
+    os[idx] = bf2f(dO[row(f) * lddo + h * D + d]);
+  }
+  __syncthreads();
+  for (int idx = lane; idx < F * F; idx += 64) {
+    const int i = idx / F, j = idx - i * F;
+    float sq = 0.f, sp = 0.f;
+    for (int d = 0; d < D; ++d) {
+      sq += qs[i * D + d] * ks[j * D + d];
+      sp += os[i * D + d] * vs[j * D + d];
+    }
+    P[idx] = sq * scale;
+    dS[idx] = sp;  // dP for now
+  }
+  __syncthreads();
+  if (lane < F) {
+    const int i = lane;
+    float m = -INFINITY;
+    for (int j = 0; j < F; ++j) m = fmaxf(m, P[i * F + j]);
+    float l = 0.f;
+    for (int j = 0; j < F; ++j) { const float e = __expf(P[i * F + j] - m); P[i * F + j] = e; l += e; }
+    const float inv = 1.0f / l;
+    float di = 0.f;
+    for (int j = 0; j < F; ++j) { P[i * F + j] *= inv; di += P[i * F + j] * dS[i * F + j]; }
+    Dv[i] = di;
+  }
+  __syncthreads();
+  for (int idx = lane; idx < F * F; idx += 64) {
+    const int i = idx / F;
+    dS[idx] = P[idx] * (dS[idx] - Dv[i]);
+  }
+  __syncthreads();
+  for (int idx = lane; idx < F * D; idx += 64) {
+    const int f = idx / D, d = idx - f * D;
+    float gq = 0.f, gk = 0.f, gv = 0.f;
+    for (int j = 0; j < F; ++j) {
+      gq += dS[f * F + j] * ks[j * D + d];   // row f of dS
+      gk += dS[j * F + f] * qs[j * D + d];   // column f of dS
+      gv += P[j * F + f] * os[j * D + d];    // column f of P
+    }
+    const size_t o = row(f) * lddqkv + h * D + d;
+    dQ[o] = f2bf(gq * scale);
+    dK[o] = f2bf(gk * scale);
+    dV[o] = f2bf(gv);
+  }
+}
+
 static inline uint32_t clampb(size_t b) { return b > 0x7fffffffULL ? 0x7fffffffu : (uint32_t)b; }
 
 template <int NT, int D>
@@ -419,4 +493,20 @@ extern "C" int vst_temporal_attention(const void* q, const void* k, const void* 
       return VST_ERR_ARG;
   }
 #undef VST_TA
+}
+
+extern "C" int vst_temporal_attention_bwd(const void* q, const void* k, const void* v, int ldqkv, const void* dout,
+                                          int lddo, void* dq, void* dk, void* dv, int lddqkv, int nclip, int F, int HW,
+                                          int heads, int head_dim, float scale, void* stream) {
+  if (!q || !k || !v || !dout || !dq || !dk || !dv || nclip <= 0 || F <= 0 || F > 32 || HW <= 0 || heads <= 0 ||
+      head_dim <= 0 || head_dim > 256)
+    return VST_ERR_ARG;
+  const size_t units = (size_t)nclip * HW * heads;
+  if (units > 0x7fffffffULL) return VST_ERR_ARG;
+  const size_t lds = (size_t)(4 * F * head_dim + 2 * F * F + F) * sizeof(float);
+  if (lds > 64 * 1024) return VST_ERR_ARG;
+  hipLaunchKernelGGL(temporal_attn_bwd_kernel, dim3((unsigned)units), dim3(64), lds, (hipStream_t)stream,
+                     (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ldqkv, (const bf16_t*)dout, lddo,
+                     (bf16_t*)dq, (bf16_t*)dk, (bf16_t*)dv, lddqkv, nclip, F, HW, heads, head_dim, scale);
+  return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }

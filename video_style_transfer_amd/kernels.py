@@ -418,6 +418,24 @@ def geglu_bwd(p, g, out=None):
     return out
 
 
+def temporal_attention_bwd(q, k, v, dout, nclip, F, HW, heads, head_dim, scale=None, out=None):
+    """(dq, dk, dv) of temporal_attention as column views of one [tokens, 3C] bf16 buffer."""
+    for n, t in (("q", q), ("k", k), ("v", v), ("dout", dout)):
+        _dev(t, BF16, n)
+    if not (q.stride(0) == k.stride(0) == v.stride(0)):
+        raise _lib.VstError("temporal_attention_bwd: q/k/v must share a row stride")
+    C = heads * head_dim
+    rows = nclip * F * HW
+    if out is None:
+        out = torch.empty((rows, 3 * C), dtype=BF16, device=q.device)
+    scale = head_dim ** -0.5 if scale is None else scale
+    with _Rec("temporal_attention_bwd", 0.0, 2.0 * 7 * rows * C):
+        _lib.call("vst_temporal_attention_bwd", _p(q), _p(k), _p(v), q.stride(0), _p(dout), _ld(dout), _p(out[:, :C]),
+                  _p(out[:, C:2 * C]), _p(out[:, 2 * C:]), out.stride(0), nclip, F, HW, heads, head_dim, float(scale),
+                  _stream())
+    return out[:, :C], out[:, C:2 * C], out[:, 2 * C:]
+
+
 def copy2d(x, out):
     _lib.call("vst_copy2d", _p(x), _ld(x), _p(out), _ld(out), x.shape[0], x.shape[1], _stream())
     return out
