@@ -136,6 +136,12 @@ int vst_transpose(const void* x, int ldx, int rows, int cols, void* y, int ldy, 
 size_t vst_layernorm_bwd_workspace_bytes(int C, int rows);
 int vst_layernorm_bwd(const void* x, int ldx, const void* g, int ldg, int C, int rows, const float* gamma, float eps,
                       void* dx, int lddx, float* dgamma, float* dbeta, void* workspace, void* stream);
+/* vst_groupnorm_bwd: dx, dgamma, dbeta of vst_groupnorm (single source, optional fused SiLU; statistics and the
+ * affine recomputed); workspace of vst_groupnorm_bwd_workspace_bytes. */
+size_t vst_groupnorm_bwd_workspace_bytes(int nsamples, int rows_per_sample, int groups, int C);
+int vst_groupnorm_bwd(const void* x, int ldx, const void* g, int ldg, int C, int nsamples, int rows_per_sample,
+                      int groups, float eps, const float* gamma, const float* beta, int silu_act, void* dx, int lddx,
+                      float* dgamma, float* dbeta, void* workspace, void* stream);
 /* vst_temporal_attention_bwd: gradients of vst_temporal_attention (same token layout and q/k/v views) from dO; dq/dk/dv
  * are written with row stride lddqkv (e.g. column views of one [tokens, 3C] buffer).  F <= 32, head_dim <= 256. */
 int vst_temporal_attention_bwd(const void* q, const void* k, const void* v, int ldqkv, const void* dout, int lddo,

@@ -165,3 +165,28 @@ def test_temporal_attention_fn_grads(cuda, nclip, Fr, HW, C):
         e = rel(got, want)
         print(f"[train] temporal attn {nclip}x{Fr}x{HW} C={C} {name}: rel_l2={e:.2e}")
         assert e < 2e-2, (name, e)
+
+
+@pytest.mark.parametrize("ns,rps,C,silu", [(2, 16 * 64, 320, False), (4, 256, 640, True), (1, 4096, 1280, False),
+                                           (3, 77, 64, True)])
+def test_group_norm_fn_grads(cuda, ns, rps, C, silu):
+    from video_style_transfer_amd.autograd import GroupNormFn
+    g = torch.Generator().manual_seed(ns * rps + C)
+    xb = (torch.randn(ns * rps, C, generator=g) + 0.5).to(BF)
+    gam, bet = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g) * 0.1
+    gy = torch.randn(ns * rps, C, generator=g).to(BF)
+    xr, gr, br = xb.float().requires_grad_(True), gam.clone().requires_grad_(True), bet.clone().requires_grad_(True)
+    yr = torch.nn.functional.group_norm(xr.view(ns, rps, C).permute(0, 2, 1), 32, gr, br, 1e-6)
+    yr = yr.permute(0, 2, 1).reshape(ns * rps, C)
+    if silu:
+        yr = torch.nn.functional.silu(yr)
+    yr.backward(gy.float())
+    x = xb.to(cuda).requires_grad_(True)
+    gd, bd = gam.to(cuda).requires_grad_(True), bet.to(cuda).requires_grad_(True)
+    y = GroupNormFn.apply(x, gd, bd, ns, rps, 32, 1e-6, silu)
+    y.backward(gy.to(cuda))
+    for name, got, ref in (("y", y, yr), ("dx", x.grad, xr.grad), ("dgamma", gd.grad, gr.grad),
+                           ("dbeta", bd.grad, br.grad)):
+        e = rel(got, ref)
+        print(f"[train] GN {ns}x{rps}x{C} silu={silu} {name}: rel_l2={e:.2e}")
+        assert e < 2e-2, (name, e)

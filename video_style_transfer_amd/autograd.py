@@ -201,3 +201,26 @@ class TemporalAttentionFn(torch.autograd.Function):
         K.temporal_attention_bwd(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], g.to(BF16).contiguous(), nclip, F, HW,
                                  heads, C // heads, out=dqkv)
         return dqkv, None, None, None, None
+
+
+class GroupNormFn(torch.autograd.Function):
+    """GroupNorm (+SiLU) over `nsamples` groups of `rows_per_sample` token rows (the motion module's clip-wide GN:
+    rows_per_sample = F*H*W; per-frame GN: H*W) with the HIP forward (vst_groupnorm) and backward
+    (vst_groupnorm_bwd)."""
+
+    @staticmethod
+    def forward(ctx, x2d, gamma, beta, nsamples: int, rows_per_sample: int, groups: int, eps: float, silu: bool):
+        x2d = x2d.to(BF16).contiguous()
+        g32, b32 = gamma.detach().float().contiguous(), beta.detach().float().contiguous()
+        y = K.group_norm(x2d, nsamples, rows_per_sample, groups, eps, g32, b32, silu=silu)
+        ctx.save_for_backward(x2d, gamma, beta)
+        ctx.cfg = (nsamples, rows_per_sample, groups, eps, silu)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x2d, gamma, beta = ctx.saved_tensors
+        ns, rps, groups, eps, silu = ctx.cfg
+        dx, dg, db = K.group_norm_bwd(x2d, g.to(BF16).contiguous(), ns, rps, groups, eps,
+                                      gamma.detach().float().contiguous(), beta.detach().float().contiguous(), silu=silu)
+        return dx, dg.to(gamma.dtype), db.to(beta.dtype), None, None, None, None, None

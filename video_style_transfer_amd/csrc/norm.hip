@@ -107,7 +107,8 @@ __global__ __launch_bounds__(64) void gn_finalize_kernel(const float* __restrict
                                                          int rows_per_sample, int groups, int Cg, float eps,
                                                          const float* __restrict__ gamma,
                                                          const float* __restrict__ beta, float* __restrict__ scale,
-                                                         float* __restrict__ shift, int C) {
+                                                         float* __restrict__ shift, int C,
+                                                         float* __restrict__ stats = nullptr) {
   const int s = blockIdx.x / groups, gi = blockIdx.x - s * groups;
   const int lane = threadIdx.x;
   double a = 0.0, q = 0.0;
@@ -130,6 +131,151 @@ __global__ __launch_bounds__(64) void gn_finalize_kernel(const float* __restrict
     scale[(size_t)s * C + c] = sc;
     shift[(size_t)s * C + c] = beta[c] - (float)mean * sc;
   }
+  if (stats != nullptr && lane == 0) {  // backward: (mean, rstd) per (sample, group)
+    stats[(size_t)blockIdx.x * 2] = (float)mean;
+    stats[(size_t)blockIdx.x * 2 + 1] = rstd;
+  }
+}
+
+// ---- GroupNorm backward (training path) ----
+// z = x * scale + shift (the forward's affine, recomputed), dz = g (or g * silu'(z) with the fused SiLU).
+// Pass 1 (gn_bwd_sums): per (sample, chunk) and channel, sum dz and dz * x (same geometry as gn_stats).
+// Pass 2 (gn_bwd_finalize): per (sample, group), A = mean(gamma dz), B = mean(gamma dz x^) ->
+//   dx = a_c dz + b0 + b1 x  with a_c = rstd gamma_c, b0 = rstd^2 mean B - rstd A, b1 = -rstd^2 B,
+//   and the per-(sample, channel) sums for dgamma / dbeta.  Pass 3 (gn_bwd_apply) writes dx; gn_bwd_param sums
+//   dgamma_c = sum_s rstd (S_dzx - mean S_dz), dbeta_c = sum_s S_dz in a fixed order.
+__device__ __forceinline__ float silu_grad(float z) {
+  const float sg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-z * 1.4426950408889634f));
+  return sg * (1.0f + z * (1.0f - sg));
+}
+
+__global__ __launch_bounds__(512) void gn_bwd_sums_kernel(const bf16_t* __restrict__ x, int ldx,
+                                                          const bf16_t* __restrict__ g, int ldg, int C,
+                                                          int rows_per_sample, int rpc, const float* __restrict__ scale,
+                                                          const float* __restrict__ shift, int act,
+                                                          float* __restrict__ part2) {
+  extern __shared__ __attribute__((aligned(16))) float bsm[];  // [rps][C] sum dz, then [rps][C] sum dz*x
+  const int CH = C / 8;
+  const int rps = blockDim.x / CH;
+  const int s = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
+  const int r_beg = chunk * rpc, r_end = min(rows_per_sample, r_beg + rpc);
+  const int tid = threadIdx.x, cch = tid % CH, rph = tid / CH, c = cch * 8;
+  const size_t row0 = (size_t)s * rows_per_sample;
+  float sc[8], sh[8], a[8], q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = scale[(size_t)s * C + c + e];
+    sh[e] = shift[(size_t)s * C + c + e];
+    a[e] = 0.f;
+    q[e] = 0.f;
+  }
+  for (int r = r_beg + rph; r < r_end; r += rps) {
+    float xv[8], gv[8];
+    unpack8(*reinterpret_cast<const u32x4*>(x + (row0 + r) * ldx + c), xv);
+    unpack8(*reinterpret_cast<const u32x4*>(g + (row0 + r) * ldg + c), gv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float dz = act ? gv[e] * silu_grad(xv[e] * sc[e] + sh[e]) : gv[e];
+      a[e] += dz;
+      q[e] += dz * xv[e];
+    }
+  }
+  float* s1 = bsm;
+  float* s2 = bsm + rps * C;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[rph * C + c + e] = a[e]; s2[rph * C + c + e] = q[e]; }
+  __syncthreads();
+  for (int cc = tid; cc < C; cc += blockDim.x) {
+    float u = 0.f, v = 0.f;
+    for (int rr = 0; rr < rps; ++rr) { u += s1[rr * C + cc]; v += s2[rr * C + cc]; }
+    part2[(((size_t)s * nchunk + chunk) * 2) * C + cc] = u;
+    part2[(((size_t)s * nchunk + chunk) * 2 + 1) * C + cc] = v;
+  }
+}
+
+__global__ __launch_bounds__(64) void gn_bwd_finalize_kernel(const float* __restrict__ part2, int nchunk, int C,
+                                                             int groups, int rows_per_sample,
+                                                             const float* __restrict__ stats,
+                                                             const float* __restrict__ gamma,
+                                                             float* __restrict__ chsum, float* __restrict__ coef) {
+  const int s = blockIdx.x / groups, gi = blockIdx.x - s * groups;
+  const int lane = threadIdx.x;
+  const int Cg = C / groups;
+  const float mean = stats[(size_t)blockIdx.x * 2], rstd = stats[(size_t)blockIdx.x * 2 + 1];
+  double A = 0.0, Bq = 0.0;
+  for (int c = gi * Cg + lane; c < (gi + 1) * Cg; c += 64) {
+    double sdz = 0.0, sdzx = 0.0;
+    for (int ch = 0; ch < nchunk; ++ch) {
+      sdz += part2[(((size_t)s * nchunk + ch) * 2) * C + c];
+      sdzx += part2[(((size_t)s * nchunk + ch) * 2 + 1) * C + c];
+    }
+    chsum[((size_t)s * 2) * C + c] = (float)sdz;
+    chsum[((size_t)s * 2 + 1) * C + c] = (float)(rstd * (sdzx - (double)mean * sdz));  // sum dz * x^
+    A += gamma[c] * sdz;
+    Bq += gamma[c] * (sdzx - (double)mean * sdz);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    A += __shfl_xor(A, o);
+    Bq += __shfl_xor(Bq, o);
+  }
+  const double n = (double)rows_per_sample * Cg;
+  const double Am = A / n, Bm = (double)rstd * Bq / n;
+  const float b0 = (float)((double)rstd * rstd * mean * Bm - (double)rstd * Am);
+  const float b1 = (float)(-(double)rstd * rstd * Bm);
+  for (int c = gi * Cg + lane; c < (gi + 1) * Cg; c += 64) {
+    coef[((size_t)s * C + c) * 3] = rstd * gamma[c];
+    coef[((size_t)s * C + c) * 3 + 1] = b0;
+    coef[((size_t)s * C + c) * 3 + 2] = b1;
+  }
+}
+
+__global__ __launch_bounds__(512) void gn_bwd_apply_kernel(const bf16_t* __restrict__ x, int ldx,
+                                                           const bf16_t* __restrict__ g, int ldg, int C,
+                                                           int rows_per_sample, int rpc,
+                                                           const float* __restrict__ scale,
+                                                           const float* __restrict__ shift, int act,
+                                                           const float* __restrict__ coef, bf16_t* __restrict__ dx,
+                                                           int lddx) {
+  const int CH = C / 8;
+  const int rps = blockDim.x / CH;
+  const int s = blockIdx.y;
+  const int r_beg = blockIdx.x * rpc, r_end = min(rows_per_sample, r_beg + rpc);
+  const int tid = threadIdx.x, cch = tid % CH, rph = tid / CH, c = cch * 8;
+  const size_t row0 = (size_t)s * rows_per_sample;
+  float sc[8], sh[8], ca[8], c0[8], c1[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = scale[(size_t)s * C + c + e];
+    sh[e] = shift[(size_t)s * C + c + e];
+    ca[e] = coef[((size_t)s * C + c + e) * 3];
+    c0[e] = coef[((size_t)s * C + c + e) * 3 + 1];
+    c1[e] = coef[((size_t)s * C + c + e) * 3 + 2];
+  }
+  for (int r = r_beg + rph; r < r_end; r += rps) {
+    float xv[8], gv[8], o[8];
+    unpack8(*reinterpret_cast<const u32x4*>(x + (row0 + r) * ldx + c), xv);
+    unpack8(*reinterpret_cast<const u32x4*>(g + (row0 + r) * ldg + c), gv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float dz = act ? gv[e] * silu_grad(xv[e] * sc[e] + sh[e]) : gv[e];
+      o[e] = ca[e] * dz + c0[e] + c1[e] * xv[e];
+    }
+    *reinterpret_cast<u32x4*>(dx + (row0 + r) * lddx + c) = pack8(o);
+  }
+}
+
+__global__ __launch_bounds__(256) void gn_bwd_param_kernel(const float* __restrict__ chsum, int nsamples, int C,
+                                                           float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float db = 0.f, dg = 0.f;
+  for (int s = 0; s < nsamples; ++s) {
+    db += chsum[((size_t)s * 2) * C + c];
+    dg += chsum[((size_t)s * 2 + 1) * C + c];
+  }
+  dgamma[c] = dg;
+  dbeta[c] = db;
 }
 
 __global__ __launch_bounds__(512) void gn_apply_kernel(const bf16_t* __restrict__ x1, int ld1, int C1,
@@ -723,5 +869,53 @@ extern "C" int vst_layernorm_bwd(const void* x, int ldx, const void* g, int ldg,
 #undef VST_LNB
   hipLaunchKernelGGL(layernorm_bwd_reduce_kernel, dim3((2 * C + 255) / 256), dim3(256), 0, s, part, grid, C, dgamma,
                      dbeta);
+  return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+}
+
+// ---- GroupNorm backward host side ----
+static inline size_t gnb_floats(int nsamples, int rows_per_sample, int groups, int C) {
+  const size_t nchunk = gn_nchunk(nsamples, rows_per_sample);
+  const size_t a4 = 4;
+  auto up = [&](size_t n) { return (n + a4 - 1) / a4 * a4; };
+  return up(gn_part_floats(nsamples, rows_per_sample, groups)) + up((size_t)2 * nsamples * C)  // part, scale/shift
+         + up((size_t)2 * nsamples * groups) + up((size_t)nsamples * nchunk * 2 * C)           // stats, part2
+         + up((size_t)2 * nsamples * C) + up((size_t)3 * nsamples * C);                        // chsum, coef
+}
+
+extern "C" size_t vst_groupnorm_bwd_workspace_bytes(int nsamples, int rows_per_sample, int groups, int C) {
+  return gnb_floats(nsamples, rows_per_sample, groups, C) * sizeof(float);
+}
+
+extern "C" int vst_groupnorm_bwd(const void* x, int ldx, const void* g, int ldg, int C, int nsamples,
+                                 int rows_per_sample, int groups, float eps, const float* gamma, const float* beta,
+                                 int silu_act, void* dx, int lddx, float* dgamma, float* dbeta, void* workspace,
+                                 void* stream) {
+  if (!x || !g || !dx || !gamma || !beta || !dgamma || !dbeta || !workspace || nsamples <= 0 ||
+      rows_per_sample <= 0 || groups <= 0 || C % groups || C % 8 || C > 4096 || (ldx & 7) || (ldg & 7) || (lddx & 7))
+    return VST_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int rpc = gn_rpc(nsamples, rows_per_sample);
+  const int nchunk = gn_nchunk(nsamples, rows_per_sample);
+  const int CH = C / 8, rps = gn_rps(C);
+  auto up = [](size_t n) { return (n + 3) / 4 * 4; };
+  float* part = (float*)workspace;
+  float* scale = part + up(gn_part_floats(nsamples, rows_per_sample, groups));
+  float* shift = scale + nsamples * (size_t)C;
+  float* stats = scale + up((size_t)2 * nsamples * C);
+  float* part2 = stats + up((size_t)2 * nsamples * groups);
+  float* chsum = part2 + up((size_t)nsamples * nchunk * 2 * C);
+  float* coef = chsum + up((size_t)2 * nsamples * C);
+  const size_t lds = (size_t)2 * rps * C * sizeof(float);
+  hipLaunchKernelGGL(gn_stats_kernel, dim3(nchunk, nsamples), dim3(rps * CH), lds, s, (const bf16_t*)x, ldx, C,
+                     (const bf16_t*)nullptr, 0, 0, rows_per_sample, rpc, groups, part);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(nsamples * groups), dim3(64), 0, s, part, nchunk, rows_per_sample,
+                     groups, C / groups, eps, gamma, beta, scale, shift, C, stats);
+  hipLaunchKernelGGL(gn_bwd_sums_kernel, dim3(nchunk, nsamples), dim3(rps * CH), lds, s, (const bf16_t*)x, ldx,
+                     (const bf16_t*)g, ldg, C, rows_per_sample, rpc, scale, shift, silu_act, part2);
+  hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(nsamples * groups), dim3(64), 0, s, part2, nchunk, C, groups,
+                     rows_per_sample, stats, gamma, chsum, coef);
+  hipLaunchKernelGGL(gn_bwd_apply_kernel, dim3(nchunk, nsamples), dim3(rps * CH), 0, s, (const bf16_t*)x, ldx,
+                     (const bf16_t*)g, ldg, C, rows_per_sample, rpc, scale, shift, silu_act, coef, (bf16_t*)dx, lddx);
+  hipLaunchKernelGGL(gn_bwd_param_kernel, dim3((C + 255) / 256), dim3(256), 0, s, chsum, nsamples, C, dgamma, dbeta);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }

@@ -404,6 +404,24 @@ def layer_norm_bwd(x, g, gamma, eps=1e-5):
     return dx, dgamma, dbeta
 
 
+def group_norm_bwd(x, g, nsamples, rows_per_sample, groups, eps, gamma, beta, *, silu=False):
+    """GroupNorm (+SiLU) backward: (dx bf16, dgamma fp32 [C], dbeta fp32 [C])."""
+    _dev(x, BF16, "x")
+    _dev(g, BF16, "g")
+    rows, C = x.shape
+    if rows != nsamples * rows_per_sample or g.shape != x.shape:
+        raise _lib.VstError("group_norm_bwd: shapes")
+    dx = torch.empty((rows, C), dtype=BF16, device=x.device)
+    dgamma = torch.empty(C, dtype=F32, device=x.device)
+    dbeta = torch.empty(C, dtype=F32, device=x.device)
+    ws = torch.empty((_lib.load().vst_groupnorm_bwd_workspace_bytes(nsamples, rows_per_sample, groups, C) + 3) // 4,
+                     dtype=F32, device=x.device)
+    with _Rec("groupnorm_bwd", 0.0, 2.0 * 5 * rows * C):
+        _lib.call("vst_groupnorm_bwd", _p(x), _ld(x), _p(g), _ld(g), C, nsamples, rows_per_sample, groups, float(eps),
+                  _p(gamma), _p(beta), int(silu), _p(dx), _ld(dx), _p(dgamma), _p(dbeta), _p(ws), _stream())
+    return dx, dgamma, dbeta
+
+
 def geglu_bwd(p, g, out=None):
     """dp (32-interleaved like p) from p = the GEGLU projection output and g = dL/d(h * gelu(gate))."""
     _dev(p, BF16, "p")
