@@ -190,3 +190,76 @@ def test_group_norm_fn_grads(cuda, ns, rps, C, silu):
         e = rel(got, ref)
         print(f"[train] GN {ns}x{rps}x{C} silu={silu} {name}: rel_l2={e:.2e}")
         assert e < 2e-2, (name, e)
+
+
+def test_motion_module_forward_backward_vs_oracle(cuda):
+    """A whole motion module (diffusers AnimateDiffTransformer3D) with temporal LoRA on its attention
+    projections (temporal_lora.py:10-69), trained the way train_animatediff.py does (base projection weights frozen,
+    LoRA / FF / proj / norms trainable): forward and backward on the HIP Functions vs torch.autograd through the fp32
+    oracle (oracle/unet.py motion_module) on the same bf16-rounded weights."""
+    from oracle.unet import motion_module
+    from video_style_transfer_amd.autograd import motion_module_train
+    from video_style_transfer_amd.temporal_lora import TemporalLoRALinear
+    from video_style_transfer_amd.unet_motion import MotionModule
+    torch.manual_seed(3)
+    C, nclip, Fr, H, W = 128, 2, 8, 4, 4
+    HW = H * W
+    mm = MotionModule(C, heads=8)
+    with torch.no_grad():
+        for n, p in mm.named_parameters():
+            if n.endswith("weight") and p.dim() == 2:
+                p.copy_(torch.randn_like(p) * p.shape[1] ** -0.5)
+            elif n.endswith("bias"):
+                p.copy_(torch.randn_like(p) * 0.05)
+            else:  # norms
+                p.copy_(1.0 + 0.1 * torch.randn_like(p))
+    blk = mm.transformer_blocks[0]
+    for attn in (blk.attn1, blk.attn2):
+        attn.to_q, attn.to_k, attn.to_v = (TemporalLoRALinear(l, rank=8, alpha=1.0) for l in (attn.to_q, attn.to_k,
+                                                                                              attn.to_v))
+        attn.to_out[0] = TemporalLoRALinear(attn.to_out[0], rank=8, alpha=1.0)
+        with torch.no_grad():
+            for l in (attn.to_q, attn.to_k, attn.to_v, attn.to_out[0]):
+                l.lora_A.normal_(0, 0.1)
+                l.lora_B.normal_(0, 0.1)
+    mm = mm.to(cuda)
+    for n, p in mm.named_parameters():  # bf16 linear weights (incl. frozen bases), fp32 norms / LoRA factors
+        if p.dim() == 2 and "lora_" not in n:
+            p.data = p.data.to(torch.bfloat16)
+    # oracle parameters: the same values in fp32, temporal LoRA as W + s B A (autograd-tracked)
+    leaves = {n: p.detach().float().cpu().clone().requires_grad_(p.requires_grad) for n, p in mm.named_parameters()}
+    P = {}
+    for n, t in leaves.items():
+        if ".base." in n:
+            stem = n.replace(".base", "")
+            P[stem] = t
+        elif "lora_" not in n:
+            P[n] = t
+    for attn in ("attn1", "attn2"):
+        for proj in ("to_q", "to_k", "to_v", "to_out.0"):
+            pre = f"transformer_blocks.0.{attn}.{proj}"
+            P[pre + ".weight"] = leaves[pre + ".base.weight"] + (1.0 / 8) * leaves[pre + ".lora_B"] @ leaves[pre + ".lora_A"]
+    P["transformer_blocks.0.pos_embed.pe"] = mm.transformer_blocks[0].pos_embed.pe.float().cpu()
+    P = {("mm." + k): v for k, v in P.items()}
+
+    x_img = (torch.randn(nclip * Fr, C, H, W)).to(torch.bfloat16).float()
+    gy_img = torch.randn(nclip * Fr, C, H, W).to(torch.bfloat16).float()
+    xr = x_img.clone().requires_grad_(True)
+    yr = motion_module(P, "mm", xr, Fr, heads=8)
+    yr.backward(gy_img)
+
+    tok = lambda t: t.permute(0, 2, 3, 1).reshape(-1, C)  # noqa: E731
+    x = tok(x_img).to(cuda, torch.bfloat16).requires_grad_(True)
+    y = motion_module_train(mm, x, nclip, Fr, HW)
+    y.backward(tok(gy_img).to(cuda, torch.bfloat16))
+    named = dict(mm.named_parameters())
+    checks = [("y", y, tok(yr.detach())), ("dx", x.grad, tok(xr.grad))]
+    for n in ("norm.weight", "proj_in.weight", "proj_out.bias", "transformer_blocks.0.norm1.weight",
+              "transformer_blocks.0.attn1.to_q.lora_A", "transformer_blocks.0.attn2.to_out.0.lora_B",
+              "transformer_blocks.0.ff.net.0.proj.weight", "transformer_blocks.0.ff.net.2.weight"):
+        checks.append((n, named[n].grad, leaves[n].grad))
+    assert named["transformer_blocks.0.attn1.to_q.base.weight"].grad is None  # frozen base
+    for name, got, ref in checks:
+        e = rel(got, ref)
+        print(f"[train] motion module {name}: rel_l2={e:.2e}")
+        assert e < 3e-2, (name, e)

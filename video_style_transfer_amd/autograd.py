@@ -112,10 +112,12 @@ class LayerNormFn(torch.autograd.Function):
     HIP forward (vst_layernorm) and backward (vst_layernorm_bwd: dx, dgamma, dbeta; statistics recomputed)."""
 
     @staticmethod
-    def forward(ctx, x2d, gamma, beta, eps: float):
+    def forward(ctx, x2d, gamma, beta, eps: float, pe=None, pe_div: int = 1, pe_mod: int = 1):
+        """pe: optional [max_len, C] fp32 table added after the affine, row r gets pe[(r // pe_div) % pe_mod]
+        (motion-module norm1/norm2 + sinusoidal PE); a constant, so the backward is unchanged."""
         x2d = x2d.to(BF16).contiguous()
         g32 = gamma.detach().float().contiguous()
-        y = K.layer_norm(x2d, g32, beta.detach().float().contiguous(), eps)
+        y = K.layer_norm(x2d, g32, beta.detach().float().contiguous(), eps, pe=pe, pe_div=pe_div, pe_mod=pe_mod)
         ctx.save_for_backward(x2d, gamma)
         ctx.eps = eps
         ctx.beta_dtype = beta.dtype
@@ -125,7 +127,7 @@ class LayerNormFn(torch.autograd.Function):
     def backward(ctx, g):
         x2d, gamma = ctx.saved_tensors
         dx, dgam, dbet = K.layer_norm_bwd(x2d, g.to(BF16).contiguous(), gamma.detach().float().contiguous(), ctx.eps)
-        return dx, dgam.to(gamma.dtype), dbet.to(ctx.beta_dtype), None
+        return dx, dgam.to(gamma.dtype), dbet.to(ctx.beta_dtype), None, None, None, None
 
 
 def _interleave32(t: torch.Tensor) -> torch.Tensor:
@@ -224,3 +226,66 @@ class GroupNormFn(torch.autograd.Function):
         dx, dg, db = K.group_norm_bwd(x2d, g.to(BF16).contiguous(), ns, rps, groups, eps,
                                       gamma.detach().float().contiguous(), beta.detach().float().contiguous(), silu=silu)
         return dx, dg.to(gamma.dtype), db.to(beta.dtype), None, None, None, None, None
+
+
+
+class AddFn(torch.autograd.Function):
+    """Residual add on the HIP path (vst_add); the gradient passes to both operands."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        return K.add(a.contiguous(), b.contiguous())
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, g
+
+
+def _proj_parts(lins):
+    """(W [sum out, in], b or None, A [sum r, in], B [sum out, sum r] with the LoRA scales folded in) of projections
+    sharing one input, as autograd-tracked concatenations of the modules' own parameters."""
+    from .temporal_lora import TemporalLoRALinear
+    Ws, bs, As, Bs = [], [], [], []
+    for lin in lins:
+        base = lin.base if isinstance(lin, TemporalLoRALinear) else lin
+        Ws.append(base.weight)
+        bs.append(base.bias)
+        if isinstance(lin, TemporalLoRALinear):
+            As.append(lin.lora_A)
+            Bs.append(lin.lora_B * lin.scale)
+        else:
+            As.append(base.weight.new_zeros(0, base.in_features, dtype=torch.float32))
+            Bs.append(base.weight.new_zeros(base.out_features, 0, dtype=torch.float32))
+    W = Ws[0] if len(Ws) == 1 else torch.cat(Ws, 0)
+    b = None
+    if any(x is not None for x in bs):
+        b = torch.cat([x.float() if x is not None else torch.zeros(w.shape[0], device=w.device) for w, x in zip(Ws, bs)])
+    A = torch.cat([a.float() for a in As], 0)
+    B = torch.block_diag(*[bb.float() for bb in Bs])
+    return W, b, A, B
+
+
+def proj_train(lins, x2d):
+    W, b, A, B = _proj_parts(lins)
+    return LoRALinearFn.apply(x2d, W, b, A, B, 1.0)
+
+
+def motion_module_train(mm, x2d, nclip: int, F: int, HW: int):
+    """Forward of a motion module (unet_motion.MotionModule = diffusers AnimateDiffTransformer3D) built from the
+    autograd Functions above, so loss.backward() runs the whole module backward on HIP kernels: GroupNorm over the
+    clip, proj_in, [LN+PE -> fused q/k/v (+temporal LoRA) -> frame-axis attention -> to_out (+LoRA) -> +res] x2,
+    LN -> GEGLU -> ff.2 -> +res, proj_out -> +x.  Tokens [(b*F + f)*HW + p, C] bf16."""
+    C = x2d.shape[1]
+    h = GroupNormFn.apply(x2d, mm.norm.weight, mm.norm.bias, nclip, F * HW, mm.norm.num_groups, mm.norm.eps, False)
+    h = proj_train([mm.proj_in], h)
+    for blk in mm.transformer_blocks:
+        pe = blk.pos_embed.pe.detach().float().reshape(-1, C).contiguous()
+        for norm, attn in ((blk.norm1, blk.attn1), (blk.norm2, blk.attn2)):
+            n = LayerNormFn.apply(h, norm.weight, norm.bias, norm.eps, pe, HW, F)
+            qkv = proj_train([attn.to_q, attn.to_k, attn.to_v], n)
+            o = TemporalAttentionFn.apply(qkv, nclip, F, HW, attn.heads)
+            h = AddFn.apply(h, proj_train([attn.to_out[0]], o))
+        n = LayerNormFn.apply(h, blk.norm3.weight, blk.norm3.bias, blk.norm3.eps)
+        f = GEGLUFn.apply(n, blk.ff.net[0].proj.weight, blk.ff.net[0].proj.bias)
+        h = AddFn.apply(h, proj_train([blk.ff.net[2]], f))
+    return AddFn.apply(x2d, proj_train([mm.proj_out], h))
