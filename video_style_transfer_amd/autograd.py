@@ -289,3 +289,60 @@ def motion_module_train(mm, x2d, nclip: int, F: int, HW: int):
         f = GEGLUFn.apply(n, blk.ff.net[0].proj.weight, blk.ff.net[0].proj.bias)
         h = AddFn.apply(h, proj_train([blk.ff.net[2]], f))
     return AddFn.apply(x2d, proj_train([mm.proj_out], h))
+
+
+def _conv_dgrad_weight(conv):
+    """Kernel-layout weight of the stride-1 3x3 conv's data gradient: W'[ci, co, ky, kx] = W[co, ci, 2-ky, 2-kx]
+    (flipped taps, swapped channels), laid out [ci, (ky, kx, co)] like Conv3x3.kernel_weight; cached per version."""
+    W = conv.weight
+    key = (W.data_ptr(), W._version)
+    c = conv.__dict__.get("_vst_wdgrad")
+    if c is None or c[0] != key:
+        wf = W.detach().flip(2, 3).transpose(0, 1)                      # [ci, co, 3, 3]
+        ci, co = wf.shape[:2]
+        w = wf.permute(0, 2, 3, 1).reshape(ci, 9 * co)
+        kp = (9 * co + 7) & ~7
+        if kp != 9 * co:
+            w = torch.cat([w, w.new_zeros(ci, kp - 9 * co)], 1)
+        c = (key, w.to(BF16).contiguous())
+        conv.__dict__["_vst_wdgrad"] = c
+    return c[1]
+
+
+class Conv3x3Fn(torch.autograd.Function):
+    """Frozen stride-1 3x3 conv (ResnetBlock2D conv1/conv2 of the spatial path, frozen in train_animatediff.py):
+    forward = the implicit-GEMM conv (+ per-frame temb row bias, a constant here); backward dX = the same conv kernel
+    applied to dY with flipped, channel-swapped weights (pad 1, stride 1)."""
+
+    @staticmethod
+    def forward(ctx, x2d, conv, nimg: int, H: int, W: int, row_bias=None, row_bias_div: int = 1):
+        if conv.stride[0] != 1 or conv.weight.requires_grad:
+            raise NotImplementedError("Conv3x3Fn: stride-1 frozen convs only (dgrad); dW is not on the training path")
+        x2d = x2d.to(BF16).contiguous()
+        y = conv.run(x2d, nimg, H, W, row_bias=row_bias, row_bias_div=row_bias_div)
+        ctx.conv, ctx.dims = conv, (nimg, H, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        nimg, H, W = ctx.dims
+        dx = K.conv3x3(g.to(BF16).contiguous(), nimg, H, W, _conv_dgrad_weight(ctx.conv), None)
+        return dx, None, None, None, None, None, None
+
+
+def resnet_train(rb, x2d, nimg: int, H: int, W: int, temb_rows=None, rows_per_bias: int = 1):
+    """ResnetBlock2D (frozen spatial path) forward on autograd Functions, so the gradient w.r.t. its input flows back
+    on HIP kernels: GN+SiLU -> conv1 (+temb row bias) -> GN+SiLU -> conv2 -> + shortcut.
+    temb_rows: fp32 [n, Cout] time-embedding projection rows (row r of the output adds temb_rows[r // rows_per_bias])."""
+    HW = H * W
+    h = GroupNormFn.apply(x2d, rb.norm1.weight, rb.norm1.bias, nimg, HW, rb.norm1.num_groups, rb.norm1.eps, True)
+    h = Conv3x3Fn.apply(h, rb.conv1, nimg, H, W, temb_rows, rows_per_bias)
+    h = GroupNormFn.apply(h, rb.norm2.weight, rb.norm2.bias, nimg, HW, rb.norm2.num_groups, rb.norm2.eps, True)
+    h = Conv3x3Fn.apply(h, rb.conv2, nimg, H, W)
+    if rb.conv_shortcut is not None:
+        sc = rb.conv_shortcut
+        Wsc = sc.weight.reshape(sc.weight.shape[0], -1)
+        A0 = Wsc.new_zeros(0, Wsc.shape[1], dtype=torch.float32)
+        B0 = Wsc.new_zeros(Wsc.shape[0], 0, dtype=torch.float32)
+        x2d = LoRALinearFn.apply(x2d, Wsc, sc.bias, A0, B0, 1.0)
+    return AddFn.apply(x2d, h)
