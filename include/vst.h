@@ -142,6 +142,15 @@ size_t vst_groupnorm_bwd_workspace_bytes(int nsamples, int rows_per_sample, int 
 int vst_groupnorm_bwd(const void* x, int ldx, const void* g, int ldg, int C, int nsamples, int rows_per_sample,
                       int groups, float eps, const float* gamma, const float* beta, int silu_act, void* dx, int lddx,
                       float* dgamma, float* dbeta, void* workspace, void* stream);
+/* vst_spatial_attention_bwd: gradients of vst_spatial_attention (head_dim 64; K/V shared by kv_div consecutive
+ * batches, as for the per-clip text states) from dO and the forward output o: dq (lddq), dk/dv (lddkv, one row per
+ * kv token: the gradient of text K/V summed over the frames sharing it).  Workspace:
+ * vst_spatial_attention_bwd_workspace_bytes (per-query logsumexp and dO.O). */
+size_t vst_spatial_attention_bwd_workspace_bytes(int nbatch, int heads, int Nq);
+int vst_spatial_attention_bwd(const void* q, int ldq, const void* k, const void* v, int ldkv, const void* o, int ldo,
+                              const void* dout, int lddo, void* dq, int lddq, void* dk, void* dv, int lddkv, int nbatch,
+                              int heads, int Nq, int Nk, int kv_div, int head_dim, float scale, void* workspace,
+                              void* stream);
 /* vst_temporal_attention_bwd: gradients of vst_temporal_attention (same token layout and q/k/v views) from dO; dq/dk/dv
  * are written with row stride lddqkv (e.g. column views of one [tokens, 3C] buffer).  F <= 32, head_dim <= 256. */
 int vst_temporal_attention_bwd(const void* q, const void* k, const void* v, int ldqkv, const void* dout, int lddo,

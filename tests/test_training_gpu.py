@@ -306,3 +306,30 @@ def test_resnet_block_backward_vs_oracle(cuda, cin, cout, H):
         e = rel(got, ref)
         print(f"[train] resnet {cin}->{cout} {H}x{H} {name}: rel_l2={e:.2e}")
         assert e < 2e-2, (name, e)
+
+
+@pytest.mark.parametrize("nb,heads,Nq,Nk,kv_div", [(2, 2, 256, 256, 1), (4, 3, 100, 77, 2), (1, 1, 64, 130, 1)])
+def test_spatial_attention_fn_grads(cuda, nb, heads, Nq, Nk, kv_div):
+    from video_style_transfer_amd.autograd import SpatialAttentionFn
+    g = torch.Generator().manual_seed(nb * Nq + Nk)
+    C = heads * 64
+    nkv = nb // kv_div
+    q = torch.randn(nb * Nq, C, generator=g).to(BF)
+    k = torch.randn(nkv * Nk, C, generator=g).to(BF)
+    v = torch.randn(nkv * Nk, C, generator=g).to(BF)
+    gy = torch.randn(nb * Nq, C, generator=g).to(BF)
+    qr, kr, vr = (t.float().requires_grad_(True) for t in (q, k, v))
+    qh = qr.view(nb, Nq, heads, 64).transpose(1, 2)
+    kh = kr.view(nkv, Nk, heads, 64).transpose(1, 2).repeat_interleave(kv_div, 0)
+    vh = vr.view(nkv, Nk, heads, 64).transpose(1, 2).repeat_interleave(kv_div, 0)
+    o = torch.softmax(qh @ kh.transpose(-1, -2) * 0.125, -1) @ vh
+    ref = o.transpose(1, 2).reshape(nb * Nq, C)
+    ref.backward(gy.float())
+    qd, kd, vd = (t.to(cuda).requires_grad_(True) for t in (q, k, v))
+    out = SpatialAttentionFn.apply(qd, kd, vd, nb, heads, Nq, Nk, kv_div)
+    out.backward(gy.to(cuda))
+    for name, got, want in (("o", out, ref), ("dq", qd.grad, qr.grad), ("dk", kd.grad, kr.grad),
+                            ("dv", vd.grad, vr.grad)):
+        e = rel(got, want)
+        print(f"[train] spatial attn nb={nb} h={heads} {Nq}x{Nk} kv_div={kv_div} {name}: rel_l2={e:.2e}")
+        assert e < 2e-2, (name, e)

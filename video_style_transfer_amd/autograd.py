@@ -346,3 +346,25 @@ def resnet_train(rb, x2d, nimg: int, H: int, W: int, temb_rows=None, rows_per_bi
         B0 = Wsc.new_zeros(Wsc.shape[0], 0, dtype=torch.float32)
         x2d = LoRALinearFn.apply(x2d, Wsc, sc.bias, A0, B0, 1.0)
     return AddFn.apply(x2d, h)
+
+
+class SpatialAttentionFn(torch.autograd.Function):
+    """SDPA core of AnimateDiffAttnProcessor2_0 (animatediff/attention_processor.py:78-80), head_dim 64: forward =
+    vst_spatial_attention (MFMA), backward = vst_spatial_attention_bwd.  q: [nbatch*Nq, C]; k, v: [nkv*Nk, C] with
+    nkv = nbatch / kv_div (text K/V shared by the frames of a clip: their gradient sums over those frames)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, nbatch: int, heads: int, Nq: int, Nk: int, kv_div: int):
+        q, k, v = (t.to(BF16).contiguous() for t in (q, k, v))
+        o = K.spatial_attention(q, k, v, nbatch, heads, Nq, Nk, kv_div, scale=0.125)
+        ctx.save_for_backward(q, k, v, o)
+        ctx.dims = (nbatch, heads, Nq, Nk, kv_div)
+        return o
+
+    @staticmethod
+    def backward(ctx, g):
+        q, k, v, o = ctx.saved_tensors
+        nbatch, heads, Nq, Nk, kv_div = ctx.dims
+        dq, dk, dv = K.spatial_attention_bwd(q, k, v, o, g.to(BF16).contiguous(), nbatch, heads, Nq, Nk, kv_div,
+                                             scale=0.125)
+        return dq, dk, dv, None, None, None, None, None

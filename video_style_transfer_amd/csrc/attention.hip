@@ -433,6 +433,205 @@ __global__ __launch_bounds__(64) void temporal_attn_bwd_kernel(
   }
 }
 
+
+// ---------------------------------------------------------------------------------
+// Spatial attention backward (training path), head_dim 64, two passes (correctness-first,
+// scalar fp32 FMAs on LDS tiles; the forward is the MFMA kernel above):
+//  sa_bwd_dq_kernel  (per batch*head, 64-query block): lse_i by an online pass over the keys, D_i = dO_i . O_i, then
+//                    P = exp(scale S - lse), dP = dO V^T, dS = P (dP - D), dQ = scale dS K; writes lse and D.
+//  sa_bwd_dkv_kernel (per kv batch*head, 64-key block): over every query that attends to these keys (all frames
+//                    sharing the text K/V when kv_div > 1): dV += P^T dO, dK += scale dS^T Q.
+// Thread t of 256 owns tile row (t >> 2) and 16 columns ((t & 3) * 16 ..); row reductions use xor-1/2 shuffles.
+constexpr int SB_T = 64;
+
+__device__ __forceinline__ void sb_load_tile(float* dst, const bf16_t* src, int ld, int row0, int nrows, int col0) {
+  // dst[64][64] <- src[(row0 + r) * ld + col0 + c], zero beyond nrows
+  for (int idx = threadIdx.x; idx < SB_T * 8; idx += 256) {
+    const int r = idx >> 3, c8 = (idx & 7) * 8;
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (row0 + r < nrows) unpack8(*reinterpret_cast<const u32x4*>(src + (size_t)(row0 + r) * ld + col0 + c8), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dst[r * SB_T + c8 + e] = v[e];
+  }
+}
+
+__global__ __launch_bounds__(256) void sa_bwd_dq_kernel(const bf16_t* __restrict__ Q, int ldq,
+                                                        const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
+                                                        int ldkv, const bf16_t* __restrict__ O, int ldo,
+                                                        const bf16_t* __restrict__ dO, int lddo,
+                                                        bf16_t* __restrict__ dQ, int lddq, int heads, int Nq, int Nk,
+                                                        int kv_div, float scale, float* __restrict__ lse_out,
+                                                        float* __restrict__ d_out) {
+  extern __shared__ float sbm[];
+  float* qs = sbm;
+  float* os = qs + SB_T * SB_T;  // dO
+  float* ks = os + SB_T * SB_T;
+  float* vs = ks + SB_T * SB_T;
+  const int nqb = (Nq + SB_T - 1) / SB_T;
+  const int qb = blockIdx.x % nqb, bh = blockIdx.x / nqb;
+  const int h = bh % heads, b = bh / heads, bkv = b / kv_div;
+  const int t = threadIdx.x, r = t >> 2, c0 = (t & 3) * 16;
+  const int q0 = qb * SB_T;
+  sb_load_tile(qs, Q + (size_t)b * Nq * ldq, ldq, q0, Nq, h * 64);
+  sb_load_tile(os, dO + (size_t)b * Nq * lddo, lddo, q0, Nq, h * 64);
+  __syncthreads();  // other threads' rows of the dO tile are read below
+  // D_r = dO_r . O_r
+  float dr = 0.f;
+  if (q0 + r < Nq) {
+    const bf16_t* orow = O + ((size_t)b * Nq + q0 + r) * ldo + h * 64 + c0;
+    for (int d = 0; d < 16; ++d) dr += os[r * SB_T + c0 + d] * bf2f(orow[d]);
+  }
+  dr += __shfl_xor(dr, 1);
+  dr += __shfl_xor(dr, 2);
+  const int nkt = (Nk + SB_T - 1) / SB_T;
+  const bf16_t* Kb = K + (size_t)bkv * Nk * ldkv;
+  const bf16_t* Vb = V + (size_t)bkv * Nk * ldkv;
+  // pass 1: lse
+  float m = -INFINITY, l = 0.f;
+  for (int kt = 0; kt < nkt; ++kt) {
+    __syncthreads();
+    sb_load_tile(ks, Kb, ldkv, kt * SB_T, Nk, h * 64);
+    __syncthreads();
+    float sv[16];
+    float tm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      float a = 0.f;
+      for (int d = 0; d < 64; ++d) a += qs[r * SB_T + d] * ks[(c0 + j) * SB_T + d];
+      sv[j] = kt * SB_T + c0 + j < Nk ? a * scale : -INFINITY;
+      tm = fmaxf(tm, sv[j]);
+    }
+    tm = fmaxf(tm, __shfl_xor(tm, 1));
+    tm = fmaxf(tm, __shfl_xor(tm, 2));
+    const float mn = fmaxf(m, tm);
+    float ts = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) ts += __expf(sv[j] - mn);
+    ts += __shfl_xor(ts, 1);
+    ts += __shfl_xor(ts, 2);
+    l = l * __expf(m - mn) + ts;
+    m = mn;
+  }
+  const float lse = m + __logf(l);
+  // pass 2: dQ
+  float acc[64];
+#pragma unroll
+  for (int d = 0; d < 64; ++d) acc[d] = 0.f;
+  for (int kt = 0; kt < nkt; ++kt) {
+    __syncthreads();
+    sb_load_tile(ks, Kb, ldkv, kt * SB_T, Nk, h * 64);
+    sb_load_tile(vs, Vb, ldkv, kt * SB_T, Nk, h * 64);
+    __syncthreads();
+#pragma unroll 2
+    for (int j = 0; j < 16; ++j) {
+      const int c = c0 + j;
+      if (kt * SB_T + c >= Nk) continue;
+      float sq = 0.f, dp = 0.f;
+      for (int d = 0; d < 64; ++d) {
+        sq += qs[r * SB_T + d] * ks[c * SB_T + d];
+        dp += os[r * SB_T + d] * vs[c * SB_T + d];
+      }
+      const float p = __expf(sq * scale - lse);
+      const float ds = p * (dp - dr);
+#pragma unroll
+      for (int d = 0; d < 64; ++d) acc[d] += ds * ks[c * SB_T + d];
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < 64; ++d) {
+    acc[d] += __shfl_xor(acc[d], 1);
+    acc[d] += __shfl_xor(acc[d], 2);
+  }
+  if (q0 + r < Nq) {
+    bf16_t* out = dQ + ((size_t)b * Nq + q0 + r) * lddq + h * 64 + c0;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq)  // compile-time register indices (a runtime acc[c0 + d] would go to scratch)
+      if ((t & 3) == qq) {
+#pragma unroll
+        for (int d = 0; d < 16; ++d) out[d] = f2bf(acc[qq * 16 + d] * scale);
+      }
+    if ((t & 3) == 0) {
+      lse_out[(size_t)bh * Nq + q0 + r] = lse;
+      d_out[(size_t)bh * Nq + q0 + r] = dr;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void sa_bwd_dkv_kernel(const bf16_t* __restrict__ Q, int ldq,
+                                                         const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
+                                                         int ldkv, const bf16_t* __restrict__ dO, int lddo,
+                                                         bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int lddkv,
+                                                         int heads, int Nq, int Nk, int kv_div, float scale,
+                                                         const float* __restrict__ lse_in,
+                                                         const float* __restrict__ d_in) {
+  extern __shared__ float sbm[];
+  float* ks = sbm;
+  float* vs = ks + SB_T * SB_T;
+  float* qs = vs + SB_T * SB_T;
+  float* os = qs + SB_T * SB_T;
+  const int nkb = (Nk + SB_T - 1) / SB_T;
+  const int kb = blockIdx.x % nkb, bh = blockIdx.x / nkb;
+  const int h = bh % heads, bkv = bh / heads;
+  const int t = threadIdx.x, c = t >> 2, i0 = (t & 3) * 16;  // this thread: key row c, queries i0..i0+15 of a tile
+  const int k0 = kb * SB_T;
+  sb_load_tile(ks, K + (size_t)bkv * Nk * ldkv, ldkv, k0, Nk, h * 64);
+  sb_load_tile(vs, V + (size_t)bkv * Nk * ldkv, ldkv, k0, Nk, h * 64);
+  float gk[64], gv[64];
+#pragma unroll
+  for (int d = 0; d < 64; ++d) { gk[d] = 0.f; gv[d] = 0.f; }
+  const int nqt = (Nq + SB_T - 1) / SB_T;
+  for (int bb = 0; bb < kv_div; ++bb) {
+    const int b = bkv * kv_div + bb;
+    const int bhq = b * heads + h;
+    for (int qt = 0; qt < nqt; ++qt) {
+      __syncthreads();
+      sb_load_tile(qs, Q + (size_t)b * Nq * ldq, ldq, qt * SB_T, Nq, h * 64);
+      sb_load_tile(os, dO + (size_t)b * Nq * lddo, lddo, qt * SB_T, Nq, h * 64);
+      __syncthreads();
+      if (k0 + c >= Nk) continue;
+#pragma unroll 2
+      for (int j = 0; j < 16; ++j) {
+        const int i = qt * SB_T + i0 + j;
+        if (i >= Nq) continue;
+        const int il = i0 + j;
+        float sq = 0.f, dp = 0.f;
+        for (int d = 0; d < 64; ++d) {
+          sq += qs[il * SB_T + d] * ks[c * SB_T + d];
+          dp += os[il * SB_T + d] * vs[c * SB_T + d];
+        }
+        const float p = __expf(sq * scale - lse_in[(size_t)bhq * Nq + i]);
+        const float ds = p * (dp - d_in[(size_t)bhq * Nq + i]);
+#pragma unroll
+        for (int d = 0; d < 64; ++d) {
+          gv[d] += p * os[il * SB_T + d];
+          gk[d] += ds * qs[il * SB_T + d];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < 64; ++d) {
+    gk[d] += __shfl_xor(gk[d], 1);
+    gk[d] += __shfl_xor(gk[d], 2);
+    gv[d] += __shfl_xor(gv[d], 1);
+    gv[d] += __shfl_xor(gv[d], 2);
+  }
+  if (k0 + c < Nk) {
+    const int dd = (t & 3) * 16;
+    bf16_t* okr = dK + ((size_t)bkv * Nk + k0 + c) * lddkv + h * 64 + dd;
+    bf16_t* ovr = dV + ((size_t)bkv * Nk + k0 + c) * lddkv + h * 64 + dd;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq)
+      if ((t & 3) == qq) {
+#pragma unroll
+        for (int d = 0; d < 16; ++d) {
+          okr[d] = f2bf(gk[qq * 16 + d] * scale);
+          ovr[d] = f2bf(gv[qq * 16 + d]);
+        }
+      }
+  }
+}
+
 static inline uint32_t clampb(size_t b) { return b > 0x7fffffffULL ? 0x7fffffffu : (uint32_t)b; }
 
 template <int NT, int D>
@@ -508,5 +707,31 @@ extern "C" int vst_temporal_attention_bwd(const void* q, const void* k, const vo
   hipLaunchKernelGGL(temporal_attn_bwd_kernel, dim3((unsigned)units), dim3(64), lds, (hipStream_t)stream,
                      (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ldqkv, (const bf16_t*)dout, lddo,
                      (bf16_t*)dq, (bf16_t*)dk, (bf16_t*)dv, lddqkv, nclip, F, HW, heads, head_dim, scale);
+  return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+}
+
+extern "C" size_t vst_spatial_attention_bwd_workspace_bytes(int nbatch, int heads, int Nq) {
+  return (size_t)2 * nbatch * heads * Nq * sizeof(float);
+}
+
+extern "C" int vst_spatial_attention_bwd(const void* q, int ldq, const void* k, const void* v, int ldkv, const void* o,
+                                         int ldo, const void* dout, int lddo, void* dq, int lddq, void* dk, void* dv,
+                                         int lddkv, int nbatch, int heads, int Nq, int Nk, int kv_div, int head_dim,
+                                         float scale, void* workspace, void* stream) {
+  if (head_dim != 64 || !q || !k || !v || !o || !dout || !dq || !dk || !dv || !workspace || nbatch <= 0 ||
+      heads <= 0 || Nq <= 0 || Nk <= 0 || kv_div <= 0 || nbatch % kv_div)
+    return VST_ERR_ARG;
+  if ((ldq & 7) || (ldkv & 7) || (ldo & 7) || (lddo & 7)) return VST_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  float* lse = (float*)workspace;
+  float* dvec = lse + (size_t)nbatch * heads * Nq;
+  const size_t lds = 4 * SB_T * SB_T * sizeof(float);
+  const int nqb = (Nq + SB_T - 1) / SB_T, nkb = (Nk + SB_T - 1) / SB_T;
+  hipLaunchKernelGGL(sa_bwd_dq_kernel, dim3(nqb * heads * nbatch), dim3(256), lds, s, (const bf16_t*)q, ldq,
+                     (const bf16_t*)k, (const bf16_t*)v, ldkv, (const bf16_t*)o, ldo, (const bf16_t*)dout, lddo,
+                     (bf16_t*)dq, lddq, heads, Nq, Nk, kv_div, scale, lse, dvec);
+  hipLaunchKernelGGL(sa_bwd_dkv_kernel, dim3(nkb * heads * (nbatch / kv_div)), dim3(256), lds, s, (const bf16_t*)q,
+                     ldq, (const bf16_t*)k, (const bf16_t*)v, ldkv, (const bf16_t*)dout, lddo, (bf16_t*)dk,
+                     (bf16_t*)dv, lddkv, heads, Nq, Nk, kv_div, scale, lse, dvec);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }

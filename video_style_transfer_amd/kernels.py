@@ -436,6 +436,28 @@ def geglu_bwd(p, g, out=None):
     return out
 
 
+def spatial_attention_bwd(q, k, v, o, dout, nbatch, heads, Nq, Nk, kv_div=1, scale=None, dq=None, dkv=None):
+    """(dq [nbatch*Nq, heads*64], dk, dv [nbatch/kv_div*Nk, heads*64] as column views of one [.., 2*heads*64])."""
+    for n, t in (("q", q), ("k", k), ("v", v), ("o", o), ("dout", dout)):
+        _dev(t, BF16, n)
+    if k.stride(0) != v.stride(0):
+        raise _lib.VstError("spatial_attention_bwd: k and v must share a row stride")
+    C = heads * 64
+    nkv = nbatch // kv_div
+    if dq is None:
+        dq = torch.empty((nbatch * Nq, C), dtype=BF16, device=q.device)
+    if dkv is None:
+        dkv = torch.empty((nkv * Nk, 2 * C), dtype=BF16, device=q.device)
+    ws = torch.empty((_lib.load().vst_spatial_attention_bwd_workspace_bytes(nbatch, heads, Nq) + 3) // 4,
+                     dtype=F32, device=q.device)
+    scale = 0.125 if scale is None else scale
+    with _Rec("spatial_attention_bwd", 10.0 * nbatch * heads * Nq * Nk * 64, 0.0):
+        _lib.call("vst_spatial_attention_bwd", _p(q), _ld(q), _p(k), _p(v), k.stride(0), _p(o), _ld(o), _p(dout),
+                  _ld(dout), _p(dq), _ld(dq), _p(dkv[:, :C]), _p(dkv[:, C:]), dkv.stride(0), nbatch, heads, Nq, Nk,
+                  kv_div, 64, float(scale), _p(ws), _stream())
+    return dq, dkv[:, :C], dkv[:, C:]
+
+
 def temporal_attention_bwd(q, k, v, dout, nclip, F, HW, heads, head_dim, scale=None, out=None):
     """(dq, dk, dv) of temporal_attention as column views of one [tokens, 3C] bf16 buffer."""
     for n, t in (("q", q), ("k", k), ("v", v), ("dout", dout)):
