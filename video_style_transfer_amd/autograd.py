@@ -241,18 +241,24 @@ class AddFn(torch.autograd.Function):
         return g, g
 
 
-def _proj_parts(lins):
+def _proj_parts(lins, scale: float = 1.0):
     """(W [sum out, in], b or None, A [sum r, in], B [sum out, sum r] with the LoRA scales folded in) of projections
-    sharing one input, as autograd-tracked concatenations of the modules' own parameters."""
+    sharing one input, as autograd-tracked concatenations of the modules' own parameters.  Frozen UnZipLoRA layers
+    (Stage 2 keeps the spatial LoRA frozen) contribute their low-rank factors (lowrank_factors(scale)) as constants."""
     from .temporal_lora import TemporalLoRALinear
     Ws, bs, As, Bs = [], [], [], []
     for lin in lins:
         base = lin.base if isinstance(lin, TemporalLoRALinear) else lin
         Ws.append(base.weight)
         bs.append(base.bias)
+        lora = getattr(lin, "lora_layer", None)
         if isinstance(lin, TemporalLoRALinear):
             As.append(lin.lora_A)
             Bs.append(lin.lora_B * lin.scale)
+        elif lora is not None:
+            A, V = lora.lowrank_factors(scale)
+            As.append(A.detach().float())
+            Bs.append(V.detach().float())
         else:
             As.append(base.weight.new_zeros(0, base.in_features, dtype=torch.float32))
             Bs.append(base.weight.new_zeros(base.out_features, 0, dtype=torch.float32))
@@ -265,9 +271,40 @@ def _proj_parts(lins):
     return W, b, A, B
 
 
-def proj_train(lins, x2d):
-    W, b, A, B = _proj_parts(lins)
+def proj_train(lins, x2d, scale: float = 1.0):
+    W, b, A, B = _proj_parts(lins, scale)
     return LoRALinearFn.apply(x2d, W, b, A, B, 1.0)
+
+
+def transformer2d_train(t2d, x2d, nimg: int, H: int, W: int, enc=None, frames_per_text: int = 1, scale: float = 1.0):
+    """Transformer2DModel of the frozen spatial path (unziplora_unet/transformer_2d.py:137-352; BasicTransformerBlock
+    unzip_attention.py:113-239 with the UnZipLoRA delta on every q/k/v/out) on autograd Functions, so dL/dx flows
+    back on HIP kernels: per-frame GroupNorm, proj_in, [LN -> fused q/k/v (+LoRA) -> self-attention -> to_out
+    (+LoRA) + res; LN -> q (+LoRA) x text K/V -> cross-attention -> to_out + res; LN -> GEGLU -> ff.2 + res],
+    proj_out + x.  enc: [nimg / frames_per_text * L, D] bf16 text states (constants: no gradient is taken)."""
+    HW = H * W
+    C = x2d.shape[1]
+    h = GroupNormFn.apply(x2d, t2d.norm.weight, t2d.norm.bias, nimg, HW, t2d.norm.num_groups, t2d.norm.eps, False)
+    h = proj_train([t2d.proj_in], h)
+    for blk in t2d.transformer_blocks:
+        a1, a2 = blk.attn1, blk.attn2
+        n = LayerNormFn.apply(h, blk.norm1.weight, blk.norm1.bias, blk.norm1.eps)
+        qkv = proj_train([a1.to_q, a1.to_k, a1.to_v], n, scale)
+        inner = qkv.shape[1] // 3
+        o = SpatialAttentionFn.apply(qkv[:, :inner], qkv[:, inner:2 * inner], qkv[:, 2 * inner:], nimg, a1.heads, HW,
+                                     HW, 1)
+        h = AddFn.apply(h, proj_train([a1.to_out[0]], o, scale))
+        n = LayerNormFn.apply(h, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps)
+        q = proj_train([a2.to_q], n, scale)
+        with torch.no_grad():
+            L = enc.shape[0] // (nimg // frames_per_text)
+            kv = proj_train([a2.to_k, a2.to_v], enc, scale)
+        o = SpatialAttentionFn.apply(q, kv[:, :inner], kv[:, inner:], nimg, a2.heads, HW, L, frames_per_text)
+        h = AddFn.apply(h, proj_train([a2.to_out[0]], o, scale))
+        n = LayerNormFn.apply(h, blk.norm3.weight, blk.norm3.bias, blk.norm3.eps)
+        f = GEGLUFn.apply(n, blk.ff.net[0].proj.weight, blk.ff.net[0].proj.bias)
+        h = AddFn.apply(h, proj_train([blk.ff.net[2]], f))
+    return AddFn.apply(x2d, proj_train([t2d.proj_out], h))
 
 
 def motion_module_train(mm, x2d, nclip: int, F: int, HW: int):
