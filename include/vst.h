@@ -151,6 +151,11 @@ int vst_spatial_attention_bwd(const void* q, int ldq, const void* k, const void*
                               const void* dout, int lddo, void* dq, int lddq, void* dk, void* dv, int lddkv, int nbatch,
                               int heads, int Nq, int Nk, int kv_div, int head_dim, float scale, void* workspace,
                               void* stream);
+/* Sampler data gradients (NHWC tokens, C % 8 == 0): vst_zero_insert writes x [nimg, h, w, C] onto the even
+ * positions of a caller-zeroed [nimg, 2h, 2w, C] (Downsample2D stride-2 conv dgrad); vst_sumpool2x2 sums 2x2 blocks
+ * of x [nimg, 2h, 2w, C] into y [nimg, h, w, C] (adjoint of Upsample2D's nearest-2x). */
+int vst_zero_insert(const void* x, int nimg, int h, int w, int C, void* y, void* stream);
+int vst_sumpool2x2(const void* x, int nimg, int h, int w, int C, void* y, void* stream);
 /* vst_temporal_attention_bwd: gradients of vst_temporal_attention (same token layout and q/k/v views) from dO; dq/dk/dv
  * are written with row stride lddqkv (e.g. column views of one [tokens, 3C] buffer).  F <= 32, head_dim <= 256. */
 int vst_temporal_attention_bwd(const void* q, const void* k, const void* v, int ldqkv, const void* dout, int lddo,

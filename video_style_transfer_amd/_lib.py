@@ -54,6 +54,8 @@ SIGNATURES = {
     "vst_spatial_attention_bwd_workspace_bytes": (_S, [_I, _I, _I]),
     "vst_spatial_attention_bwd": (_I, [_P, _I, _P, _P, _I, _P, _I, _P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _I,
                                        _F, _P, _P]),
+    "vst_zero_insert": (_I, [_P, _I, _I, _I, _I, _P, _P]),
+    "vst_sumpool2x2": (_I, [_P, _I, _I, _I, _I, _P, _P]),
     "vst_temporal_attention_bwd": (_I, [_P, _P, _P, _I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P]),
     "vst_probe_mfma": (_I, [_I, _I, _P, _P]),
     "vst_probe_hbm_read": (_I, [_P, _S, _I, _P, _P]),

@@ -347,24 +347,50 @@ def _conv_dgrad_weight(conv):
 
 
 class Conv3x3Fn(torch.autograd.Function):
-    """Frozen stride-1 3x3 conv (ResnetBlock2D conv1/conv2 of the spatial path, frozen in train_animatediff.py):
-    forward = the implicit-GEMM conv (+ per-frame temb row bias, a constant here); backward dX = the same conv kernel
-    applied to dY with flipped, channel-swapped weights (pad 1, stride 1)."""
+    """Frozen 3x3 conv of the spatial path (frozen in train_animatediff.py): forward = the implicit-GEMM conv
+    (+ per-frame temb row bias, a constant here); backward dX = the same conv kernel on dY with flipped,
+    channel-swapped weights — stride 1 directly; stride 2 (Downsample2D) on the zero-inserted dY; the
+    nearest-2x-upsampled conv (Upsample2D) at the upsampled size followed by the 2x2 sum-pool adjoint."""
 
     @staticmethod
-    def forward(ctx, x2d, conv, nimg: int, H: int, W: int, row_bias=None, row_bias_div: int = 1):
-        if conv.stride[0] != 1 or conv.weight.requires_grad:
-            raise NotImplementedError("Conv3x3Fn: stride-1 frozen convs only (dgrad); dW is not on the training path")
+    def forward(ctx, x2d, conv, nimg: int, H: int, W: int, row_bias=None, row_bias_div: int = 1,
+                upsample: bool = False):
+        if conv.weight.requires_grad:
+            raise NotImplementedError("Conv3x3Fn: frozen convs only (dgrad); dW is not on the training path")
+        stride = conv.stride[0]
+        if stride == 2 and (H % 2 or W % 2):
+            raise NotImplementedError("Conv3x3Fn: stride-2 dgrad assumes even spatial sizes")
         x2d = x2d.to(BF16).contiguous()
-        y = conv.run(x2d, nimg, H, W, row_bias=row_bias, row_bias_div=row_bias_div)
-        ctx.conv, ctx.dims = conv, (nimg, H, W)
+        y = conv.run(x2d, nimg, H, W, upsample=upsample, row_bias=row_bias, row_bias_div=row_bias_div)
+        ctx.conv, ctx.dims, ctx.mode = conv, (nimg, H, W), ("up" if upsample else stride)
         return y
 
     @staticmethod
     def backward(ctx, g):
         nimg, H, W = ctx.dims
-        dx = K.conv3x3(g.to(BF16).contiguous(), nimg, H, W, _conv_dgrad_weight(ctx.conv), None)
-        return dx, None, None, None, None, None, None
+        wd = _conv_dgrad_weight(ctx.conv)
+        g = g.to(BF16).contiguous()
+        if ctx.mode == 2:
+            dx = K.conv3x3(K.zero_insert(g, nimg, H // 2, W // 2), nimg, H, W, wd, None)
+        elif ctx.mode == "up":
+            dx = K.sumpool2x2(K.conv3x3(g, nimg, 2 * H, 2 * W, wd, None), nimg, H, W)
+        else:
+            dx = K.conv3x3(g, nimg, H, W, wd, None)
+        return dx, None, None, None, None, None, None, None
+
+
+class CatFn(torch.autograd.Function):
+    """Up-block skip concat [x | skip] on channels (the inference path reads the two sources in place; the training
+    path materialises it once for the GroupNorm / conv / shortcut backward)."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.ca = a.shape[1]
+        return torch.cat([a.to(BF16), b.to(BF16)], 1)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g[:, :ctx.ca].contiguous(), g[:, ctx.ca:].contiguous()
 
 
 def resnet_train(rb, x2d, nimg: int, H: int, W: int, temb_rows=None, rows_per_bias: int = 1):
@@ -405,3 +431,52 @@ class SpatialAttentionFn(torch.autograd.Function):
         dq, dk, dv = K.spatial_attention_bwd(q, k, v, o, g.to(BF16).contiguous(), nbatch, heads, Nq, Nk, kv_div,
                                              scale=0.125)
         return dq, dk, dv, None, None, None, None, None
+
+
+
+def unet_train_tokens(unet, x, B: int, F: int, h: int, w: int, emb_silu, enc2d, scale: float = 1.0):
+    """UNetMotionModel.forward_tokens (unet_motion.py) on the autograd Functions: the training forward of
+    train_animatediff.py:265-273 whose loss.backward() runs on HIP kernels end to end — frozen spatial path (convs,
+    ResnetBlock2D, Transformer2DModel with UnZipLoRA) dX only, motion modules with their trainable parameters.
+    x: [B*F*h*w, in] bf16 tokens of the noisy latents; emb_silu: SiLU(time + add embedding) [B, T] (constant);
+    enc2d: [B*L, D] text states (constant)."""
+    temb = unet.batched_temb(emb_silu)
+    nimg = B * F
+    H, W = h, w
+
+    def res_block(res, t):
+        return resnet_train(res, t, nimg, H, W, temb[res], F * H * W)
+
+    x = Conv3x3Fn.apply(x, unet.conv_in, nimg, H, W)
+    skips = [(x, H, W)]
+    for blk in unet.down_blocks:
+        for j, res in enumerate(blk.resnets):
+            x = res_block(res, x)
+            if blk.attentions is not None:
+                x = transformer2d_train(blk.attentions[j], x, nimg, H, W, enc2d, F, scale)
+            x = motion_module_train(blk.motion_modules[j], x, B, F, H * W)
+            skips.append((x, H, W))
+        if blk.downsamplers is not None:
+            x = Conv3x3Fn.apply(x, blk.downsamplers[0].conv, nimg, H, W)
+            H, W = H // 2, W // 2
+            skips.append((x, H, W))
+    mid = unet.mid_block
+    x = res_block(mid.resnets[0], x)
+    x = transformer2d_train(mid.attentions[0], x, nimg, H, W, enc2d, F, scale)
+    if mid.motion_modules is not None:
+        x = motion_module_train(mid.motion_modules[0], x, B, F, H * W)
+    x = res_block(mid.resnets[1], x)
+    for blk in unet.up_blocks:
+        for j, res in enumerate(blk.resnets):
+            sk, sh, sw = skips.pop()
+            assert (sh, sw) == (H, W)
+            x = res_block(res, CatFn.apply(x, sk))
+            if blk.attentions is not None:
+                x = transformer2d_train(blk.attentions[j], x, nimg, H, W, enc2d, F, scale)
+            x = motion_module_train(blk.motion_modules[j], x, B, F, H * W)
+        if blk.upsamplers is not None:
+            x = Conv3x3Fn.apply(x, blk.upsamplers[0].conv, nimg, H, W, None, 1, True)
+            H, W = 2 * H, 2 * W
+    n = unet.conv_norm_out
+    x = GroupNormFn.apply(x, n.weight, n.bias, nimg, H * W, n.num_groups, n.eps, True)
+    return Conv3x3Fn.apply(x, unet.conv_out, nimg, H, W)

@@ -242,6 +242,47 @@ __global__ __launch_bounds__(256) void geglu_bwd_kernel(const bf16_t* __restrict
   }
 }
 
+// Conv data-gradient helpers for the down/up samplers (training path):
+//  zero_insert: y[n, 2i, 2j, :] = x[n, i, j, :] on a zeroed [n, 2h, 2w, C] grid (stride-2 conv dgrad = stride-1
+//               conv of the zero-inserted dY with flipped weights);
+//  sumpool2x2:  y[n, i, j, :] = sum of x[n, 2i..2i+1, 2j..2j+1, :] (the adjoint of the nearest-2x upsample).
+__global__ __launch_bounds__(256) void zero_insert_kernel(const bf16_t* __restrict__ x, int nimg, int h, int w, int C,
+                                                          bf16_t* __restrict__ y) {
+  const int CH = C / 8;
+  const size_t total = (size_t)nimg * h * w * CH;
+  for (size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (size_t)gridDim.x * 256) {
+    const int c = (int)(idx % CH) * 8;
+    const size_t pix = idx / CH;
+    const int j = (int)(pix % w), i = (int)((pix / w) % h);
+    const size_t n = pix / ((size_t)w * h);
+    *reinterpret_cast<u32x4*>(y + ((n * 2 * h + 2 * i) * 2 * w + 2 * j) * C + c) =
+        *reinterpret_cast<const u32x4*>(x + pix * C + c);
+  }
+}
+
+__global__ __launch_bounds__(256) void sumpool2x2_kernel(const bf16_t* __restrict__ x, int nimg, int h, int w, int C,
+                                                         bf16_t* __restrict__ y) {
+  const int CH = C / 8;
+  const size_t total = (size_t)nimg * h * w * CH;  // output pixels x chunks (h, w: OUTPUT size)
+  for (size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (size_t)gridDim.x * 256) {
+    const int c = (int)(idx % CH) * 8;
+    const size_t pix = idx / CH;
+    const int j = (int)(pix % w), i = (int)((pix / w) % h);
+    const size_t n = pix / ((size_t)w * h);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 2; ++dx) {
+        float v[8];
+        unpack8(*reinterpret_cast<const u32x4*>(x + ((n * 2 * h + 2 * i + dy) * 2 * w + 2 * j + dx) * C + c), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += v[e];
+      }
+    *reinterpret_cast<u32x4*>(y + pix * C + c) = pack8(acc);
+  }
+}
+
 __global__ void step_advance_kernel(int* step) {
   if (threadIdx.x == 0 && blockIdx.x == 0) *step += 1;
 }
@@ -363,6 +404,24 @@ extern "C" int vst_geglu_bwd(const void* p, int ldp, const void* g, int ldg, int
   const int grid = (int)std::min<size_t>((total + 255) / 256, 16384);
   hipLaunchKernelGGL(geglu_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)p, ldp,
                      (const bf16_t*)g, ldg, M, Nh, (bf16_t*)dp, lddp);
+  return ok();
+}
+
+extern "C" int vst_zero_insert(const void* x, int nimg, int h, int w, int C, void* y, void* stream) {
+  if (!x || !y || nimg <= 0 || h <= 0 || w <= 0 || C <= 0 || C % 8) return VST_ERR_ARG;
+  const size_t total = (size_t)nimg * h * w * (C / 8);
+  const int grid = (int)std::min<size_t>((total + 255) / 256, 16384);
+  hipLaunchKernelGGL(zero_insert_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, nimg, h, w,
+                     C, (bf16_t*)y);
+  return ok();
+}
+
+extern "C" int vst_sumpool2x2(const void* x, int nimg, int h, int w, int C, void* y, void* stream) {
+  if (!x || !y || nimg <= 0 || h <= 0 || w <= 0 || C <= 0 || C % 8) return VST_ERR_ARG;
+  const size_t total = (size_t)nimg * h * w * (C / 8);
+  const int grid = (int)std::min<size_t>((total + 255) / 256, 16384);
+  hipLaunchKernelGGL(sumpool2x2_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, nimg, h, w,
+                     C, (bf16_t*)y);
   return ok();
 }
 

@@ -476,6 +476,24 @@ def temporal_attention_bwd(q, k, v, dout, nclip, F, HW, heads, head_dim, scale=N
     return out[:, :C], out[:, C:2 * C], out[:, 2 * C:]
 
 
+def zero_insert(x, nimg, h, w):
+    """[nimg*h*w, C] -> [nimg*2h*2w, C] with x on the even (2i, 2j) pixels, zeros elsewhere."""
+    _dev(x, BF16, "x")
+    C = x.shape[1]
+    out = torch.zeros((nimg * 4 * h * w, C), dtype=BF16, device=x.device)
+    _lib.call("vst_zero_insert", _p(x), nimg, h, w, C, _p(out), _stream())
+    return out
+
+
+def sumpool2x2(x, nimg, h, w):
+    """[nimg*2h*2w, C] -> [nimg*h*w, C], 2x2 block sums (h, w: output size)."""
+    _dev(x, BF16, "x")
+    C = x.shape[1]
+    out = torch.empty((nimg * h * w, C), dtype=BF16, device=x.device)
+    _lib.call("vst_sumpool2x2", _p(x), nimg, h, w, C, _p(out), _stream())
+    return out
+
+
 def copy2d(x, out):
     _lib.call("vst_copy2d", _p(x), _ld(x), _p(out), _ld(out), x.shape[0], x.shape[1], _stream())
     return out
