@@ -146,7 +146,7 @@ int vst_groupnorm_bwd(const void* x, int ldx, const void* g, int ldg, int C, int
  * batches, as for the per-clip text states) from dO and the forward output o: dq (lddq), dk/dv (lddkv, one row per
  * kv token: the gradient of text K/V summed over the frames sharing it).  Workspace:
  * vst_spatial_attention_bwd_workspace_bytes (per-query logsumexp and dO.O). */
-size_t vst_spatial_attention_bwd_workspace_bytes(int nbatch, int heads, int Nq);
+size_t vst_spatial_attention_bwd_workspace_bytes(int nbatch, int heads, int Nq, int Nk);
 int vst_spatial_attention_bwd(const void* q, int ldq, const void* k, const void* v, int ldkv, const void* o, int ldo,
                               const void* dout, int lddo, void* dq, int lddq, void* dk, void* dv, int lddkv, int nbatch,
                               int heads, int Nq, int Nk, int kv_div, int head_dim, float scale, void* workspace,

@@ -51,7 +51,7 @@ SIGNATURES = {
     "vst_geglu_bwd": (_I, [_P, _I, _P, _I, _I, _I, _P, _I, _P]),
     "vst_groupnorm_bwd_workspace_bytes": (_S, [_I, _I, _I, _I]),
     "vst_groupnorm_bwd": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _F, _P, _P, _I, _P, _I, _P, _P, _P, _P]),
-    "vst_spatial_attention_bwd_workspace_bytes": (_S, [_I, _I, _I]),
+    "vst_spatial_attention_bwd_workspace_bytes": (_S, [_I, _I, _I, _I]),
     "vst_spatial_attention_bwd": (_I, [_P, _I, _P, _P, _I, _P, _I, _P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _I,
                                        _F, _P, _P]),
     "vst_zero_insert": (_I, [_P, _I, _I, _I, _I, _P, _P]),

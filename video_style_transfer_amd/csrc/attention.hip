@@ -563,7 +563,10 @@ __global__ __launch_bounds__(256) void sa_bwd_dkv_kernel(const bf16_t* __restric
                                                          bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int lddkv,
                                                          int heads, int Nq, int Nk, int kv_div, float scale,
                                                          const float* __restrict__ lse_in,
-                                                         const float* __restrict__ d_in) {
+                                                         const float* __restrict__ d_in, float* __restrict__ part) {
+  // part == nullptr: one workgroup per (kv batch, head, key block) loops over the kv_div query batches sharing it.
+  // part != nullptr (shared text K/V, kv_div > 1): one workgroup per (query batch, head, key block) writes its fp32
+  // contribution to part[b][key][2C] and sa_bwd_kv_reduce_kernel sums the kv_div batches (kv_div x more workgroups).
   extern __shared__ float sbm[];
   float* ks = sbm;
   float* vs = ks + SB_T * SB_T;
@@ -571,7 +574,10 @@ __global__ __launch_bounds__(256) void sa_bwd_dkv_kernel(const bf16_t* __restric
   float* os = qs + SB_T * SB_T;
   const int nkb = (Nk + SB_T - 1) / SB_T;
   const int kb = blockIdx.x % nkb, bh = blockIdx.x / nkb;
-  const int h = bh % heads, bkv = bh / heads;
+  const int h = bh % heads;
+  const int bq0 = part ? bh / heads : (bh / heads) * kv_div;  // first query batch handled here
+  const int nbq = part ? 1 : kv_div;
+  const int bkv = bq0 / kv_div;
   const int t = threadIdx.x, c = t >> 2, i0 = (t & 3) * 16;  // this thread: key row c, queries i0..i0+15 of a tile
   const int k0 = kb * SB_T;
   sb_load_tile(ks, K + (size_t)bkv * Nk * ldkv, ldkv, k0, Nk, h * 64);
@@ -580,8 +586,8 @@ __global__ __launch_bounds__(256) void sa_bwd_dkv_kernel(const bf16_t* __restric
 #pragma unroll
   for (int d = 0; d < 64; ++d) { gk[d] = 0.f; gv[d] = 0.f; }
   const int nqt = (Nq + SB_T - 1) / SB_T;
-  for (int bb = 0; bb < kv_div; ++bb) {
-    const int b = bkv * kv_div + bb;
+  for (int bb = 0; bb < nbq; ++bb) {
+    const int b = bq0 + bb;
     const int bhq = b * heads + h;
     for (int qt = 0; qt < nqt; ++qt) {
       __syncthreads();
@@ -616,7 +622,20 @@ __global__ __launch_bounds__(256) void sa_bwd_dkv_kernel(const bf16_t* __restric
     gv[d] += __shfl_xor(gv[d], 1);
     gv[d] += __shfl_xor(gv[d], 2);
   }
-  if (k0 + c < Nk) {
+  if (k0 + c < Nk && part) {
+    const int dd = (t & 3) * 16;
+    const int C = heads * 64;
+    float* pr = part + ((size_t)bq0 * Nk + k0 + c) * 2 * C + h * 64 + dd;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq)
+      if ((t & 3) == qq) {
+#pragma unroll
+        for (int d = 0; d < 16; ++d) {
+          pr[d] = gk[qq * 16 + d] * scale;
+          pr[C + d] = gv[qq * 16 + d];
+        }
+      }
+  } else if (k0 + c < Nk) {
     const int dd = (t & 3) * 16;
     bf16_t* okr = dK + ((size_t)bkv * Nk + k0 + c) * lddkv + h * 64 + dd;
     bf16_t* ovr = dV + ((size_t)bkv * Nk + k0 + c) * lddkv + h * 64 + dd;
@@ -629,6 +648,21 @@ __global__ __launch_bounds__(256) void sa_bwd_dkv_kernel(const bf16_t* __restric
           ovr[d] = f2bf(gv[qq * 16 + d]);
         }
       }
+  }
+}
+
+__global__ __launch_bounds__(256) void sa_bwd_kv_reduce_kernel(const float* __restrict__ part, int nkv, int kv_div,
+                                                               int Nk, int C, bf16_t* __restrict__ dK,
+                                                               bf16_t* __restrict__ dV, int lddkv) {
+  const size_t total = (size_t)nkv * Nk * 2 * C;
+  for (size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (size_t)gridDim.x * 256) {
+    const int col = (int)(idx % (2 * C));
+    const size_t row = idx / (2 * C);  // kv batch * Nk + key
+    const size_t bkv = row / Nk, key = row - bkv * Nk;
+    float a = 0.f;
+    for (int j = 0; j < kv_div; ++j) a += part[(((bkv * kv_div + j) * Nk) + key) * 2 * C + col];
+    bf16_t* dst = col < C ? dK + row * lddkv + col : dV + row * lddkv + (col - C);
+    *dst = f2bf(a);
   }
 }
 
@@ -710,8 +744,9 @@ extern "C" int vst_temporal_attention_bwd(const void* q, const void* k, const vo
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 
-extern "C" size_t vst_spatial_attention_bwd_workspace_bytes(int nbatch, int heads, int Nq) {
-  return (size_t)2 * nbatch * heads * Nq * sizeof(float);
+// lse + D per query, then (shared text K/V) the per-query-batch fp32 dK/dV partials
+extern "C" size_t vst_spatial_attention_bwd_workspace_bytes(int nbatch, int heads, int Nq, int Nk) {
+  return ((size_t)2 * nbatch * heads * Nq + (size_t)nbatch * Nk * 2 * heads * 64) * sizeof(float);
 }
 
 extern "C" int vst_spatial_attention_bwd(const void* q, int ldq, const void* k, const void* v, int ldkv, const void* o,
@@ -730,8 +765,18 @@ extern "C" int vst_spatial_attention_bwd(const void* q, int ldq, const void* k, 
   hipLaunchKernelGGL(sa_bwd_dq_kernel, dim3(nqb * heads * nbatch), dim3(256), lds, s, (const bf16_t*)q, ldq,
                      (const bf16_t*)k, (const bf16_t*)v, ldkv, (const bf16_t*)o, ldo, (const bf16_t*)dout, lddo,
                      (bf16_t*)dq, lddq, heads, Nq, Nk, kv_div, scale, lse, dvec);
-  hipLaunchKernelGGL(sa_bwd_dkv_kernel, dim3(nkb * heads * (nbatch / kv_div)), dim3(256), lds, s, (const bf16_t*)q,
-                     ldq, (const bf16_t*)k, (const bf16_t*)v, ldkv, (const bf16_t*)dout, lddo, (bf16_t*)dk,
-                     (bf16_t*)dv, lddkv, heads, Nq, Nk, kv_div, scale, lse, dvec);
+  if (kv_div > 1) {
+    float* part = dvec + (size_t)nbatch * heads * Nq;
+    hipLaunchKernelGGL(sa_bwd_dkv_kernel, dim3(nkb * heads * nbatch), dim3(256), lds, s, (const bf16_t*)q, ldq,
+                       (const bf16_t*)k, (const bf16_t*)v, ldkv, (const bf16_t*)dout, lddo, (bf16_t*)dk, (bf16_t*)dv,
+                       lddkv, heads, Nq, Nk, kv_div, scale, lse, dvec, part);
+    const size_t tot = (size_t)(nbatch / kv_div) * Nk * 2 * heads * 64;
+    hipLaunchKernelGGL(sa_bwd_kv_reduce_kernel, dim3((unsigned)std::min<size_t>((tot + 255) / 256, 16384)), dim3(256),
+                       0, s, part, nbatch / kv_div, kv_div, Nk, heads * 64, (bf16_t*)dk, (bf16_t*)dv, lddkv);
+  } else {
+    hipLaunchKernelGGL(sa_bwd_dkv_kernel, dim3(nkb * heads * nbatch), dim3(256), lds, s, (const bf16_t*)q, ldq,
+                       (const bf16_t*)k, (const bf16_t*)v, ldkv, (const bf16_t*)dout, lddo, (bf16_t*)dk, (bf16_t*)dv,
+                       lddkv, heads, Nq, Nk, kv_div, scale, lse, dvec, (float*)nullptr);
+  }
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }

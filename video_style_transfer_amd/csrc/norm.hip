@@ -683,14 +683,23 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const bf16_t* __rest
   }
 }
 
+// 64 columns per workgroup, 4 threads per column over strided partial blocks, combined in a fixed order
 __global__ __launch_bounds__(256) void layernorm_bwd_reduce_kernel(const float* __restrict__ part, int nblk, int C,
                                                                    float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= 2 * C) return;
-  const int which = c / C, cc = c - which * C;
+  __shared__ float red[4][64];
+  const int lc = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lc;
   float a = 0.f;
-  for (int b = 0; b < nblk; ++b) a += part[((size_t)b * 2 + which) * C + cc];
-  (which ? dbeta : dgamma)[cc] = a;
+  if (c < 2 * C) {
+    const int which = c / C, cc = c - which * C;
+    for (int b = q; b < nblk; b += 4) a += part[((size_t)b * 2 + which) * C + cc];
+  }
+  red[q][lc] = a;
+  __syncthreads();
+  if (q == 0 && c < 2 * C) {
+    const int which = c / C, cc = c - which * C;
+    (which ? dbeta : dgamma)[cc] = red[0][lc] + red[1][lc] + red[2][lc] + red[3][lc];
+  }
 }
 
 }  // namespace vst
@@ -867,7 +876,7 @@ extern "C" int vst_layernorm_bwd(const void* x, int ldx, const void* g, int ldg,
   else if (CH <= 128) VST_LNB(2);
   else VST_LNB(4);
 #undef VST_LNB
-  hipLaunchKernelGGL(layernorm_bwd_reduce_kernel, dim3((2 * C + 255) / 256), dim3(256), 0, s, part, grid, C, dgamma,
+  hipLaunchKernelGGL(layernorm_bwd_reduce_kernel, dim3((2 * C + 63) / 64), dim3(256), 0, s, part, grid, C, dgamma,
                      dbeta);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }

@@ -448,7 +448,7 @@ def spatial_attention_bwd(q, k, v, o, dout, nbatch, heads, Nq, Nk, kv_div=1, sca
         dq = torch.empty((nbatch * Nq, C), dtype=BF16, device=q.device)
     if dkv is None:
         dkv = torch.empty((nkv * Nk, 2 * C), dtype=BF16, device=q.device)
-    ws = torch.empty((_lib.load().vst_spatial_attention_bwd_workspace_bytes(nbatch, heads, Nq) + 3) // 4,
+    ws = torch.empty((_lib.load().vst_spatial_attention_bwd_workspace_bytes(nbatch, heads, Nq, Nk) + 3) // 4,
                      dtype=F32, device=q.device)
     scale = 0.125 if scale is None else scale
     with _Rec("spatial_attention_bwd", 10.0 * nbatch * heads * Nq * Nk * 64, 0.0):
