@@ -1,0 +1,185 @@
+"""The optimisation step of train_animatediff.py (BASELINE configs[4]) on the HIP training path,
+with data-parallel gradient averaging over RCCL.
+
+- `GradBucketAllReducer` replaces accelerate's DDP wrapper (train_animatediff.py:314-319 `accelerator.backward`,
+  `clip_grad_norm_`): gradients of the trainable set are copied into fp32 buckets by post-accumulate hooks as the
+  backward produces them, and each full bucket's all-reduce is launched asynchronously at once, so the exchange of
+  the up-block gradients overlaps the backward through the down blocks. Buckets are large (64 MB by default): xGMI
+  is point-to-point, a ring all-reduce is per-link bound, and fewer, larger messages amortise the per-call latency.
+  fp32 reduction keeps the 1/N averaging exact for the bf16 motion weights (the trainable set is ~156 M params,
+  626 MB of fp32 buckets, ~7 ms of ring time per step next to a ~1.2 s step).
+- `TrainStep` is one iteration of the loop body train_animatediff.py:214-319: Euler `add_noise` x + sigma(t)*eps
+  (:228-236, no input scaling), optional unconditional prompt with p = 0.1 (:248-254), the UNet forward through
+  `autograd.unet_train_tokens` (every forward and backward kernel on HIP), epsilon-prediction MSE in fp32
+  (:294-300), the orthogonality loss (:307-312, evaluated low-rank by `temporal_lora.compute_orth_loss`),
+  backward, gradient averaging, clip_grad_norm_ (:316), optimizer step (:317).
+"""
+from __future__ import annotations
+
+from typing import Dict, Iterable, List, Optional
+
+import torch
+import torch.distributed as dist
+
+BF16 = torch.bfloat16
+
+
+class GradBucketAllReducer:
+    """Bucketed, backward-overlapped gradient averaging over a torch.distributed group (RCCL on ROCm, gloo on CPU).
+
+    Usage per step: loss.backward(); reducer.finish(); optimizer.step().  Parameters that received no gradient in a
+    step contribute zeros (as DDP with find_unused_parameters would) and get an averaged gradient back, so every rank
+    takes the same optimizer step."""
+
+    def __init__(self, params: Iterable[torch.nn.Parameter], group=None, bucket_mb: float = 64.0,
+                 reduce_dtype: torch.dtype = torch.float32):
+        self.params: List[torch.nn.Parameter] = [p for p in params if p.requires_grad]
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.reduce_dtype = reduce_dtype
+        cap = max(1, int(bucket_mb * 2 ** 20) // torch.tensor([], dtype=reduce_dtype).element_size())
+        # autograd produces gradients roughly in reverse registration order: fill buckets in that order so the
+        # first bucket completes early in the backward.
+        self.buckets: List[List[torch.nn.Parameter]] = []
+        cur, n = [], 0
+        for p in reversed(self.params):
+            if cur and n + p.numel() > cap:
+                self.buckets.append(cur)
+                cur, n = [], 0
+            cur.append(p)
+            n += p.numel()
+        if cur:
+            self.buckets.append(cur)
+        self.flat: List[torch.Tensor] = []
+        self.where: Dict[int, tuple] = {}
+        for b, plist in enumerate(self.buckets):
+            off = 0
+            for p in plist:
+                self.where[id(p)] = (b, off)
+                off += p.numel()
+            self.flat.append(torch.zeros(off, dtype=reduce_dtype, device=plist[0].device))
+        self._ready = [set() for _ in self.buckets]
+        self._works: List[Optional[object]] = [None] * len(self.buckets)
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+
+    def bucket_sizes_mb(self) -> List[float]:
+        return [t.numel() * t.element_size() / 2 ** 20 for t in self.flat]
+
+    def _on_grad(self, p: torch.nn.Parameter) -> None:
+        b, off = self.where[id(p)]
+        self.flat[b][off:off + p.numel()].copy_(p.grad.reshape(-1))
+        self._ready[b].add(id(p))
+        if len(self._ready[b]) == len(self.buckets[b]):
+            self._launch(b)
+
+    def _launch(self, b: int) -> None:
+        if self._works[b] is not None:
+            raise RuntimeError(f"GradBucketAllReducer: bucket {b} launched twice in one step "
+                               "(a parameter received two gradients; call finish() after every backward)")
+        if self.world == 1:
+            self._works[b] = True
+            return
+        self._works[b] = dist.all_reduce(self.flat[b], group=self.group, async_op=True)
+
+    def finish(self) -> None:
+        """Launch the buckets that still wait for unused parameters (their segments are zero-filled), wait for every
+        all-reduce, divide by the world size and write the averages back into p.grad."""
+        for b, plist in enumerate(self.buckets):
+            if self._works[b] is None:
+                for p in plist:
+                    if id(p) not in self._ready[b]:
+                        _, off = self.where[id(p)]
+                        self.flat[b][off:off + p.numel()].zero_()
+                self._launch(b)
+        for b, plist in enumerate(self.buckets):
+            w = self._works[b]
+            if w is not True:
+                w.wait()
+            flat = self.flat[b]
+            if self.world > 1:
+                flat.div_(self.world)
+            for p in plist:
+                _, off = self.where[id(p)]
+                seg = flat[off:off + p.numel()].view(p.shape)
+                if p.grad is None:
+                    p.grad = seg.to(p.dtype).clone()
+                else:
+                    p.grad.copy_(seg)
+            self._ready[b].clear()
+            self._works[b] = None
+
+    def remove(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+
+def broadcast_parameters(module: torch.nn.Module, src: int = 0, group=None) -> None:
+    """Same initial weights on every rank (accelerate.prepare broadcasts rank 0's module state)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return
+    with torch.no_grad():
+        for t in list(module.parameters()) + list(module.buffers()):
+            dist.broadcast(t.data, src, group=group)
+
+
+class TrainStep:
+    """One train_animatediff.py iteration (:214-319) for a UNetMotionModel with temporal LoRA injected and the spatial
+    path frozen (`utils.freeze_spatial_layers`).  Inputs are VAE latents already scaled by vae.scaling_factor
+    (B, 4, F, h, w) fp32 on the device; prompt embeddings are (1, 77, D) / (1, Dp) as encode_prompt returns them."""
+
+    def __init__(self, unet, optimizer, scheduler, *, reducer: Optional[GradBucketAllReducer] = None,
+                 lambda_orth: float = 0.0, spatial_index: Optional[Dict] = None, max_grad_norm: float = 1.0,
+                 p_uncond: float = 0.1, resolution: int = 512, seed: int = 0):
+        self.unet = unet
+        self.opt = optimizer
+        self.sched = scheduler
+        self.reducer = reducer
+        self.lambda_orth = lambda_orth
+        self.spatial_index = spatial_index or {}
+        self.max_grad_norm = max_grad_norm
+        self.p_uncond = p_uncond
+        self.resolution = resolution
+        self.params = [p for p in unet.parameters() if p.requires_grad]
+        self.gen = torch.Generator(device="cpu").manual_seed(seed)
+
+    def __call__(self, latents: torch.Tensor, prompt, pooled, uncond_prompt=None, uncond_pooled=None) -> Dict:
+        from . import kernels as K
+        from .autograd import unet_train_tokens
+        from .temporal_lora import compute_orth_loss
+
+        unet = self.unet
+        B, Cl, F, h, w = latents.shape
+        dev = latents.device
+        noise = torch.randn(latents.shape, generator=self.gen).to(dev)                     # :228
+        t = torch.randint(0, self.sched.num_train_timesteps, (B,), generator=self.gen)    # :229-232
+        # add_noise with the clip's timestep on every frame (:233-236); sigma broadcasts over (C, F, h, w)
+        noisy = self.sched.add_noise(latents, noise, t.to(dev)).contiguous()
+        use_uncond = uncond_prompt is not None and float(torch.rand(1, generator=self.gen)) < self.p_uncond
+        enc = (uncond_prompt if use_uncond else prompt).to(dev, BF16)
+        pool = (uncond_pooled if use_uncond else pooled).to(dev, BF16)
+        enc = enc.expand(B, -1, -1).reshape(-1, enc.shape[-1]).contiguous()               # .repeat(B, 1, 1)
+        pool = pool.expand(B, -1).contiguous()
+        r = float(self.resolution)
+        tids = torch.tensor([[r, r, 0.0, 0.0, r, r]], device=dev).expand(B, -1).contiguous()  # :256-262
+
+        x = torch.empty(B * F * h * w, Cl, dtype=BF16, device=dev)
+        K.pack_latents(noisy, x)
+        with torch.no_grad():
+            emb = unet.embed(t.to(dev, torch.float32), pool, tids, B)
+        pred = unet_train_tokens(unet, x, B, F, h, w, emb, enc)                            # :265-273
+        target = noise.permute(0, 2, 3, 4, 1).reshape(-1, Cl)                              # epsilon, :276-277
+        loss_mse = torch.mean((pred.float() - target) ** 2)                                # :298-300
+        if self.lambda_orth > 0 and self.spatial_index:
+            loss_orth = compute_orth_loss(unet, self.spatial_index, self.lambda_orth).to(dev)
+        else:
+            loss_orth = torch.zeros((), device=dev)
+        loss = loss_mse + loss_orth
+        self.opt.zero_grad(set_to_none=True)
+        loss.backward()                                                                    # :314
+        if self.reducer is not None:
+            self.reducer.finish()
+        gnorm = torch.nn.utils.clip_grad_norm_(self.params, self.max_grad_norm)           # :316
+        self.opt.step()                                                                    # :317
+        return {"loss": loss.detach(), "loss_mse": loss_mse.detach(), "loss_orth": loss_orth.detach(),
+                "grad_norm": gnorm.detach(), "uncond": use_uncond, "timesteps": t}
