@@ -235,13 +235,9 @@ def main():
     if shard is not None and not shard.graph_capturable:
         graph_note = f"{shard.backend} collectives are not graph-capturable; eager steps"
     elif not args.no_graph:
-        try:
-            den.capture()
-        except Exception as e:  # a collective that cannot be captured: same HIP kernels, eager launches
-            graph_note = f"graph capture failed ({type(e).__name__}: {str(e)[:120]}); eager steps"
-            den.graph = None
-            den.use_graph = False
-            torch.cuda.synchronize()
+        # no silent eager fallback: a step (or an RCCL collective inside it) that cannot be captured fails the run,
+        # so an N-GPU line is never an uncaptured number; --no-graph measures eager launches on purpose
+        den.capture()
     t_build = time.perf_counter() - t_build
 
     def one_step():

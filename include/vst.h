@@ -62,7 +62,8 @@ int vst_conv3x3_ex(const void* x1, int C1, const void* x2, int C2, int nimg, int
  * AnimateDiffAttnProcessor2_0.__call__ (animatediff/attention_processor.py:78-80).  K/V row
  * batch = q batch / kv_div (replaces the repeat_interleave of text states, :63-66). */
 int vst_spatial_attention(const void* q, int ldq, const void* k, const void* v, int ldkv, void* o, int ldo,
-                          int nbatch, int heads, int Nq, int Nk, int kv_div, int head_dim, float scale, void* stream);
+                          int nbatch, int heads, int Nq, int Nk, int kv_div, int head_dim, float scale, float* lse,
+                          void* stream);  /* lse: NULL, or fp32 [nbatch*heads*Nq] log2-domain logsumexp (training) */
 
 /* Frame-axis attention (motion module / TemporalTransformerBlock, animatediff/temporal_transformer.py:66-68):
  * token (clip b, frame f, pixel p) at row (b*F + f)*HW + p; F <= 32; head_dim in {8,16,32,40,64,80,160}. */
@@ -120,7 +121,7 @@ int vst_pack_latents(const float* lat, int B, int Cl, int F, int HW, const float
                      float fixed_scale, int ncopy, void* out, void* stream);
 int vst_euler_cfg_step(const void* noise, int ncopy, float guidance, float* lat, int B, int Cl, int F, int HW,
                        const float* sigmas, const int* step_idx, void* stream);
-int vst_step_advance(int* step_idx, void* stream);
+int vst_step_advance(int* step_idx, int num_steps, void* stream);  // wraps to 0 at num_steps
 int vst_silu(const void* x, void* y, size_t n, void* stream);
 int vst_add(const void* a, const void* b, void* y, size_t n, void* stream);
 int vst_copy2d(const void* x, int ldx, void* y, int ldy, int rows, int cols, void* stream);
@@ -143,14 +144,16 @@ int vst_groupnorm_bwd(const void* x, int ldx, const void* g, int ldg, int C, int
                       int groups, float eps, const float* gamma, const float* beta, int silu_act, void* dx, int lddx,
                       float* dgamma, float* dbeta, void* workspace, void* stream);
 /* vst_spatial_attention_bwd: gradients of vst_spatial_attention (head_dim 64; K/V shared by kv_div consecutive
- * batches, as for the per-clip text states) from dO and the forward output o: dq (lddq), dk/dv (lddkv, one row per
- * kv token: the gradient of text K/V summed over the frames sharing it).  Workspace:
- * vst_spatial_attention_bwd_workspace_bytes (per-query logsumexp and dO.O). */
+ * batches, as for the per-clip text states) from dO, the forward output o and the forward's lse output (flash-
+ * attention backward on MFMA, deterministic): dq (lddq), dk/dv (lddkv, one row per kv token: the gradient of text
+ * K/V summed over the frames sharing it; both NULL when K/V are frozen, which skips that pass).  Replaces the
+ * autograd backward of F.scaled_dot_product_attention (animatediff/attention_processor.py:78-80) that
+ * accelerator.backward runs (train_animatediff.py:314).  Workspace: vst_spatial_attention_bwd_workspace_bytes. */
 size_t vst_spatial_attention_bwd_workspace_bytes(int nbatch, int heads, int Nq, int Nk);
 int vst_spatial_attention_bwd(const void* q, int ldq, const void* k, const void* v, int ldkv, const void* o, int ldo,
-                              const void* dout, int lddo, void* dq, int lddq, void* dk, void* dv, int lddkv, int nbatch,
-                              int heads, int Nq, int Nk, int kv_div, int head_dim, float scale, void* workspace,
-                              void* stream);
+                              const void* dout, int lddo, const float* lse, void* dq, int lddq, void* dk, void* dv,
+                              int lddkv, int nbatch, int heads, int Nq, int Nk, int kv_div, int head_dim, float scale,
+                              void* workspace, void* stream);
 /* Sampler data gradients (NHWC tokens, C % 8 == 0): vst_zero_insert writes x [nimg, h, w, C] onto the even
  * positions of a caller-zeroed [nimg, 2h, 2w, C] (Downsample2D stride-2 conv dgrad); vst_sumpool2x2 sums 2x2 blocks
  * of x [nimg, 2h, 2w, C] into y [nimg, h, w, C] (adjoint of Upsample2D's nearest-2x). */

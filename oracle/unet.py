@@ -145,7 +145,8 @@ def unet_forward(P, cfg, sample, timestep, encoder_hidden_states, text_embeds, t
 
     cfg: dict with block_out_channels, down_block_types, up_block_types, layers_per_block,
     transformer_layers_per_block, num_attention_heads, addition_time_embed_dim,
-    use_motion_mid_block, motion_num_attention_heads.
+    use_motion_mid_block, motion_num_attention_heads, motion_modules (default True; False = the SDXL
+    UNet2DConditionModel forward, sample (B, C, 1, h, w)).
     """
     lora = lora if lora is not None else LoRAState()
     sample = sample.float()
@@ -166,13 +167,15 @@ def unet_forward(P, cfg, sample, timestep, encoder_hidden_states, text_embeds, t
     skips = [x]
     L = cfg["layers_per_block"]
     mh = cfg.get("motion_num_attention_heads", 8)
+    motion = cfg.get("motion_modules", True)  # False: plain SDXL UNet2DConditionModel (animatediff/utils.py:20)
     for i, bt in enumerate(cfg["down_block_types"]):
         for j in range(L):
             x = resnet(P, f"down_blocks.{i}.resnets.{j}", x, emb)
             if bt.startswith("CrossAttn"):
                 x = transformer2d(P, f"down_blocks.{i}.attentions.{j}", x, enc, cfg["num_attention_heads"][i],
                                   cfg["transformer_layers_per_block"][i], lora)
-            x = motion_module(P, f"down_blocks.{i}.motion_modules.{j}", x, Fr, mh)
+            if motion:
+                x = motion_module(P, f"down_blocks.{i}.motion_modules.{j}", x, Fr, mh)
             skips.append(x)
         if i < len(ch) - 1:
             x = conv(P, f"down_blocks.{i}.downsamplers.0.conv", x, stride=2)
@@ -180,7 +183,7 @@ def unet_forward(P, cfg, sample, timestep, encoder_hidden_states, text_embeds, t
     x = resnet(P, "mid_block.resnets.0", x, emb)
     x = transformer2d(P, "mid_block.attentions.0", x, enc, cfg["num_attention_heads"][-1],
                       cfg["transformer_layers_per_block"][-1], lora)
-    if cfg.get("use_motion_mid_block", False):
+    if cfg.get("use_motion_mid_block", False) and motion:
         x = motion_module(P, "mid_block.motion_modules.0", x, Fr, mh)
     x = resnet(P, "mid_block.resnets.1", x, emb)
     rtl = list(reversed(cfg["transformer_layers_per_block"]))
@@ -191,7 +194,8 @@ def unet_forward(P, cfg, sample, timestep, encoder_hidden_states, text_embeds, t
             x = resnet(P, f"up_blocks.{i}.resnets.{j}", x, emb)
             if bt.startswith("CrossAttn"):
                 x = transformer2d(P, f"up_blocks.{i}.attentions.{j}", x, enc, rheads[i], rtl[i], lora)
-            x = motion_module(P, f"up_blocks.{i}.motion_modules.{j}", x, Fr, mh)
+            if motion:
+                x = motion_module(P, f"up_blocks.{i}.motion_modules.{j}", x, Fr, mh)
         if i < len(ch) - 1:
             x = F.interpolate(x, scale_factor=2.0, mode="nearest")
             x = conv(P, f"up_blocks.{i}.upsamplers.0.conv", x)

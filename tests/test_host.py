@@ -34,7 +34,10 @@ def test_bad_arguments_rejected_without_gpu():
     # K not a multiple of 8 -> VST_ERR_ARG before any launch
     assert lib.vst_gemm(1, 8, None, 0, 0, 1, 8, 4, 4, 6, None, None, 1, 0, None, 0, 1, 8, 0, None) == 1
     assert lib.vst_temporal_attention(1, 1, 1, 8, 1, 8, 1, 64, 1, 8, 8, 1.0, None) == 1  # F > 32
-    assert lib.vst_spatial_attention(1, 64, 1, 1, 64, 1, 64, 1, 1, 8, 8, 1, 40, 1.0, None) == 1  # head_dim != 64
+    assert lib.vst_spatial_attention(1, 64, 1, 1, 64, 1, 64, 1, 1, 8, 8, 1, 40, 1.0, None, None) == 1  # head_dim != 64
+    assert lib.vst_step_advance(1, 0, None) == 1  # empty schedule
+    assert lib.vst_spatial_attention_bwd(1, 64, 1, 1, 64, 1, 64, 1, 64, None, 1, 64, None, None, 0, 1, 1, 8, 8, 1, 64,
+                                         0.125, 1, None) == 1  # no lse
 
 
 @pytest.mark.parametrize("cfgname", ["tiny", "sdxl"])

@@ -351,8 +351,11 @@ def test_timestep_and_euler(cuda, K):
     c = noise[B * Fr * H * W:].float().view(B, Fr, H, W, Cl).permute(0, 4, 1, 2, 3)
     ref = lat + (0.0 - 0.0 + 10.0 - 14.6) * (u + 7.5 * (c - u))
     check(latd, ref, rel_l2=1e-5, rel_max=1e-5, name="euler")
-    K.step_advance(step)
+    K.step_advance(step, 50)
     assert int(step.item()) == 1
+    step.fill_(49)
+    K.step_advance(step, 50)  # end of the schedule wraps instead of indexing sigmas[51]
+    assert int(step.item()) == 0
 
 
 @pytest.mark.parametrize("M,N,Kd,tile,splits", [(700, 1280, 320, 0, 0), (4096, 2560, 640, 0, 0), (300, 384, 640, 1, 3),

@@ -308,8 +308,12 @@ def test_resnet_block_backward_vs_oracle(cuda, cin, cout, H):
         assert e < 2e-2, (name, e)
 
 
-@pytest.mark.parametrize("nb,heads,Nq,Nk,kv_div", [(2, 2, 256, 256, 1), (4, 3, 100, 77, 2), (1, 1, 64, 130, 1)])
-def test_spatial_attention_fn_grads(cuda, nb, heads, Nq, Nk, kv_div):
+@pytest.mark.parametrize("nb,heads,Nq,Nk,kv_div,kv_grad", [(2, 2, 256, 256, 1, True), (4, 3, 100, 77, 2, True),
+                                                             (1, 1, 64, 130, 1, True), (2, 10, 1024, 1024, 1, True),
+                                                             (16, 2, 200, 77, 8, False), (3, 1, 17, 300, 3, True)])
+def test_spatial_attention_fn_grads(cuda, nb, heads, Nq, Nk, kv_div, kv_grad):
+    """MFMA flash-attention backward (sa_bwd_dq_kernel / sa_bwd_dkv_kernel) vs torch.autograd in fp32 on the same
+    bf16 operands; kv_grad=False is the frozen cross-attention case (the dK/dV pass is skipped)."""
     from video_style_transfer_amd.autograd import SpatialAttentionFn
     g = torch.Generator().manual_seed(nb * Nq + Nk)
     C = heads * 64
@@ -325,17 +329,23 @@ def test_spatial_attention_fn_grads(cuda, nb, heads, Nq, Nk, kv_div):
     o = torch.softmax(qh @ kh.transpose(-1, -2) * 0.125, -1) @ vh
     ref = o.transpose(1, 2).reshape(nb * Nq, C)
     ref.backward(gy.float())
-    qd, kd, vd = (t.to(cuda).requires_grad_(True) for t in (q, k, v))
+    qd = q.to(cuda).requires_grad_(True)
+    kd, vd = (t.to(cuda).requires_grad_(kv_grad) for t in (k, v))
     out = SpatialAttentionFn.apply(qd, kd, vd, nb, heads, Nq, Nk, kv_div)
     out.backward(gy.to(cuda))
-    for name, got, want in (("o", out, ref), ("dq", qd.grad, qr.grad), ("dk", kd.grad, kr.grad),
-                            ("dv", vd.grad, vr.grad)):
+    checks = [("o", out, ref), ("dq", qd.grad, qr.grad)]
+    if kv_grad:
+        checks += [("dk", kd.grad, kr.grad), ("dv", vd.grad, vr.grad)]
+    else:
+        assert kd.grad is None and vd.grad is None
+    for name, got, want in checks:
         e = rel(got, want)
         print(f"[train] spatial attn nb={nb} h={heads} {Nq}x{Nk} kv_div={kv_div} {name}: rel_l2={e:.2e}")
         assert e < 2e-2, (name, e)
 
 
-def test_transformer2d_backward_vs_oracle(cuda):
+@pytest.mark.parametrize("unfreeze_mergers", [False, True])
+def test_transformer2d_backward_vs_oracle(cuda, unfreeze_mergers):
     """The frozen spatial Transformer2DModel with UnZipLoRA r=4 on all its q/k/v/out: output and
     dL/dx on the HIP autograd path vs torch.autograd through oracle.unet.transformer2d (fp32), text states of 2 clips
     shared by their frames (cross-attention K/V gradient-free, dQ through the text attention)."""
@@ -370,7 +380,11 @@ def test_transformer2d_backward_vs_oracle(cuda):
     for n, p in t2d.named_parameters():
         if p.dim() == 2 and "lora_layer" not in n:
             p.data = p.data.to(torch.bfloat16)
-    P = {f"t.{n}": p.detach().float().cpu() for n, p in t2d.named_parameters()}
+    if unfreeze_mergers:  # --unfreeze_mergers (animatediff/utils.py:86-88): the UnZipLoRA mergers train
+        for n, p in t2d.named_parameters():
+            if "merge_content" in n or "merge_style" in n:
+                p.requires_grad_(True)
+    P = {f"t.{n}": p.detach().float().cpu().requires_grad_(p.requires_grad) for n, p in t2d.named_parameters()}
     x_img = torch.randn(nimg, C, H, H).to(torch.bfloat16).float()
     enc = torch.randn(nclip, L, D).to(torch.bfloat16).float()
     gy = torch.randn(nimg, C, H, H).to(torch.bfloat16).float()
@@ -387,6 +401,16 @@ def test_transformer2d_backward_vs_oracle(cuda):
         e = rel(got, ref)
         print(f"[train] transformer2d {name}: rel_l2={e:.2e}")
         assert e < 3e-2, (name, e)
+    if unfreeze_mergers:
+        named = dict(t2d.named_parameters())
+        picks = [n for n in named if "merge_" in n]
+        assert len(picks) == 16
+        for n in picks[:3] + picks[-3:]:  # self-attn to_q/to_k, cross-attn to_v (through the text K/V) / to_out
+            got, want = named[n].grad, P[f"t.{n}"].grad
+            assert got is not None, n
+            e = rel(got, want)
+            print(f"[train] transformer2d merger grad {n}: rel_l2={e:.2e}")
+            assert e < 5e-2, (n, e)
 
 
 def test_unet_training_step_grads_vs_oracle(cuda):

@@ -26,7 +26,7 @@ SIGNATURES = {
     "vst_conv3x3": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P, _I, _P, _I, _P]),
     "vst_conv3x3_ex": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _I, _P, _I, _P, _I, _I, _I, _P,
                             _S, _P]),
-    "vst_spatial_attention": (_I, [_P, _I, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _F, _P]),
+    "vst_spatial_attention": (_I, [_P, _I, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _F, _P, _P]),
     "vst_temporal_attention": (_I, [_P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _F, _P]),
     "vst_groupnorm_workspace_bytes": (_S, [_I, _I, _I, _I]),
     "vst_groupnorm_sums": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
@@ -41,7 +41,7 @@ SIGNATURES = {
     "vst_timestep_embedding": (_I, [_P, _P, _I, _I, _I, _F, _P, _I, _I, _I, _P]),
     "vst_pack_latents": (_I, [_P, _I, _I, _I, _I, _P, _P, _F, _I, _P, _P]),
     "vst_euler_cfg_step": (_I, [_P, _I, _F, _P, _I, _I, _I, _I, _P, _P, _P]),
-    "vst_step_advance": (_I, [_P, _P]),
+    "vst_step_advance": (_I, [_P, _I, _P]),
     "vst_silu": (_I, [_P, _P, _S, _P]),
     "vst_add": (_I, [_P, _P, _P, _S, _P]),
     "vst_copy2d": (_I, [_P, _I, _P, _I, _I, _I, _P]),
@@ -52,8 +52,8 @@ SIGNATURES = {
     "vst_groupnorm_bwd_workspace_bytes": (_S, [_I, _I, _I, _I]),
     "vst_groupnorm_bwd": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _F, _P, _P, _I, _P, _I, _P, _P, _P, _P]),
     "vst_spatial_attention_bwd_workspace_bytes": (_S, [_I, _I, _I, _I]),
-    "vst_spatial_attention_bwd": (_I, [_P, _I, _P, _P, _I, _P, _I, _P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _I,
-                                       _F, _P, _P]),
+    "vst_spatial_attention_bwd": (_I, [_P, _I, _P, _P, _I, _P, _I, _P, _I, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _I,
+                                       _I, _F, _P, _P]),
     "vst_zero_insert": (_I, [_P, _I, _I, _I, _I, _P, _P]),
     "vst_sumpool2x2": (_I, [_P, _I, _I, _I, _I, _P, _P]),
     "vst_temporal_attention_bwd": (_I, [_P, _P, _P, _I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P]),

@@ -14,6 +14,8 @@ cast to the parameters' dtypes.
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
 
 from . import kernels as K
@@ -32,6 +34,16 @@ def _wt(W: torch.Tensor) -> torch.Tensor:
         c = (key, K.transpose(W.detach().to(BF16).contiguous()))
         W.__dict__["_vst_wt"] = c
     return c[1]
+
+
+def _transpose_padded(t: torch.Tensor, Mp: int) -> torch.Tensor:
+    """[M, C] -> [C, Mp] bf16 with zero columns M..Mp (Mp = M: a plain vst_transpose)."""
+    M = t.shape[0]
+    if Mp == M:
+        return K.transpose(t)
+    out = torch.zeros(t.shape[1], Mp, device=t.device, dtype=BF16)
+    K.transpose(t, out=out[:, :M])
+    return out
 
 
 class LoRALinearFn(torch.autograd.Function):
@@ -78,20 +90,22 @@ class LoRALinearFn(torch.autograd.Function):
             WT_aug[:, N:] = (A_pad.float().t() * s).to(BF16)
             dX = K.linear(g, WT_aug, x2=v, alg_k2=r)                             # [M, in]
         if need_w or need_b or need_a or need_bb:
-            gT = K.transpose(g)                                                  # [N, M]
+            # the weight-side GEMMs contract over the token axis: pad it to the GEMM's K granule (8) with zeros
+            Mp = (M + 7) // 8 * 8
+            gT = _transpose_padded(g, Mp)                                        # [N, Mp]
             if need_w or need_a:
-                xT = K.transpose(x2d)                                            # [in, M]
+                xT = _transpose_padded(x2d, Mp)                                  # [in, Mp]
             if need_w:
                 dW = K.linear(gT, xT).to(W.dtype)                                # [N, in] = g^T x
             if need_a:
-                vT = K.transpose(v)                                              # [P, M]
+                vT = _transpose_padded(v, Mp)                                    # [P, Mp]
                 dA = (K.linear(vT, xT)[:r].float() * s).to(A.dtype)             # [r, in] = s v^T x
             if need_bb or need_b:
                 P1 = pad32(r + 1)
-                U1 = torch.zeros(P1, M, device=dev, dtype=BF16)
+                U1 = torch.zeros(P1, Mp, device=dev, dtype=BF16)
                 if r:
-                    K.transpose(u[:, :r], out=U1[:r])                            # u^T
-                U1[r].fill_(1.0)                                                 # ones row -> db
+                    K.transpose(u[:, :r], out=U1[:r, :M])                        # u^T
+                U1[r, :M].fill_(1.0)                                             # ones row -> db
                 gu = K.linear(gT, U1)                                            # [N, P1]
                 if need_bb:
                     dB = (gu[:, :r].float() * s).to(B.dtype)                     # [N, r] = s g^T u
@@ -169,12 +183,13 @@ class GEGLUFn(torch.autograd.Function):
         if need_x:
             dX = K.linear(dp, K.transpose(Wi))                                  # [M, C] = dp W
         if need_w or need_b:
-            dpT = K.transpose(dp)                                              # [2Nh, M]
+            Mp = (M + 7) // 8 * 8
+            dpT = _transpose_padded(dp, Mp)                                    # [2Nh, Mp]
             if need_w:
-                dW = _deinterleave32(K.linear(dpT, K.transpose(x2d))).to(ctx.w_dtype)
+                dW = _deinterleave32(K.linear(dpT, _transpose_padded(x2d, Mp))).to(ctx.w_dtype)
             if need_b:
-                ones = torch.zeros(32, M, device=dp.device, dtype=BF16)
-                ones[0].fill_(1.0)
+                ones = torch.zeros(32, Mp, device=dp.device, dtype=BF16)
+                ones[0, :M].fill_(1.0)
                 db = _deinterleave32(K.linear(dpT, ones)[:, 0].float()).to(ctx.b_dtype)
         return dX, dW, db
 
@@ -241,6 +256,15 @@ class AddFn(torch.autograd.Function):
         return g, g
 
 
+def _mergers_trainable(lora) -> bool:
+    return any(getattr(lora, n, None) is not None and getattr(lora, n).requires_grad
+               for n in ("merge_content", "merge_style"))
+
+
+def _any_merger_trainable(lins) -> bool:
+    return any(getattr(lin, "lora_layer", None) is not None and _mergers_trainable(lin.lora_layer) for lin in lins)
+
+
 def _proj_parts(lins, scale: float = 1.0):
     """(W [sum out, in], b or None, A [sum r, in], B [sum out, sum r] with the LoRA scales folded in) of projections
     sharing one input, as autograd-tracked concatenations of the modules' own parameters.  Frozen UnZipLoRA layers
@@ -258,7 +282,9 @@ def _proj_parts(lins, scale: float = 1.0):
         elif lora is not None:
             A, V = lora.lowrank_factors(scale)
             As.append(A.detach().float())
-            Bs.append(V.detach().float())
+            # trainable mergers (--unfreeze_mergers, animatediff/utils.py:86-88): V = B * m stays on the autograd
+            # graph, so LoRALinearFn's dB = s g^T u reaches merge_content / merge_style
+            Bs.append(V.float() if _mergers_trainable(lora) else V.detach().float())
         else:
             As.append(base.weight.new_zeros(0, base.in_features, dtype=torch.float32))
             Bs.append(base.weight.new_zeros(base.out_features, 0, dtype=torch.float32))
@@ -296,8 +322,9 @@ def transformer2d_train(t2d, x2d, nimg: int, H: int, W: int, enc=None, frames_pe
         h = AddFn.apply(h, proj_train([a1.to_out[0]], o, scale))
         n = LayerNormFn.apply(h, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps)
         q = proj_train([a2.to_q], n, scale)
-        with torch.no_grad():
-            L = enc.shape[0] // (nimg // frames_per_text)
+        L = enc.shape[0] // (nimg // frames_per_text)
+        # text K/V are constants of the frozen path unless their UnZipLoRA mergers train
+        with contextlib.nullcontext() if _any_merger_trainable([a2.to_k, a2.to_v]) else torch.no_grad():
             kv = proj_train([a2.to_k, a2.to_v], enc, scale)
         o = SpatialAttentionFn.apply(q, kv[:, :inner], kv[:, inner:], nimg, a2.heads, HW, L, frames_per_text)
         h = AddFn.apply(h, proj_train([a2.to_out[0]], o, scale))
@@ -419,19 +446,21 @@ class SpatialAttentionFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, nbatch: int, heads: int, Nq: int, Nk: int, kv_div: int):
         q, k, v = (t.to(BF16).contiguous() for t in (q, k, v))
-        o = K.spatial_attention(q, k, v, nbatch, heads, Nq, Nk, kv_div, scale=0.125)
-        ctx.save_for_backward(q, k, v, o)
+        lse = torch.empty(nbatch * heads * Nq, dtype=torch.float32, device=q.device)
+        o = K.spatial_attention(q, k, v, nbatch, heads, Nq, Nk, kv_div, scale=0.125, lse=lse)
+        ctx.save_for_backward(q, k, v, o, lse)
         ctx.dims = (nbatch, heads, Nq, Nk, kv_div)
         return o
 
     @staticmethod
     def backward(ctx, g):
-        q, k, v, o = ctx.saved_tensors
+        q, k, v, o, lse = ctx.saved_tensors
         nbatch, heads, Nq, Nk, kv_div = ctx.dims
-        dq, dk, dv = K.spatial_attention_bwd(q, k, v, o, g.to(BF16).contiguous(), nbatch, heads, Nq, Nk, kv_div,
-                                             scale=0.125)
+        # frozen K/V (the cross-attention over text states of the frozen spatial path) skip the dK/dV pass
+        need_dkv = bool(ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
+        dq, dk, dv = K.spatial_attention_bwd(q, k, v, o, g.to(BF16).contiguous(), lse, nbatch, heads, Nq, Nk, kv_div,
+                                             scale=0.125, need_dkv=need_dkv)
         return dq, dk, dv, None, None, None, None, None
-
 
 
 def unet_train_tokens(unet, x, B: int, F: int, h: int, w: int, emb_silu, enc2d, scale: float = 1.0):
@@ -454,7 +483,8 @@ def unet_train_tokens(unet, x, B: int, F: int, h: int, w: int, emb_silu, enc2d, 
             x = res_block(res, x)
             if blk.attentions is not None:
                 x = transformer2d_train(blk.attentions[j], x, nimg, H, W, enc2d, F, scale)
-            x = motion_module_train(blk.motion_modules[j], x, B, F, H * W)
+            if blk.motion_modules is not None:
+                x = motion_module_train(blk.motion_modules[j], x, B, F, H * W)
             skips.append((x, H, W))
         if blk.downsamplers is not None:
             x = Conv3x3Fn.apply(x, blk.downsamplers[0].conv, nimg, H, W)
@@ -473,7 +503,8 @@ def unet_train_tokens(unet, x, B: int, F: int, h: int, w: int, emb_silu, enc2d, 
             x = res_block(res, CatFn.apply(x, sk))
             if blk.attentions is not None:
                 x = transformer2d_train(blk.attentions[j], x, nimg, H, W, enc2d, F, scale)
-            x = motion_module_train(blk.motion_modules[j], x, B, F, H * W)
+            if blk.motion_modules is not None:
+                x = motion_module_train(blk.motion_modules[j], x, B, F, H * W)
         if blk.upsamplers is not None:
             x = Conv3x3Fn.apply(x, blk.upsamplers[0].conv, nimg, H, W, None, 1, True)
             H, W = 2 * H, 2 * W

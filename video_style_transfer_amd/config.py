@@ -32,6 +32,7 @@ class UNetMotionConfig:
     motion_max_seq_length: int = 32
     motion_norm_num_groups: int = 32
     use_motion_mid_block: bool = False
+    motion_modules: bool = True  # False: the plain SDXL UNet2DConditionModel (animatediff/utils.py:20), F = 1
     extra: dict = field(default_factory=dict)
 
     @property
@@ -48,6 +49,13 @@ class UNetMotionConfig:
     @classmethod
     def sdxl(cls) -> "UNetMotionConfig":
         return cls()
+
+    @classmethod
+    def sdxl_image(cls) -> "UNetMotionConfig":
+        """The SDXL UNet2DConditionModel before the motion adapter (BASELINE configs[0];
+        `UNet2DConditionModel.from_pretrained(subfolder="unet")`, animatediff/utils.py:20): same blocks, no motion
+        modules; used with one frame per sample."""
+        return cls(motion_modules=False)
 
     @classmethod
     def tiny(cls) -> "UNetMotionConfig":

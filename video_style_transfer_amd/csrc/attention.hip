@@ -57,7 +57,7 @@ constexpr int SA_LDS = 4 * SA_TILE;               // K,V double-buffered
 __global__ __launch_bounds__(256, 2) void spatial_attn_kernel(
     const bf16_t* __restrict__ Q, int ldq, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V, int ldkv,
     bf16_t* __restrict__ O, int ldo, int nbatch, int heads, int Nq, int Nk, int kv_div, float scale_log2,
-    uint32_t q_bytes, uint32_t kv_bytes) {
+    uint32_t q_bytes, uint32_t kv_bytes, float* __restrict__ lse) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nqb = (Nq + 127) / 128;
@@ -220,6 +220,7 @@ __global__ __launch_bounds__(256, 2) void spatial_attn_kernel(
     const float inv = 1.0f / l;
     const int q = qbase + qb * 16 + fr;
     if (q >= Nq) continue;
+    if (lse && g == 0) lse[(size_t)bh * Nq + q] = mrun[qb] * scale_log2 + __log2f(l);  // training: P = exp2(s sl2 - lse)
     bf16_t* orow = O + (size_t)(b * Nq + q) * ldo + h * 64;
 #pragma unroll
     for (int db = 0; db < 4; ++db) {
@@ -435,234 +436,346 @@ __global__ __launch_bounds__(64) void temporal_attn_bwd_kernel(
 
 
 // ---------------------------------------------------------------------------------
-// Spatial attention backward (training path), head_dim 64, two passes (correctness-first,
-// scalar fp32 FMAs on LDS tiles; the forward is the MFMA kernel above):
-//  sa_bwd_dq_kernel  (per batch*head, 64-query block): lse_i by an online pass over the keys, D_i = dO_i . O_i, then
-//                    P = exp(scale S - lse), dP = dO V^T, dS = P (dP - D), dQ = scale dS K; writes lse and D.
-//  sa_bwd_dkv_kernel (per kv batch*head, 64-key block): over every query that attends to these keys (all frames
-//                    sharing the text K/V when kv_div > 1): dV += P^T dO, dK += scale dS^T Q.
-// Thread t of 256 owns tile row (t >> 2) and 16 columns ((t & 3) * 16 ..); row reductions use xor-1/2 shuffles.
-constexpr int SB_T = 64;
+// Spatial attention backward (training path), head_dim 64, flash-attention style on the same
+// v_mfma_f32_16x16x32_bf16 tiles as the forward, deterministic (no atomics), P recomputed from the forward's
+// log2-domain logsumexp (lse2 = max * scale*log2(e) + log2(l), written by spatial_attn_kernel):
+//   P = exp2(S * sl2 - lse2),  dP = dO V^T,  D_i = dO_i . O_i,  dS = P * (dP - D),
+//   dQ = scale dS K,  dK = scale dS^T Q,  dV = P^T dO.
+// sa_bwd_dq_kernel: 4 waves x 32 queries per workgroup, loop over 64-key tiles (K row + K transposed + V row copies
+//   double-buffered in LDS); per tile and wave 48 MFMAs (S^T, dP^T, dQ^T); also writes D for the dK/dV kernel.
+// sa_bwd_dkv_kernel: 4 waves x 32 keys per workgroup, loop over 64-query tiles of every query batch that reads these
+//   K/V (kv_div > 1: all frames of a clip share the text K/V, so their contributions sum in registers); per tile and
+//   wave 64 MFMAs (S, dP, dV^T, dK^T).  Skipped when the caller needs no dK/dV (frozen cross-attention K/V).
+// Fragment conventions follow the forward: accumulators hold transposed tiles (lane column = the row token), P / dS
+// feed the B operand straight from the accumulators, and the A operands of the d-major products (K^T, dO^T, Q^T)
+// come from ds_read_b64_tr_b16 reads of a v_off-swizzled LDS copy.
+constexpr int SB_TILE = 64 * 64 * 2;  // one 64-row x 64-d bf16 tile, 8 KiB
 
-__device__ __forceinline__ void sb_load_tile(float* dst, const bf16_t* src, int ld, int row0, int nrows, int col0) {
-  // dst[64][64] <- src[(row0 + r) * ld + col0 + c], zero beyond nrows
-  for (int idx = threadIdx.x; idx < SB_T * 8; idx += 256) {
-    const int r = idx >> 3, c8 = (idx & 7) * 8;
-    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (row0 + r < nrows) unpack8(*reinterpret_cast<const u32x4*>(src + (size_t)(row0 + r) * ld + col0 + c8), v);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) dst[r * SB_T + c8 + e] = v[e];
-  }
+// one transposed A fragment: T^T[d = 16 db + li][rows 32 st + 4 g + {0..3}, 32 st + 16 + 4 g + {0..3}]
+__device__ __forceinline__ bf16x8 tr_frag(const char* T, int st, int db, int lane) {
+  const int li = lane & 15, g = lane >> 4;
+  const int r0 = st * 32 + g * 4 + (li >> 2);
+  const int col = db * 16 + (li & 3) * 4;
+  const int ch = col >> 3, within = (col & 7) * 2;
+  return cat_tr(ds_read_tr(T + v_off(r0, ch) + within), ds_read_tr(T + v_off(r0 + 16, ch) + within));
 }
 
-__global__ __launch_bounds__(256) void sa_bwd_dq_kernel(const bf16_t* __restrict__ Q, int ldq,
-                                                        const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
-                                                        int ldkv, const bf16_t* __restrict__ O, int ldo,
-                                                        const bf16_t* __restrict__ dO, int lddo,
-                                                        bf16_t* __restrict__ dQ, int lddq, int heads, int Nq, int Nk,
-                                                        int kv_div, float scale, float* __restrict__ lse_out,
-                                                        float* __restrict__ d_out) {
-  extern __shared__ float sbm[];
-  float* qs = sbm;
-  float* os = qs + SB_T * SB_T;  // dO
-  float* ks = os + SB_T * SB_T;
-  float* vs = ks + SB_T * SB_T;
-  const int nqb = (Nq + SB_T - 1) / SB_T;
-  const int qb = blockIdx.x % nqb, bh = blockIdx.x / nqb;
+__global__ __launch_bounds__(256, 2) void sa_bwd_dq_kernel(
+    const bf16_t* __restrict__ Q, int ldq, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V, int ldkv,
+    const bf16_t* __restrict__ O, int ldo, const bf16_t* __restrict__ dO, int lddo, const float* __restrict__ lse,
+    bf16_t* __restrict__ dQ, int lddq, float* __restrict__ dvec, int nbatch, int heads, int Nq, int Nk, int kv_div,
+    float scale, float sl2, uint32_t q_bytes, uint32_t o_bytes, uint32_t do_bytes, uint32_t kv_bytes) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nqb = (Nq + 127) / 128;
+  const int wg = xcd_remap(blockIdx.x, nqb * heads * nbatch);
+  const int qblk = wg % nqb, bh = wg / nqb;
   const int h = bh % heads, b = bh / heads, bkv = b / kv_div;
-  const int t = threadIdx.x, r = t >> 2, c0 = (t & 3) * 16;
-  const int q0 = qb * SB_T;
-  sb_load_tile(qs, Q + (size_t)b * Nq * ldq, ldq, q0, Nq, h * 64);
-  sb_load_tile(os, dO + (size_t)b * Nq * lddo, lddo, q0, Nq, h * 64);
-  __syncthreads();  // other threads' rows of the dO tile are read below
-  // D_r = dO_r . O_r
-  float dr = 0.f;
-  if (q0 + r < Nq) {
-    const bf16_t* orow = O + ((size_t)b * Nq + q0 + r) * ldo + h * 64 + c0;
-    for (int d = 0; d < 16; ++d) dr += os[r * SB_T + c0 + d] * bf2f(orow[d]);
-  }
-  dr += __shfl_xor(dr, 1);
-  dr += __shfl_xor(dr, 2);
-  const int nkt = (Nk + SB_T - 1) / SB_T;
-  const bf16_t* Kb = K + (size_t)bkv * Nk * ldkv;
-  const bf16_t* Vb = V + (size_t)bkv * Nk * ldkv;
-  // pass 1: lse
-  float m = -INFINITY, l = 0.f;
-  for (int kt = 0; kt < nkt; ++kt) {
-    __syncthreads();
-    sb_load_tile(ks, Kb, ldkv, kt * SB_T, Nk, h * 64);
-    __syncthreads();
-    float sv[16];
-    float tm = -INFINITY;
+  const int fr = lane & 15, g = lane >> 4;
+  const auto rq = make_rsrc(Q, q_bytes);
+  const auto ro = make_rsrc(O, o_bytes);
+  const auto rdo = make_rsrc(dO, do_bytes);
+  const auto rk = make_rsrc(K, kv_bytes);
+  const auto rv = make_rsrc(V, kv_bytes);
+
+  // Q^T / dO^T B fragments (lane column = query), D = dO . O, lse per query
+  bf16x8 qf[2][2], dof[2][2];
+  float Dq[2], l2[2];
+  const int qbase = qblk * 128 + wid * 32;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      float a = 0.f;
-      for (int d = 0; d < 64; ++d) a += qs[r * SB_T + d] * ks[(c0 + j) * SB_T + d];
-      sv[j] = kt * SB_T + c0 + j < Nk ? a * scale : -INFINITY;
-      tm = fmaxf(tm, sv[j]);
+  for (int qb = 0; qb < 2; ++qb) {
+    const int q = qbase + qb * 16 + fr;
+    float dsum = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int col = h * 64 + kk * 32 + g * 8;
+      qf[qb][kk] = __builtin_bit_cast(bf16x8, buf_load16(rq, q < Nq ? ((b * Nq + q) * ldq + col) * 2 : kOOB));
+      const u32x4 dov = buf_load16(rdo, q < Nq ? ((b * Nq + q) * lddo + col) * 2 : kOOB);
+      const u32x4 ov = buf_load16(ro, q < Nq ? ((b * Nq + q) * ldo + col) * 2 : kOOB);
+      dof[qb][kk] = __builtin_bit_cast(bf16x8, dov);
+      float a[8], c[8];
+      unpack8(dov, a);
+      unpack8(ov, c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dsum += a[e] * c[e];
     }
-    tm = fmaxf(tm, __shfl_xor(tm, 1));
-    tm = fmaxf(tm, __shfl_xor(tm, 2));
-    const float mn = fmaxf(m, tm);
-    float ts = 0.f;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) ts += __expf(sv[j] - mn);
-    ts += __shfl_xor(ts, 1);
-    ts += __shfl_xor(ts, 2);
-    l = l * __expf(m - mn) + ts;
-    m = mn;
+    dsum += __shfl_xor(dsum, 16);
+    dsum += __shfl_xor(dsum, 32);
+    Dq[qb] = dsum;
+    const size_t qi = (size_t)bh * Nq + q;
+    l2[qb] = q < Nq ? lse[qi] : 0.f;
+    if (g == 0 && q < Nq) dvec[qi] = dsum;
   }
-  const float lse = m + __logf(l);
-  // pass 2: dQ
-  float acc[64];
+
+  const int sc = tid & 7, sr = tid >> 3;  // staging: rows sr, sr + 32, 16-B chunk sc
+  u32x4 kreg[2], vreg[2];
+  auto load_kv = [&](int t) {
 #pragma unroll
-  for (int d = 0; d < 64; ++d) acc[d] = 0.f;
-  for (int kt = 0; kt < nkt; ++kt) {
-    __syncthreads();
-    sb_load_tile(ks, Kb, ldkv, kt * SB_T, Nk, h * 64);
-    sb_load_tile(vs, Vb, ldkv, kt * SB_T, Nk, h * 64);
-    __syncthreads();
-#pragma unroll 2
-    for (int j = 0; j < 16; ++j) {
-      const int c = c0 + j;
-      if (kt * SB_T + c >= Nk) continue;
-      float sq = 0.f, dp = 0.f;
-      for (int d = 0; d < 64; ++d) {
-        sq += qs[r * SB_T + d] * ks[c * SB_T + d];
-        dp += os[r * SB_T + d] * vs[c * SB_T + d];
-      }
-      const float p = __expf(sq * scale - lse);
-      const float ds = p * (dp - dr);
-#pragma unroll
-      for (int d = 0; d < 64; ++d) acc[d] += ds * ks[c * SB_T + d];
+    for (int i = 0; i < 2; ++i) {
+      const int key = t * 64 + sr + 32 * i;
+      const int off = key < Nk ? ((bkv * Nk + key) * ldkv + h * 64 + sc * 8) * 2 : kOOB;
+      kreg[i] = buf_load16(rk, off);
+      vreg[i] = buf_load16(rv, off);
     }
-  }
+  };
+  auto store_kv = [&](int buf) {
+    char* Kr = smem + buf * 3 * SB_TILE;
+    char* Kt = Kr + SB_TILE;
+    char* Vr = Kt + SB_TILE;
 #pragma unroll
-  for (int d = 0; d < 64; ++d) {
-    acc[d] += __shfl_xor(acc[d], 1);
-    acc[d] += __shfl_xor(acc[d], 2);
-  }
-  if (q0 + r < Nq) {
-    bf16_t* out = dQ + ((size_t)b * Nq + q0 + r) * lddq + h * 64 + c0;
+    for (int i = 0; i < 2; ++i) {
+      const int row = sr + 32 * i;
+      *reinterpret_cast<u32x4*>(Kr + k_off(row, sc)) = kreg[i];
+      *reinterpret_cast<u32x4*>(Kt + v_off(row, sc)) = kreg[i];
+      *reinterpret_cast<u32x4*>(Vr + k_off(row, sc)) = vreg[i];
+    }
+  };
+
+  f32x4 acc[4][2];  // dQ^T [d-block][q-block]
 #pragma unroll
-    for (int qq = 0; qq < 4; ++qq)  // compile-time register indices (a runtime acc[c0 + d] would go to scratch)
-      if ((t & 3) == qq) {
+  for (int d = 0; d < 4; ++d)
 #pragma unroll
-        for (int d = 0; d < 16; ++d) out[d] = f2bf(acc[qq * 16 + d] * scale);
+    for (int qb = 0; qb < 2; ++qb) acc[d][qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nt = (Nk + 63) / 64;
+  load_kv(0);
+  store_kv(0);
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nt) load_kv(t + 1);
+    const char* Kr = smem + cur * 3 * SB_TILE;
+    const char* Kt = Kr + SB_TILE;
+    const char* Vr = Kt + SB_TILE;
+    f32x4 s[4][2], dp[4][2];  // S^T, dP^T: lane column q, rows key = 16 kt + 4 g + i
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      bf16x8 kf[2], vf[2];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        kf[kk] = *reinterpret_cast<const bf16x8*>(Kr + k_off(kt * 16 + fr, kk * 4 + g));
+        vf[kk] = *reinterpret_cast<const bf16x8*>(Vr + k_off(kt * 16 + fr, kk * 4 + g));
       }
-    if ((t & 3) == 0) {
-      lse_out[(size_t)bh * Nq + q0 + r] = lse;
-      d_out[(size_t)bh * Nq + q0 + r] = dr;
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        f32x4 a{0.f, 0.f, 0.f, 0.f}, c{0.f, 0.f, 0.f, 0.f};
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[0], qf[qb][0], a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[1], qf[qb][1], a, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[0], dof[qb][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[1], dof[qb][1], c, 0, 0, 0);
+        s[kt][qb] = a;
+        dp[kt][qb] = c;
+      }
+    }
+    // dS^T = P^T * (dP^T - D), keys >= Nk masked
+    const bool tail = (t + 1) * 64 > Nk;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool dead = tail && (t * 64 + kt * 16 + g * 4 + i >= Nk);
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+          const float pv = dead ? 0.f : fast_exp2(s[kt][qb][i] * sl2 - l2[qb]);
+          s[kt][qb][i] = pv * (dp[kt][qb][i] - Dq[qb]);
+        }
+      }
+    // dQ^T += K^T dS^T
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      bf16x8 pf[2];
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+        pf[qb] = pack_p8(s[2 * st][qb][0], s[2 * st][qb][1], s[2 * st][qb][2], s[2 * st][qb][3],
+                         s[2 * st + 1][qb][0], s[2 * st + 1][qb][1], s[2 * st + 1][qb][2], s[2 * st + 1][qb][3]);
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const bf16x8 kt_f = tr_frag(Kt, st, db, lane);
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+          acc[db][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt_f, pf[qb], acc[db][qb], 0, 0, 0);
+      }
+    }
+    if (t + 1 < nt) store_kv(cur ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int q = qbase + qb * 16 + fr;
+    if (q >= Nq) continue;
+    bf16_t* row = dQ + (size_t)(b * Nq + q) * lddq + h * 64;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const f32x4 v = acc[db][qb] * scale;
+      *reinterpret_cast<u32x2*>(row + db * 16 + g * 4) = u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
     }
   }
 }
 
-__global__ __launch_bounds__(256) void sa_bwd_dkv_kernel(const bf16_t* __restrict__ Q, int ldq,
-                                                         const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
-                                                         int ldkv, const bf16_t* __restrict__ dO, int lddo,
-                                                         bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int lddkv,
-                                                         int heads, int Nq, int Nk, int kv_div, float scale,
-                                                         const float* __restrict__ lse_in,
-                                                         const float* __restrict__ d_in, float* __restrict__ part) {
-  // part == nullptr: one workgroup per (kv batch, head, key block) loops over the kv_div query batches sharing it.
-  // part != nullptr (shared text K/V, kv_div > 1): one workgroup per (query batch, head, key block) writes its fp32
-  // contribution to part[b][key][2C] and sa_bwd_kv_reduce_kernel sums the kv_div batches (kv_div x more workgroups).
-  extern __shared__ float sbm[];
-  float* ks = sbm;
-  float* vs = ks + SB_T * SB_T;
-  float* qs = vs + SB_T * SB_T;
-  float* os = qs + SB_T * SB_T;
-  const int nkb = (Nk + SB_T - 1) / SB_T;
-  const int kb = blockIdx.x % nkb, bh = blockIdx.x / nkb;
-  const int h = bh % heads;
-  const int bq0 = part ? bh / heads : (bh / heads) * kv_div;  // first query batch handled here
-  const int nbq = part ? 1 : kv_div;
-  const int bkv = bq0 / kv_div;
-  const int t = threadIdx.x, c = t >> 2, i0 = (t & 3) * 16;  // this thread: key row c, queries i0..i0+15 of a tile
-  const int k0 = kb * SB_T;
-  sb_load_tile(ks, K + (size_t)bkv * Nk * ldkv, ldkv, k0, Nk, h * 64);
-  sb_load_tile(vs, V + (size_t)bkv * Nk * ldkv, ldkv, k0, Nk, h * 64);
-  float gk[64], gv[64];
+__global__ __launch_bounds__(256, 2) void sa_bwd_dkv_kernel(
+    const bf16_t* __restrict__ Q, int ldq, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V, int ldkv,
+    const bf16_t* __restrict__ dO, int lddo, const float* __restrict__ lse, const float* __restrict__ dvec,
+    bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int lddkv, int nkv, int heads, int Nq, int Nk, int kv_div,
+    float scale, float sl2, uint32_t q_bytes, uint32_t do_bytes, uint32_t kv_bytes) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BUF = 4 * SB_TILE + 2 * 64 * 4;  // Q row, Q^T, dO row, dO^T, lse2[64], D[64]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nkb = (Nk + 127) / 128;
+  const int wg = xcd_remap(blockIdx.x, nkb * heads * nkv);
+  const int kblk = wg % nkb, bh = wg / nkb;
+  const int h = bh % heads, bkv = bh / heads;
+  const int fr = lane & 15, g = lane >> 4;
+  const auto rq = make_rsrc(Q, q_bytes);
+  const auto rdo = make_rsrc(dO, do_bytes);
+  const auto rk = make_rsrc(K, kv_bytes);
+  const auto rv = make_rsrc(V, kv_bytes);
+
+  // K / V B fragments (lane column = key)
+  bf16x8 kf[2][2], vf[2][2];
+  const int kbase = kblk * 128 + wid * 32;
 #pragma unroll
-  for (int d = 0; d < 64; ++d) { gk[d] = 0.f; gv[d] = 0.f; }
-  const int nqt = (Nq + SB_T - 1) / SB_T;
-  for (int bb = 0; bb < nbq; ++bb) {
-    const int b = bq0 + bb;
-    const int bhq = b * heads + h;
-    for (int qt = 0; qt < nqt; ++qt) {
-      __syncthreads();
-      sb_load_tile(qs, Q + (size_t)b * Nq * ldq, ldq, qt * SB_T, Nq, h * 64);
-      sb_load_tile(os, dO + (size_t)b * Nq * lddo, lddo, qt * SB_T, Nq, h * 64);
-      __syncthreads();
-      if (k0 + c >= Nk) continue;
-#pragma unroll 2
-      for (int j = 0; j < 16; ++j) {
-        const int i = qt * SB_T + i0 + j;
-        if (i >= Nq) continue;
-        const int il = i0 + j;
-        float sq = 0.f, dp = 0.f;
-        for (int d = 0; d < 64; ++d) {
-          sq += qs[il * SB_T + d] * ks[c * SB_T + d];
-          dp += os[il * SB_T + d] * vs[c * SB_T + d];
+  for (int kb = 0; kb < 2; ++kb) {
+    const int key = kbase + kb * 16 + fr;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int off = key < Nk ? ((bkv * Nk + key) * ldkv + h * 64 + kk * 32 + g * 8) * 2 : kOOB;
+      kf[kb][kk] = __builtin_bit_cast(bf16x8, buf_load16(rk, off));
+      vf[kb][kk] = __builtin_bit_cast(bf16x8, buf_load16(rv, off));
+    }
+  }
+
+  const int sc = tid & 7, sr = tid >> 3;
+  const int nqt = (Nq + 63) / 64;
+  const int ntiles = kv_div * nqt;  // (query batch bkv * kv_div + j, query tile)
+  u32x4 qreg[2], oreg[2];
+  float lreg = 0.f, dreg = 0.f;
+  auto load_q = [&](int it) {
+    const int b = bkv * kv_div + it / nqt, q0 = (it % nqt) * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = q0 + sr + 32 * i;
+      qreg[i] = buf_load16(rq, q < Nq ? ((b * Nq + q) * ldq + h * 64 + sc * 8) * 2 : kOOB);
+      oreg[i] = buf_load16(rdo, q < Nq ? ((b * Nq + q) * lddo + h * 64 + sc * 8) * 2 : kOOB);
+    }
+    if (tid < 64) {
+      const int q = q0 + tid;
+      const size_t qi = (size_t)(b * heads + h) * Nq + q;
+      lreg = q < Nq ? lse[qi] : INFINITY;  // padded queries: P = 0
+      dreg = q < Nq ? dvec[qi] : 0.f;
+    }
+  };
+  auto store_q = [&](int buf) {
+    char* Qr = smem + buf * BUF;
+    char* Qt = Qr + SB_TILE;
+    char* Or = Qt + SB_TILE;
+    char* Ot = Or + SB_TILE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = sr + 32 * i;
+      *reinterpret_cast<u32x4*>(Qr + k_off(row, sc)) = qreg[i];
+      *reinterpret_cast<u32x4*>(Qt + v_off(row, sc)) = qreg[i];
+      *reinterpret_cast<u32x4*>(Or + k_off(row, sc)) = oreg[i];
+      *reinterpret_cast<u32x4*>(Ot + v_off(row, sc)) = oreg[i];
+    }
+    if (tid < 64) {
+      float* ls = reinterpret_cast<float*>(Ot + SB_TILE);
+      ls[tid] = lreg;
+      ls[64 + tid] = dreg;
+    }
+  };
+
+  f32x4 dk[4][2], dv[4][2];  // dK^T, dV^T [d-block][key-block]
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      dk[d][kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dv[d][kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+
+  load_q(0);
+  store_q(0);
+  __syncthreads();
+  for (int it = 0; it < ntiles; ++it) {
+    const int cur = it & 1;
+    if (it + 1 < ntiles) load_q(it + 1);
+    const char* Qr = smem + cur * BUF;
+    const char* Qt = Qr + SB_TILE;
+    const char* Or = Qt + SB_TILE;
+    const char* Ot = Or + SB_TILE;
+    const float* ls = reinterpret_cast<const float*>(Ot + SB_TILE);
+    f32x4 s[4][2], dp[4][2];  // S, dP: lane column key, rows q = 16 qt + 4 g + i
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      bf16x8 qa[2], oa[2];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        qa[kk] = *reinterpret_cast<const bf16x8*>(Qr + k_off(qt * 16 + fr, kk * 4 + g));
+        oa[kk] = *reinterpret_cast<const bf16x8*>(Or + k_off(qt * 16 + fr, kk * 4 + g));
+      }
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        f32x4 a{0.f, 0.f, 0.f, 0.f}, c{0.f, 0.f, 0.f, 0.f};
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[0], kf[kb][0], a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[1], kf[kb][1], a, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa[0], vf[kb][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa[1], vf[kb][1], c, 0, 0, 0);
+        s[qt][kb] = a;
+        dp[qt][kb] = c;
+      }
+    }
+    // P into s, dS into dp
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      const f32x4 lq = *reinterpret_cast<const f32x4*>(ls + qt * 16 + g * 4);
+      const f32x4 dq = *reinterpret_cast<const f32x4*>(ls + 64 + qt * 16 + g * 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          const float pv = fast_exp2(s[qt][kb][i] * sl2 - lq[i]);
+          s[qt][kb][i] = pv;
+          dp[qt][kb][i] = pv * (dp[qt][kb][i] - dq[i]);
         }
-        const float p = __expf(sq * scale - lse_in[(size_t)bhq * Nq + i]);
-        const float ds = p * (dp - d_in[(size_t)bhq * Nq + i]);
+    }
+    // dV^T += dO^T P,  dK^T += Q^T dS
 #pragma unroll
-        for (int d = 0; d < 64; ++d) {
-          gv[d] += p * os[il * SB_T + d];
-          gk[d] += ds * qs[il * SB_T + d];
+    for (int st = 0; st < 2; ++st) {
+      bf16x8 pf[2], sf[2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        pf[kb] = pack_p8(s[2 * st][kb][0], s[2 * st][kb][1], s[2 * st][kb][2], s[2 * st][kb][3],
+                         s[2 * st + 1][kb][0], s[2 * st + 1][kb][1], s[2 * st + 1][kb][2], s[2 * st + 1][kb][3]);
+        sf[kb] = pack_p8(dp[2 * st][kb][0], dp[2 * st][kb][1], dp[2 * st][kb][2], dp[2 * st][kb][3],
+                         dp[2 * st + 1][kb][0], dp[2 * st + 1][kb][1], dp[2 * st + 1][kb][2], dp[2 * st + 1][kb][3]);
+      }
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const bf16x8 ot = tr_frag(Ot, st, db, lane);
+        const bf16x8 qtf = tr_frag(Qt, st, db, lane);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          dv[db][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ot, pf[kb], dv[db][kb], 0, 0, 0);
+          dk[db][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qtf, sf[kb], dk[db][kb], 0, 0, 0);
         }
       }
     }
+    if (it + 1 < ntiles) store_q(cur ^ 1);
+    __syncthreads();
   }
 #pragma unroll
-  for (int d = 0; d < 64; ++d) {
-    gk[d] += __shfl_xor(gk[d], 1);
-    gk[d] += __shfl_xor(gk[d], 2);
-    gv[d] += __shfl_xor(gv[d], 1);
-    gv[d] += __shfl_xor(gv[d], 2);
-  }
-  if (k0 + c < Nk && part) {
-    const int dd = (t & 3) * 16;
-    const int C = heads * 64;
-    float* pr = part + ((size_t)bq0 * Nk + k0 + c) * 2 * C + h * 64 + dd;
+  for (int kb = 0; kb < 2; ++kb) {
+    const int key = kbase + kb * 16 + fr;
+    if (key >= Nk) continue;
+    bf16_t* krow = dK + (size_t)(bkv * Nk + key) * lddkv + h * 64;
+    bf16_t* vrow = dV + (size_t)(bkv * Nk + key) * lddkv + h * 64;
 #pragma unroll
-    for (int qq = 0; qq < 4; ++qq)
-      if ((t & 3) == qq) {
-#pragma unroll
-        for (int d = 0; d < 16; ++d) {
-          pr[d] = gk[qq * 16 + d] * scale;
-          pr[C + d] = gv[qq * 16 + d];
-        }
-      }
-  } else if (k0 + c < Nk) {
-    const int dd = (t & 3) * 16;
-    bf16_t* okr = dK + ((size_t)bkv * Nk + k0 + c) * lddkv + h * 64 + dd;
-    bf16_t* ovr = dV + ((size_t)bkv * Nk + k0 + c) * lddkv + h * 64 + dd;
-#pragma unroll
-    for (int qq = 0; qq < 4; ++qq)
-      if ((t & 3) == qq) {
-#pragma unroll
-        for (int d = 0; d < 16; ++d) {
-          okr[d] = f2bf(gk[qq * 16 + d] * scale);
-          ovr[d] = f2bf(gv[qq * 16 + d]);
-        }
-      }
-  }
-}
-
-__global__ __launch_bounds__(256) void sa_bwd_kv_reduce_kernel(const float* __restrict__ part, int nkv, int kv_div,
-                                                               int Nk, int C, bf16_t* __restrict__ dK,
-                                                               bf16_t* __restrict__ dV, int lddkv) {
-  const size_t total = (size_t)nkv * Nk * 2 * C;
-  for (size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (size_t)gridDim.x * 256) {
-    const int col = (int)(idx % (2 * C));
-    const size_t row = idx / (2 * C);  // kv batch * Nk + key
-    const size_t bkv = row / Nk, key = row - bkv * Nk;
-    float a = 0.f;
-    for (int j = 0; j < kv_div; ++j) a += part[(((bkv * kv_div + j) * Nk) + key) * 2 * C + col];
-    bf16_t* dst = col < C ? dK + row * lddkv + col : dV + row * lddkv + (col - C);
-    *dst = f2bf(a);
+    for (int db = 0; db < 4; ++db) {
+      const f32x4 a = dk[db][kb] * scale;
+      const f32x4 c = dv[db][kb];
+      *reinterpret_cast<u32x2*>(krow + db * 16 + g * 4) = u32x2{pack2bf(a[0], a[1]), pack2bf(a[2], a[3])};
+      *reinterpret_cast<u32x2*>(vrow + db * 16 + g * 4) = u32x2{pack2bf(c[0], c[1]), pack2bf(c[2], c[3])};
+    }
   }
 }
 
@@ -686,7 +799,7 @@ using namespace vst;
 
 extern "C" int vst_spatial_attention(const void* q, int ldq, const void* k, const void* v, int ldkv, void* o,
                                      int ldo, int nbatch, int heads, int Nq, int Nk, int kv_div, int head_dim,
-                                     float scale, void* stream) {
+                                     float scale, float* lse, void* stream) {
   if (head_dim != 64 || !q || !k || !v || !o || nbatch <= 0 || heads <= 0 || Nq <= 0 || Nk <= 0 || kv_div <= 0)
     return VST_ERR_ARG;
   if ((ldq & 7) || (ldkv & 7) || (ldo & 7) || nbatch % kv_div) return VST_ERR_ARG;
@@ -697,7 +810,7 @@ extern "C" int vst_spatial_attention(const void* q, int ldq, const void* k, cons
   const uint32_t kvb_v = clampb(((size_t)(nkv * Nk - 1) * ldkv + heads * 64) * 2);
   hipLaunchKernelGGL(spatial_attn_kernel, dim3(nqb * heads * nbatch), dim3(256), SA_LDS, (hipStream_t)stream,
                      (const bf16_t*)q, ldq, (const bf16_t*)k, (const bf16_t*)v, ldkv, (bf16_t*)o, ldo, nbatch, heads,
-                     Nq, Nk, kv_div, scale * 1.4426950408889634f, qb, kvb_v);
+                     Nq, Nk, kv_div, scale * 1.4426950408889634f, qb, kvb_v, lse);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 
@@ -744,39 +857,36 @@ extern "C" int vst_temporal_attention_bwd(const void* q, const void* k, const vo
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 
-// lse + D per query, then (shared text K/V) the per-query-batch fp32 dK/dV partials
+// D = dO . O per query (written by the dQ kernel, read by the dK/dV kernel)
 extern "C" size_t vst_spatial_attention_bwd_workspace_bytes(int nbatch, int heads, int Nq, int Nk) {
-  return ((size_t)2 * nbatch * heads * Nq + (size_t)nbatch * Nk * 2 * heads * 64) * sizeof(float);
+  (void)Nk;
+  return (size_t)nbatch * heads * Nq * sizeof(float);
 }
 
 extern "C" int vst_spatial_attention_bwd(const void* q, int ldq, const void* k, const void* v, int ldkv, const void* o,
-                                         int ldo, const void* dout, int lddo, void* dq, int lddq, void* dk, void* dv,
-                                         int lddkv, int nbatch, int heads, int Nq, int Nk, int kv_div, int head_dim,
-                                         float scale, void* workspace, void* stream) {
-  if (head_dim != 64 || !q || !k || !v || !o || !dout || !dq || !dk || !dv || !workspace || nbatch <= 0 ||
-      heads <= 0 || Nq <= 0 || Nk <= 0 || kv_div <= 0 || nbatch % kv_div)
+                                         int ldo, const void* dout, int lddo, const float* lse, void* dq, int lddq,
+                                         void* dk, void* dv, int lddkv, int nbatch, int heads, int Nq, int Nk,
+                                         int kv_div, int head_dim, float scale, void* workspace, void* stream) {
+  if (head_dim != 64 || !q || !k || !v || !o || !dout || !lse || !dq || !workspace || nbatch <= 0 || heads <= 0 ||
+      Nq <= 0 || Nk <= 0 || kv_div <= 0 || nbatch % kv_div || (!dk) != (!dv))
     return VST_ERR_ARG;
-  if ((ldq & 7) || (ldkv & 7) || (ldo & 7) || (lddo & 7)) return VST_ERR_ARG;
+  if ((ldq & 7) || (ldkv & 7) || (ldo & 7) || (lddo & 7) || (lddq & 3) || (dk && (lddkv & 3))) return VST_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
-  float* lse = (float*)workspace;
-  float* dvec = lse + (size_t)nbatch * heads * Nq;
-  const size_t lds = 4 * SB_T * SB_T * sizeof(float);
-  const int nqb = (Nq + SB_T - 1) / SB_T, nkb = (Nk + SB_T - 1) / SB_T;
-  hipLaunchKernelGGL(sa_bwd_dq_kernel, dim3(nqb * heads * nbatch), dim3(256), lds, s, (const bf16_t*)q, ldq,
-                     (const bf16_t*)k, (const bf16_t*)v, ldkv, (const bf16_t*)o, ldo, (const bf16_t*)dout, lddo,
-                     (bf16_t*)dq, lddq, heads, Nq, Nk, kv_div, scale, lse, dvec);
-  if (kv_div > 1) {
-    float* part = dvec + (size_t)nbatch * heads * Nq;
-    hipLaunchKernelGGL(sa_bwd_dkv_kernel, dim3(nkb * heads * nbatch), dim3(256), lds, s, (const bf16_t*)q, ldq,
-                       (const bf16_t*)k, (const bf16_t*)v, ldkv, (const bf16_t*)dout, lddo, (bf16_t*)dk, (bf16_t*)dv,
-                       lddkv, heads, Nq, Nk, kv_div, scale, lse, dvec, part);
-    const size_t tot = (size_t)(nbatch / kv_div) * Nk * 2 * heads * 64;
-    hipLaunchKernelGGL(sa_bwd_kv_reduce_kernel, dim3((unsigned)std::min<size_t>((tot + 255) / 256, 16384)), dim3(256),
-                       0, s, part, nbatch / kv_div, kv_div, Nk, heads * 64, (bf16_t*)dk, (bf16_t*)dv, lddkv);
-  } else {
-    hipLaunchKernelGGL(sa_bwd_dkv_kernel, dim3(nkb * heads * nbatch), dim3(256), lds, s, (const bf16_t*)q, ldq,
-                       (const bf16_t*)k, (const bf16_t*)v, ldkv, (const bf16_t*)dout, lddo, (bf16_t*)dk, (bf16_t*)dv,
-                       lddkv, heads, Nq, Nk, kv_div, scale, lse, dvec, (float*)nullptr);
+  float* dvec = (float*)workspace;
+  const int nkv = nbatch / kv_div;
+  const float sl2 = scale * 1.4426950408889634f;
+  const uint32_t qb = clampb(((size_t)(nbatch * Nq - 1) * ldq + heads * 64) * 2);
+  const uint32_t ob = clampb(((size_t)(nbatch * Nq - 1) * ldo + heads * 64) * 2);
+  const uint32_t dob = clampb(((size_t)(nbatch * Nq - 1) * lddo + heads * 64) * 2);
+  const uint32_t kvb = clampb(((size_t)(nkv * Nk - 1) * ldkv + heads * 64) * 2);
+  const int nqb = (Nq + 127) / 128, nkb = (Nk + 127) / 128;
+  hipLaunchKernelGGL(sa_bwd_dq_kernel, dim3(nqb * heads * nbatch), dim3(256), 6 * SB_TILE, s, (const bf16_t*)q, ldq,
+                     (const bf16_t*)k, (const bf16_t*)v, ldkv, (const bf16_t*)o, ldo, (const bf16_t*)dout, lddo, lse,
+                     (bf16_t*)dq, lddq, dvec, nbatch, heads, Nq, Nk, kv_div, scale, sl2, qb, ob, dob, kvb);
+  if (dk) {
+    hipLaunchKernelGGL(sa_bwd_dkv_kernel, dim3(nkb * heads * nkv), dim3(256), 2 * (4 * SB_TILE + 512), s,
+                       (const bf16_t*)q, ldq, (const bf16_t*)k, (const bf16_t*)v, ldkv, (const bf16_t*)dout, lddo, lse,
+                       dvec, (bf16_t*)dk, (bf16_t*)dv, lddkv, nkv, heads, Nq, Nk, kv_div, scale, sl2, qb, dob, kvb);
   }
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }

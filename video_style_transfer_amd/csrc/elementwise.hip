@@ -283,8 +283,13 @@ __global__ __launch_bounds__(256) void sumpool2x2_kernel(const bf16_t* __restric
   }
 }
 
-__global__ void step_advance_kernel(int* step) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) *step += 1;
+// The counter wraps at num_steps: a graph replayed past the end of the schedule starts it again instead of
+// indexing sigmas[] / timesteps[] (num_steps + 1 / num_steps entries) out of bounds.
+__global__ void step_advance_kernel(int* step, int num_steps) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const int s = *step + 1;
+    *step = (s >= num_steps || s < 0) ? 0 : s;
+  }
 }
 
 }  // namespace vst
@@ -345,9 +350,9 @@ extern "C" int vst_euler_cfg_step(const void* noise, int ncopy, float guidance, 
   return ok();
 }
 
-extern "C" int vst_step_advance(int* step_idx, void* stream) {
-  if (!step_idx) return VST_ERR_ARG;
-  hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, step_idx);
+extern "C" int vst_step_advance(int* step_idx, int num_steps, void* stream) {
+  if (!step_idx || num_steps <= 0) return VST_ERR_ARG;
+  hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, step_idx, num_steps);
   return ok();
 }
 

@@ -193,8 +193,9 @@ def conv3x3(x1: torch.Tensor, nimg: int, H: int, W: int, w: torch.Tensor, bias: 
     return out
 
 
-def spatial_attention(q, k, v, nbatch, heads, Nq, Nk, kv_div=1, out=None, scale=None):
-    """q: [nbatch*Nq, >=heads*64] view; k/v: [nbatch/kv_div*Nk, >=heads*64] views."""
+def spatial_attention(q, k, v, nbatch, heads, Nq, Nk, kv_div=1, out=None, scale=None, lse=None):
+    """q: [nbatch*Nq, >=heads*64] view; k/v: [nbatch/kv_div*Nk, >=heads*64] views.  lse: optional fp32
+    [nbatch*heads*Nq] output of the log2-domain logsumexp per query (the training backward recomputes P from it)."""
     for n, t in (("q", q), ("k", k), ("v", v)):
         _dev(t, BF16, n)
     if q.shape[0] != nbatch * Nq or k.shape[0] != (nbatch // kv_div) * Nk or v.shape[0] != k.shape[0]:
@@ -204,11 +205,13 @@ def spatial_attention(q, k, v, nbatch, heads, Nq, Nk, kv_div=1, out=None, scale=
     if out is None:
         out = torch.empty((nbatch * Nq, heads * 64), dtype=BF16, device=q.device)
     _dev(out, BF16, "out")
+    if lse is not None and (lse.dtype != F32 or not lse.is_cuda or lse.numel() != nbatch * heads * Nq):
+        raise _lib.VstError("spatial_attention: lse must be fp32 [nbatch*heads*Nq] on device")
     scale = 0.125 if scale is None else scale
     with _Rec("spatial_attention", 4.0 * nbatch * heads * Nq * Nk * 64,
               2.0 * 64 * heads * (2 * nbatch * Nq + 2 * (nbatch // kv_div) * Nk), None, (nbatch * heads, Nq, Nk)):
         _lib.call("vst_spatial_attention", _p(q), _ld(q), _p(k), _p(v), k.stride(0), _p(out), _ld(out), nbatch,
-                  heads, Nq, Nk, kv_div, 64, float(scale), _stream())
+                  heads, Nq, Nk, kv_div, 64, float(scale), _p(lse), _stream())
     return out
 
 
@@ -436,25 +439,33 @@ def geglu_bwd(p, g, out=None):
     return out
 
 
-def spatial_attention_bwd(q, k, v, o, dout, nbatch, heads, Nq, Nk, kv_div=1, scale=None, dq=None, dkv=None):
-    """(dq [nbatch*Nq, heads*64], dk, dv [nbatch/kv_div*Nk, heads*64] as column views of one [.., 2*heads*64])."""
+def spatial_attention_bwd(q, k, v, o, dout, lse, nbatch, heads, Nq, Nk, kv_div=1, scale=None, dq=None, dkv=None,
+                          need_dkv=True):
+    """(dq [nbatch*Nq, heads*64], dk, dv [nbatch/kv_div*Nk, heads*64] as column views of one [.., 2*heads*64], or
+    None, None when need_dkv is False: frozen K/V skip the dK/dV kernel).  lse: the forward's logsumexp output."""
     for n, t in (("q", q), ("k", k), ("v", v), ("o", o), ("dout", dout)):
         _dev(t, BF16, n)
     if k.stride(0) != v.stride(0):
         raise _lib.VstError("spatial_attention_bwd: k and v must share a row stride")
+    if lse.dtype != F32 or not lse.is_cuda or lse.numel() != nbatch * heads * Nq:
+        raise _lib.VstError("spatial_attention_bwd: lse must be the forward's fp32 [nbatch*heads*Nq] logsumexp")
     C = heads * 64
     nkv = nbatch // kv_div
     if dq is None:
         dq = torch.empty((nbatch * Nq, C), dtype=BF16, device=q.device)
-    if dkv is None:
+    if need_dkv and dkv is None:
         dkv = torch.empty((nkv * Nk, 2 * C), dtype=BF16, device=q.device)
     ws = torch.empty((_lib.load().vst_spatial_attention_bwd_workspace_bytes(nbatch, heads, Nq, Nk) + 3) // 4,
                      dtype=F32, device=q.device)
     scale = 0.125 if scale is None else scale
-    with _Rec("spatial_attention_bwd", 10.0 * nbatch * heads * Nq * Nk * 64, 0.0):
+    # MFMA work: dQ pass 3 products (S, dP, dQ), dK/dV pass 4 (S, dP, dV, dK), 2*64 flop per (q, key) each
+    with _Rec("spatial_attention_bwd", (6.0 + (8.0 if need_dkv else 0.0)) * nbatch * heads * Nq * Nk * 64, 0.0):
         _lib.call("vst_spatial_attention_bwd", _p(q), _ld(q), _p(k), _p(v), k.stride(0), _p(o), _ld(o), _p(dout),
-                  _ld(dout), _p(dq), _ld(dq), _p(dkv[:, :C]), _p(dkv[:, C:]), dkv.stride(0), nbatch, heads, Nq, Nk,
+                  _ld(dout), _p(lse), _p(dq), _ld(dq), _p(dkv[:, :C]) if need_dkv else None,
+                  _p(dkv[:, C:]) if need_dkv else None, dkv.stride(0) if need_dkv else 0, nbatch, heads, Nq, Nk,
                   kv_div, 64, float(scale), _p(ws), _stream())
+    if not need_dkv:
+        return dq, None, None
     return dq, dkv[:, :C], dkv[:, C:]
 
 
@@ -514,8 +525,9 @@ def euler_cfg_step(noise, lat, sigmas, step_idx, *, guidance=7.5, ncopy=2):
               _p(step_idx), _stream())
 
 
-def step_advance(step_idx):
-    _lib.call("vst_step_advance", _p(step_idx), _stream())
+def step_advance(step_idx, num_steps):
+    """step_idx <- (step_idx + 1) mod num_steps on the device (a schedule of num_steps steps)."""
+    _lib.call("vst_step_advance", _p(step_idx), int(num_steps), _stream())
 
 
 # ---- ceiling probes (bench.py: measured peaks next to the vendor figures) ----

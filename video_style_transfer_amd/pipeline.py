@@ -87,7 +87,7 @@ class AnimateDiffDenoiser:
         emb = self.unet.embed(self.timesteps, self.pooled, self.time_ids, B, step_idx=self.step_idx)
         noise = self.unet.forward_tokens(self.x, B, self.F, self.h, self.w, emb, self.enc, shard=self.shard)
         K.euler_cfg_step(noise, self.lat, self.sigmas, self.step_idx, guidance=self.guidance, ncopy=self.ncopy)
-        K.step_advance(self.step_idx)
+        K.step_advance(self.step_idx, self.num_steps)
 
     def capture(self):
         """Warm up (fills every derived-weight cache), then capture one step into a HIP graph."""

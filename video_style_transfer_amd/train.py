@@ -130,10 +130,14 @@ class TrainStep:
 
     def __init__(self, unet, optimizer, scheduler, *, reducer: Optional[GradBucketAllReducer] = None,
                  lambda_orth: float = 0.0, spatial_index: Optional[Dict] = None, max_grad_norm: float = 1.0,
-                 p_uncond: float = 0.1, resolution: int = 512, seed: int = 0):
+                 p_uncond: float = 0.1, resolution: int = 512, seed: int = 0, lr_scheduler=None):
+        """`seed` is offset by the process rank: every data-parallel rank draws its own noise, timesteps and
+        unconditional-prompt coin (the reference's per-process RNG streams).  `lr_scheduler` (optional) steps after
+        the optimizer (train_animatediff.py:318)."""
         self.unet = unet
         self.opt = optimizer
         self.sched = scheduler
+        self.lr_scheduler = lr_scheduler
         self.reducer = reducer
         self.lambda_orth = lambda_orth
         self.spatial_index = spatial_index or {}
@@ -141,9 +145,14 @@ class TrainStep:
         self.p_uncond = p_uncond
         self.resolution = resolution
         self.params = [p for p in unet.parameters() if p.requires_grad]
-        self.gen = torch.Generator(device="cpu").manual_seed(seed)
+        rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+        self.gen = torch.Generator(device="cpu").manual_seed(seed + 1000003 * rank)
 
-    def __call__(self, latents: torch.Tensor, prompt, pooled, uncond_prompt=None, uncond_pooled=None) -> Dict:
+    def __call__(self, latents: torch.Tensor, prompt, pooled, uncond_prompt=None, uncond_pooled=None, *,
+                 noise: Optional[torch.Tensor] = None, timesteps: Optional[torch.Tensor] = None,
+                 use_uncond: Optional[bool] = None) -> Dict:
+        """noise / timesteps / use_uncond override the step's random draws (tests compare a data-parallel step
+        with a single-process step on the concatenated batch)."""
         from . import kernels as K
         from .autograd import unet_train_tokens
         from .temporal_lora import compute_orth_loss
@@ -151,11 +160,14 @@ class TrainStep:
         unet = self.unet
         B, Cl, F, h, w = latents.shape
         dev = latents.device
-        noise = torch.randn(latents.shape, generator=self.gen).to(dev)                     # :228
-        t = torch.randint(0, self.sched.num_train_timesteps, (B,), generator=self.gen)    # :229-232
+        draw_noise = torch.randn(latents.shape, generator=self.gen)                         # :228
+        draw_t = torch.randint(0, self.sched.num_train_timesteps, (B,), generator=self.gen)  # :229-232
+        draw_u = float(torch.rand(1, generator=self.gen)) < self.p_uncond                  # :248-254
+        noise = (draw_noise if noise is None else noise).to(dev, torch.float32)
+        t = (draw_t if timesteps is None else timesteps).cpu()
         # add_noise with the clip's timestep on every frame (:233-236); sigma broadcasts over (C, F, h, w)
         noisy = self.sched.add_noise(latents, noise, t.to(dev)).contiguous()
-        use_uncond = uncond_prompt is not None and float(torch.rand(1, generator=self.gen)) < self.p_uncond
+        use_uncond = uncond_prompt is not None and (draw_u if use_uncond is None else use_uncond)
         enc = (uncond_prompt if use_uncond else prompt).to(dev, BF16)
         pool = (uncond_pooled if use_uncond else pooled).to(dev, BF16)
         enc = enc.expand(B, -1, -1).reshape(-1, enc.shape[-1]).contiguous()               # .repeat(B, 1, 1)
@@ -181,5 +193,7 @@ class TrainStep:
             self.reducer.finish()
         gnorm = torch.nn.utils.clip_grad_norm_(self.params, self.max_grad_norm)           # :316
         self.opt.step()                                                                    # :317
+        if self.lr_scheduler is not None:
+            self.lr_scheduler.step()                                                       # :318
         return {"loss": loss.detach(), "loss_mse": loss_mse.detach(), "loss_orth": loss_orth.detach(),
                 "grad_norm": gnorm.detach(), "uncond": use_uncond, "timesteps": t}

@@ -309,12 +309,12 @@ class Upsample2D(nn.Module):
 class DownBlock(nn.Module):
     """DownBlockMotion / CrossAttnDownBlockMotion."""
 
-    def __init__(self, cin, cout, temb, layers, cross, t_layers, heads, cross_dim, add_down, motion_heads):
+    def __init__(self, cin, cout, temb, layers, cross, t_layers, heads, cross_dim, add_down, motion_heads, motion=True):
         super().__init__()
         self.resnets = nn.ModuleList([ResnetBlock2D(cin if j == 0 else cout, cout, temb) for j in range(layers)])
         self.attentions = nn.ModuleList(
             [Transformer2DModel(heads, cout // heads, cout, t_layers, cross_dim) for _ in range(layers)]) if cross else None
-        self.motion_modules = nn.ModuleList([MotionModule(cout, motion_heads) for _ in range(layers)])
+        self.motion_modules = nn.ModuleList([MotionModule(cout, motion_heads) for _ in range(layers)]) if motion else None
         self.downsamplers = nn.ModuleList([Downsample2D(cout)]) if add_down else None
 
     def run(self, x, nimg, H, W, ctx):
@@ -323,7 +323,8 @@ class DownBlock(nn.Module):
             x = res.run(x, nimg, H, W, ctx)
             if self.attentions is not None:
                 x = self.attentions[j].run(x, nimg, H, W, ctx)
-            x = self.motion_modules[j].run(x, nimg, H, W, ctx)
+            if self.motion_modules is not None:
+                x = self.motion_modules[j].run(x, nimg, H, W, ctx)
             outs.append((x, H, W))
         if self.downsamplers is not None:
             x, H, W = self.downsamplers[0].run(x, nimg, H, W)
@@ -334,7 +335,8 @@ class DownBlock(nn.Module):
 class UpBlock(nn.Module):
     """UpBlockMotion / CrossAttnUpBlockMotion."""
 
-    def __init__(self, prev_c, cout, skip_in, temb, layers, cross, t_layers, heads, cross_dim, add_up, motion_heads):
+    def __init__(self, prev_c, cout, skip_in, temb, layers, cross, t_layers, heads, cross_dim, add_up, motion_heads,
+                 motion=True):
         super().__init__()
         n = layers + 1
         self.resnets = nn.ModuleList([
@@ -342,7 +344,7 @@ class UpBlock(nn.Module):
             for j in range(n)])
         self.attentions = nn.ModuleList(
             [Transformer2DModel(heads, cout // heads, cout, t_layers, cross_dim) for _ in range(n)]) if cross else None
-        self.motion_modules = nn.ModuleList([MotionModule(cout, motion_heads) for _ in range(n)])
+        self.motion_modules = nn.ModuleList([MotionModule(cout, motion_heads) for _ in range(n)]) if motion else None
         self.upsamplers = nn.ModuleList([Upsample2D(cout)]) if add_up else None
 
     def run(self, x, nimg, H, W, ctx, skips):
@@ -352,7 +354,8 @@ class UpBlock(nn.Module):
             x = res.run(x, nimg, H, W, ctx, x2=s)  # channel concat [x, skip] read from two sources
             if self.attentions is not None:
                 x = self.attentions[j].run(x, nimg, H, W, ctx)
-            x = self.motion_modules[j].run(x, nimg, H, W, ctx)
+            if self.motion_modules is not None:
+                x = self.motion_modules[j].run(x, nimg, H, W, ctx)
         if self.upsamplers is not None:
             x, H, W = self.upsamplers[0].run(x, nimg, H, W)
         return x, H, W
@@ -408,9 +411,11 @@ class UNetMotionModel(nn.Module):
             in_c, out_c = out_c, ch[i]
             self.down_blocks.append(DownBlock(in_c, out_c, T, cfg.layers_per_block, bt.startswith("CrossAttn"),
                                               cfg.transformer_layers_per_block[i], cfg.num_attention_heads[i],
-                                              cfg.cross_attention_dim, i < len(ch) - 1, cfg.motion_num_attention_heads))
+                                              cfg.cross_attention_dim, i < len(ch) - 1, cfg.motion_num_attention_heads,
+                                              cfg.motion_modules))
         self.mid_block = MidBlock(ch[-1], T, cfg.transformer_layers_per_block[-1], cfg.num_attention_heads[-1],
-                                  cfg.cross_attention_dim, cfg.use_motion_mid_block, cfg.motion_num_attention_heads)
+                                  cfg.cross_attention_dim, cfg.use_motion_mid_block and cfg.motion_modules,
+                                  cfg.motion_num_attention_heads)
         rch = list(reversed(ch))
         rtl = list(reversed(cfg.transformer_layers_per_block))
         rheads = list(reversed(cfg.num_attention_heads))
@@ -421,7 +426,7 @@ class UNetMotionModel(nn.Module):
             skip_in = rch[min(i + 1, len(ch) - 1)]
             self.up_blocks.append(UpBlock(prev_c, out_c, skip_in, T, cfg.layers_per_block, bt.startswith("CrossAttn"),
                                           rtl[i], rheads[i], cfg.cross_attention_dim, i < len(ch) - 1,
-                                          cfg.motion_num_attention_heads))
+                                          cfg.motion_num_attention_heads, cfg.motion_modules))
         self.conv_norm_out = GroupNorm(cfg.norm_num_groups, ch[0], eps=cfg.norm_eps)
         self.conv_out = Conv3x3(ch[0], cfg.out_channels)
 

@@ -118,14 +118,15 @@ def param_shapes(cfg: UNetMotionConfig, lora_rank: int | None = 8) -> "OrderedDi
             if bt.startswith("CrossAttn"):
                 _transformer2d(S, f"down_blocks.{i}.attentions.{j}", out_c, cfg.transformer_layers_per_block[i],
                                cfg.cross_attention_dim, lora_rank)
-            _motion(S, f"down_blocks.{i}.motion_modules.{j}", out_c)
+            if cfg.motion_modules:
+                _motion(S, f"down_blocks.{i}.motion_modules.{j}", out_c)
         if i < len(ch) - 1:
             _conv(S, f"down_blocks.{i}.downsamplers.0.conv", out_c, out_c)
     C = ch[-1]
     _resnet(S, "mid_block.resnets.0", C, C, T)
     _transformer2d(S, "mid_block.attentions.0", C, cfg.transformer_layers_per_block[-1], cfg.cross_attention_dim,
                    lora_rank)
-    if cfg.use_motion_mid_block:
+    if cfg.use_motion_mid_block and cfg.motion_modules:
         _motion(S, "mid_block.motion_modules.0", C)
     _resnet(S, "mid_block.resnets.1", C, C, T)
     rch = list(reversed(ch))
@@ -141,7 +142,8 @@ def param_shapes(cfg: UNetMotionConfig, lora_rank: int | None = 8) -> "OrderedDi
             _resnet(S, f"up_blocks.{i}.resnets.{j}", rin + skip, out_c, T)
             if bt.startswith("CrossAttn"):
                 _transformer2d(S, f"up_blocks.{i}.attentions.{j}", out_c, rtl[i], cfg.cross_attention_dim, lora_rank)
-            _motion(S, f"up_blocks.{i}.motion_modules.{j}", out_c)
+            if cfg.motion_modules:
+                _motion(S, f"up_blocks.{i}.motion_modules.{j}", out_c)
         if i < len(ch) - 1:
             _conv(S, f"up_blocks.{i}.upsamplers.0.conv", out_c, out_c)
     _norm(S, "conv_norm_out", ch[0])
