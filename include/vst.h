@@ -132,8 +132,9 @@ int vst_transpose(const void* x, int ldx, int rows, int cols, void* y, int ldy, 
 
 /* Training path (torch.autograd of train_animatediff.py:265-319 in the reference).
  * vst_layernorm_bwd: dx and (dgamma, dbeta) of BasicTransformerBlock LayerNorm (x, g = dL/dy: rows x C bf16), stats
- * recomputed; workspace of vst_layernorm_bwd_workspace_bytes(C, rows).  vst_geglu_bwd: dp of the GEGLU projection output
- * p (32-interleaved [h | gate] blocks, as the fused GEMM stores them) from g = dL/d(h * gelu(gate)) (M x Nh). */
+ * recomputed; workspace of vst_layernorm_bwd_workspace_bytes(C, rows); dgamma = dbeta = NULL (frozen affine):
+ * dx only, no workspace.  vst_geglu_bwd: dp of the GEGLU projection output p (32-interleaved [h | gate] blocks,
+ * as the fused GEMM stores them) from g = dL/d(h * gelu(gate)) (M x Nh). */
 size_t vst_layernorm_bwd_workspace_bytes(int C, int rows);
 int vst_layernorm_bwd(const void* x, int ldx, const void* g, int ldg, int C, int rows, const float* gamma, float eps,
                       void* dx, int lddx, float* dgamma, float* dbeta, void* workspace, void* stream);

@@ -122,3 +122,68 @@ def test_insert_unziplora_from_stage1_files(tmp_path):
             assert torch.equal(d["style_up"].weight, style[f"unet.unet.{attn_name}.{part}.lora.up.weight"])
             assert torch.equal(layer.merge_content.detach(), mc[f"unet.{attn_name}.{part}.lora.merge_content"])
             assert torch.equal(layer.merge_style.detach(), ms[f"unet.{attn_name}.{part}.lora.merge_style"])
+
+
+# ---------------------------------------------------------------------------- pinned to the reference's own output
+class _GoldAttn(torch.nn.Module):
+    """The module tree tests/golden/make_golden.py gave the reference's temporal_lora.py (duck-typed attention with
+    to_q/to_k/to_v/to_out), rebuilt from this package's classes."""
+
+    def __init__(self, C, with_lora):
+        super().__init__()
+        from video_style_transfer_amd.lora_linear import LoRACompatibleLinear
+        L = LoRACompatibleLinear if with_lora else torch.nn.Linear
+        self.to_q = L(C, C, bias=False)
+        self.to_k = L(C, C, bias=False)
+        self.to_v = L(C, C, bias=False)
+        self.to_out = torch.nn.ModuleList([L(C, C, bias=True), torch.nn.Dropout(0.0)])
+
+
+class _GoldTr(torch.nn.Module):
+    def __init__(self, C, with_lora):
+        super().__init__()
+        blk = torch.nn.Module()
+        blk.attn1, blk.attn2 = _GoldAttn(C, with_lora), _GoldAttn(C, with_lora)
+        self.transformer_blocks = torch.nn.ModuleList([blk])
+
+
+def test_temporal_lora_formats_match_reference_golden(tmp_path):
+    """inject_temporal_lora / build_spatial_lora_index / compute_orth_loss / get_merged_motion_state_dict /
+    save_checkpoint against the reference's own outputs on the same tree and weights (tests/golden/temporal_lora,
+    produced by animatediff/temporal_lora.py:44-192): same wrapped-layer count, same orth-loss pairs and value, the
+    merged motion_modules state dict with exactly the reference's key set and values (what the reference writes to
+    checkpoint-{step}/motion_modules.pth, animatediff/utils.py:102-144)."""
+    from safetensors import safe_open
+    from safetensors.torch import load_file
+    from video_style_transfer_amd.temporal_lora import (build_spatial_lora_index, compute_orth_loss,
+                                                        get_merged_motion_state_dict, inject_temporal_lora)
+    from video_style_transfer_amd.unziplora_linear_layer import UnZipLoRALinearLayerInfer
+    path = os.path.join(os.path.dirname(__file__), "golden", "temporal_lora.safetensors")
+    T = load_file(path)
+    with safe_open(path, "pt") as f:
+        meta = json.loads(f.metadata()["meta"])
+    C = meta["C"]
+    u = torch.nn.Module()
+    down = torch.nn.Module()
+    down.attentions = torch.nn.ModuleList([_GoldTr(C, True), _GoldTr(C, True)])
+    down.motion_modules = torch.nn.ModuleList([_GoldTr(C, False), _GoldTr(C, False)])
+    u.down_blocks = torch.nn.ModuleList([down])
+    for n, m in u.named_modules():
+        if hasattr(m, "set_lora_layer"):
+            m.set_lora_layer(UnZipLoRALinearLayerInfer(m.in_features, m.out_features, 8, ["content", "style"]))
+    assert inject_temporal_lora(u, rank=meta["rank"], alpha=meta["alpha"]) == meta["n_wrapped"]
+    sd = {k[3:]: v for k, v in T.items() if k.startswith("sd.")}
+    u.load_state_dict(sd, strict=True)  # the reference's parameter names load as they are
+    idx = build_spatial_lora_index(u)
+    assert sorted(idx) == sorted(meta["index"])
+    orth = compute_orth_loss(u, idx, meta["lambda"])
+    assert torch.allclose(orth.detach(), T["orth_loss"][0], rtol=1e-4), (orth, T["orth_loss"])
+    merged = get_merged_motion_state_dict(u)
+    gold_keys = meta["merged_keys"]
+    assert sorted(merged) == sorted(gold_keys)
+    for k in gold_keys:
+        assert torch.allclose(merged[k].float(), T["merged_sd." + k].float(), rtol=1e-5, atol=1e-7), k
+    save_checkpoint(u, str(tmp_path), 7)
+    saved = torch.load(os.path.join(tmp_path, "checkpoint-7", "motion_modules.pth"), map_location="cpu",
+                       weights_only=True)
+    assert sorted(saved) == sorted(gold_keys)

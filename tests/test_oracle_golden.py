@@ -141,3 +141,35 @@ def test_temporal_lora_fwd_delta_orth():
         pairs.append((dt, sd[pre + "content_down.weight"], sd[pre + "content_up.weight"],
                       sd[pre + "style_down.weight"], sd[pre + "style_up.weight"]))
     close(R.orth_loss(pairs, meta["lambda"]).reshape(1), T["orth_loss"], 1e-4)
+
+
+@pytest.mark.parametrize("motion,ft", [(True, "both"), (True, "content"), (False, "both")])
+def test_bf16_emulation_oracle_is_the_fp32_oracle_without_rounding(monkeypatch, motion, ft):
+    """oracle/unet_bf16.py restates oracle/unet.py op for op and only adds bf16 rounding points: with the rounding
+    replaced by the identity the two agree to fp32 reassociation (tiny config, UnZipLoRA r=8, 3 denoise steps)."""
+    from oracle import unet as O
+    from oracle import unet_bf16 as E
+    from video_style_transfer_amd.config import UNetMotionConfig
+    from video_style_transfer_amd.weights import synthetic_state_dict
+    cfg = UNetMotionConfig.tiny()
+    cfg.motion_modules = motion
+    sd = synthetic_state_dict(cfg, 0, 8)
+    g = torch.Generator().manual_seed(1)
+    B, Fr, hw = 2, (4 if motion else 1), 16
+    lat = torch.randn(B, 4, Fr, hw, hw, generator=g)
+    enc = torch.randn(B, 77, cfg.cross_attention_dim, generator=g)
+    pooled = torch.randn(B, cfg.text_embed_dim, generator=g)
+    tids = torch.tensor([[128, 128, 0, 0, 128, 128]] * B, dtype=torch.float32)
+    t = torch.tensor([501.0, 501.0])
+    L = O.LoRAState(ft)
+    ref = O.unet_forward(sd, cfg.to_dict(), lat, t, enc, pooled, tids, L)
+    emu_bf = E.unet_forward(sd, cfg.to_dict(), lat, t, enc, pooled, tids, L)
+    monkeypatch.setattr(E, "q", lambda x: x)
+    out = E.unet_forward(sd, cfg.to_dict(), lat, t, enc, pooled, tids, L)
+    assert ((out - ref).norm() / ref.norm()).item() < 1e-5
+    assert 1e-3 < ((emu_bf - ref).norm() / ref.norm()).item() < 5e-2  # the rounding points are live
+    if motion and ft == "both":
+        lat0 = lat[:1] * 14.6
+        a = E.denoise(sd, cfg.to_dict(), lat0, (enc[1:2], pooled[1:2]), (enc[:1], pooled[:1]), tids[:1], 50, 7.5, steps=3)
+        b = O.denoise(sd, cfg.to_dict(), lat0, (enc[1:2], pooled[1:2]), (enc[:1], pooled[:1]), tids[:1], 50, 7.5, steps=3)
+        assert ((a - b).norm() / b.norm()).item() < 1e-5

@@ -129,8 +129,12 @@ def test_geglu_fn_grads(cuda, M, C, Nh):
     xr, Wr, br = xb.float().requires_grad_(True), W.float().requires_grad_(True), b.clone().requires_grad_(True)
     h, gate = (xr @ Wr.t() + br).chunk(2, dim=-1)
     (h * torch.nn.functional.gelu(gate)).backward(gy.float())
-    x, Wd, bd = xb.to(cuda).requires_grad_(True), W.to(cuda).requires_grad_(True), b.to(cuda).requires_grad_(True)
-    y = GEGLUFn.apply(x, Wd, bd)
+    from video_style_transfer_amd.unet_motion import GEGLU
+    mod = GEGLU(C, Nh).to(cuda)
+    mod.proj.weight = torch.nn.Parameter(W.to(cuda))          # bf16 weight, fp32 bias (as the motion FF trains)
+    mod.proj.bias = torch.nn.Parameter(b.to(cuda))
+    x, Wd, bd = xb.to(cuda).requires_grad_(True), mod.proj.weight, mod.proj.bias
+    y = GEGLUFn.apply(x, Wd, bd, mod)
     y.backward(gy.to(cuda))
     hr, gr = (xb.float() @ W.float().t() + b).chunk(2, dim=-1)
     for name, got, ref in (("y", y, hr * torch.nn.functional.gelu(gr)), ("dX", x.grad, xr.grad),

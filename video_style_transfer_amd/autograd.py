@@ -25,9 +25,8 @@ BF16 = torch.bfloat16
 
 
 def _wt(W: torch.Tensor) -> torch.Tensor:
-    """W^T (bf16, [in, out]); cached on the parameter while it is not being trained."""
-    if W.requires_grad:
-        return K.transpose(W.detach().to(BF16).contiguous())
+    """W^T (bf16, [in, out]), cached on the parameter per version: frozen weights transpose once, trained ones once
+    per optimizer step."""
     key = (W.data_ptr(), W._version)
     c = W.__dict__.get("_vst_wt")
     if c is None or c[0] != key:
@@ -46,78 +45,168 @@ def _transpose_padded(t: torch.Tensor, Mp: int) -> torch.Tensor:
     return out
 
 
+class _AugOperands:
+    """Persistent augmented operands of a LoRA projection whose base W is frozen: W_aug = [W | s B] ([N, K + P]) and
+    WT_aug = [W^T | s A^T] ([K, N + P]) hold W / W^T from construction; each call rewrites only the r LoRA columns
+    (A and B train), instead of rebuilding the whole augmented matrices."""
+
+    def __init__(self, W: torch.Tensor, P: int):
+        N, K1 = W.shape
+        dev = W.device
+        self.P = P
+        self.W_aug = torch.zeros(N, K1 + P, device=dev, dtype=BF16)
+        self.W_aug[:, :K1] = W.detach().to(BF16)
+        self.WT_aug = torch.zeros(K1, N + P, device=dev, dtype=BF16)
+        K.transpose(self.W_aug[:, :K1], out=self.WT_aug[:, :N])
+        self.A_pad = torch.zeros(P, K1, device=dev, dtype=BF16)
+        self.BT = torch.zeros(P, N, device=dev, dtype=BF16)
+
+
+def _aug_operands(owner, W: torch.Tensor, P: int) -> _AugOperands:
+    key = (W.data_ptr(), W._version, tuple(W.shape), P)
+    c = owner.__dict__.get("_vst_aug")
+    if c is None or c[0] != key:
+        c = (key, _AugOperands(W, P))
+        owner.__dict__["_vst_aug"] = c
+    return c[1]
+
+
 class LoRALinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x2d, W, b, A, B, s: float):
+    def forward(ctx, x2d, W, b, A, B, s: float, owner=None):
+        """owner: a module to hold the persistent augmented operands of a frozen W (None: rebuilt per call)."""
         if x2d.shape[1] % 64 or W.shape[0] % 64:
             raise ValueError("LoRALinearFn: in/out features must be multiples of 64 (two-source GEMM K split)")
         r = A.shape[0]
-        P = pad32(max(r, 1))  # r = 0: a plain trainable linear (u stays zero)
-        dev = x2d.device
+        P = pad32(max(r, 1))
         x2d = x2d.to(BF16).contiguous()
-        Wb = W.detach().to(BF16)
-        A_pad = torch.zeros(P, A.shape[1], device=dev, dtype=BF16)
-        A_pad[:r] = A.detach().to(BF16)
-        W_aug = torch.zeros(W.shape[0], W.shape[1] + P, device=dev, dtype=BF16)
-        W_aug[:, :W.shape[1]] = Wb
-        W_aug[:, W.shape[1]:W.shape[1] + r] = (B.detach().float() * s).to(BF16)
+        N, K1 = W.shape
+        if owner is not None and not W.requires_grad:
+            aug = _aug_operands(owner, W, P)
+        else:
+            aug = _AugOperands(W, P)
+        aug.A_pad[:r] = A.detach().to(BF16)
+        aug.W_aug[:, K1:K1 + r] = (B.detach().float() * s).to(BF16)
+        aug.WT_aug[:, N:N + r] = (A.detach().float().t() * s).to(BF16)
+        aug.BT[:r] = B.detach().t().to(BF16)
         bias = None if b is None else b.detach().float().contiguous()
-        u = K.linear(x2d, A_pad, kind="gemm_lora_down", alg_n=r)
-        y = K.linear(x2d, W_aug, bias, x2=u, alg_k2=r)
-        ctx.save_for_backward(x2d, W, A, B, u, A_pad)
+        u = K.linear(x2d, aug.A_pad, kind="gemm_lora_down", alg_n=r)
+        y = K.linear(x2d, aug.W_aug, bias, x2=u, alg_k2=r)
+        ctx.save_for_backward(x2d, W, A, B, u)
+        ctx.aug = aug
         ctx.s = s
         ctx.b_dtype = None if b is None else b.dtype
         return y
 
     @staticmethod
     def backward(ctx, g):
-        x2d, W, A, B, u, A_pad = ctx.saved_tensors
+        x2d, W, A, B, u = ctx.saved_tensors
+        aug = ctx.aug
         s = ctx.s
         g = g.to(BF16).contiguous()
         M, N = g.shape
         r = A.shape[0]
-        P = pad32(max(r, 1))
         dev = g.device
-        BT = torch.zeros(P, N, device=dev, dtype=BF16)
-        BT[:r] = B.detach().t().to(BF16)
-        v = K.linear(g, BT, kind="gemm_lora_down", alg_n=r)                    # [M, P] = g B
+        v = K.linear(g, aug.BT, kind="gemm_lora_down", alg_n=r)                # [M, P] = g B
         need_x, need_w, need_b, need_a, need_bb = ctx.needs_input_grad[:5]
         dX = dW = db = dA = dB = None
         if need_x:
-            WT = _wt(W)                                                          # [in, N]
-            WT_aug = torch.zeros(WT.shape[0], N + P, device=dev, dtype=BF16)
-            WT_aug[:, :N] = WT
-            WT_aug[:, N:] = (A_pad.float().t() * s).to(BF16)
-            dX = K.linear(g, WT_aug, x2=v, alg_k2=r)                             # [M, in]
+            dX = K.linear(g, aug.WT_aug, x2=v, alg_k2=r)                         # [M, in]
         if need_w or need_b or need_a or need_bb:
             # the weight-side GEMMs contract over the token axis: pad it to the GEMM's K granule (8) with zeros
             Mp = (M + 7) // 8 * 8
-            gT = _transpose_padded(g, Mp)                                        # [N, Mp]
             if need_w or need_a:
                 xT = _transpose_padded(x2d, Mp)                                  # [in, Mp]
             if need_w:
-                dW = K.linear(gT, xT).to(W.dtype)                                # [N, in] = g^T x
+                dW = K.linear(_transpose_padded(g, Mp), xT).to(W.dtype)          # [N, in] = g^T x
             if need_a:
                 vT = _transpose_padded(v, Mp)                                    # [P, Mp]
                 dA = (K.linear(vT, xT)[:r].float() * s).to(A.dtype)             # [r, in] = s v^T x
-            if need_bb or need_b:
-                P1 = pad32(r + 1)
-                U1 = torch.zeros(P1, Mp, device=dev, dtype=BF16)
-                if r:
-                    K.transpose(u[:, :r], out=U1[:r, :M])                        # u^T
-                U1[r, :M].fill_(1.0)                                             # ones row -> db
-                gu = K.linear(gT, U1)                                            # [N, P1]
-                if need_bb:
-                    dB = (gu[:, :r].float() * s).to(B.dtype)                     # [N, r] = s g^T u
-                if need_b:
-                    db = gu[:, r].float().to(ctx.b_dtype)
-        return dX, dW, db, dA, dB, None
+            if need_bb:
+                uT = _transpose_padded(u, Mp)                                    # [P, Mp]
+                dB = (K.linear(_transpose_padded(g, Mp), uT)[:, :r].float() * s).to(B.dtype)  # [N, r] = s g^T u
+            if need_b:
+                db = g.float().sum(0).to(ctx.b_dtype)
+        return dX, dW, db, dA, dB, None, None
 
 
-def lora_linear(x, W, b, A, B, s: float):
-    """y[..., out] = x W^T + b + s (x A^T) B^T with the HIP forward/backward (any leading shape)."""
+class PlainLinearFn(torch.autograd.Function):
+    """A trainable linear without LoRA (motion-module proj_in / proj_out / ff.net.2, animatediff/utils.py:79-85):
+    y = x W^T + b; dX = g W (W^T cached per optimizer step), dW = g^T x, db = g^T 1."""
+
+    @staticmethod
+    def forward(ctx, x2d, W, b):
+        from .unet_motion import f32
+        x2d = x2d.to(BF16).contiguous()
+        y = K.linear(x2d, W.detach().to(BF16).contiguous(), None if b is None else f32(b))
+        ctx.save_for_backward(x2d, W)
+        ctx.b_dtype = None if b is None else b.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x2d, W = ctx.saved_tensors
+        g = g.to(BF16).contiguous()
+        M = g.shape[0]
+        need_x, need_w, need_b = ctx.needs_input_grad[:3]
+        dX = dW = db = None
+        if need_x:
+            dX = K.linear(g, _wt(W))
+        if need_w:
+            Mp = (M + 7) // 8 * 8
+            dW = K.linear(_transpose_padded(g, Mp), _transpose_padded(x2d, Mp)).to(W.dtype)
+        if need_b:
+            db = g.float().sum(0).to(ctx.b_dtype)
+        return dX, dW, db
+
+
+def _frozen_bwd_operands(ops):
+    """(W_aug^T = [W^T | A^T] [K1, N + P] or W^T, V^T [P, N] or None) of a frozen projection's inference operands
+    (lora_linear.ProjOps), cached on the ops object (which is itself rebuilt when a parameter version changes)."""
+    c = ops.__dict__.get("_vst_bwd")
+    if c is None:
+        K1, N = ops.k1, ops.n
+        W = ops.w[:, :K1]
+        if ops.a is None:
+            c = (K.transpose(W), None)
+        else:
+            P = ops.a.shape[0]
+            wt = torch.empty(K1, N + P, device=W.device, dtype=BF16)
+            K.transpose(W, out=wt[:, :N])
+            K.transpose(ops.a, out=wt[:, N:])
+            c = (wt, K.transpose(ops.w[:, K1:K1 + P]))
+        ops.__dict__["_vst_bwd"] = c
+    return c
+
+
+class FrozenProjFn(torch.autograd.Function):
+    """Projections whose parameters are all frozen (the Stage-2 spatial path with its UnZipLoRA layers, frozen conv
+    shortcuts): forward = the inference operands ([x | x A^T] . [W | V]^T + b, lora_linear.build_ops, cached per
+    parameter version), backward = dX = [g | g V] . [W^T | A^T]^T only, on cached transposed operands."""
+
+    @staticmethod
+    def forward(ctx, x2d, ops):
+        from .lora_linear import run_ops
+        x2d = x2d.to(BF16).contiguous()
+        ctx.ops = ops
+        return run_ops(x2d, ops)
+
+    @staticmethod
+    def backward(ctx, g):
+        ops = ctx.ops
+        g = g.to(BF16).contiguous()
+        wt, vt = _frozen_bwd_operands(ops)
+        if vt is None:
+            return K.linear(g, wt), None
+        v = K.linear(g, vt, kind="gemm_lora_down", alg_n=ops.r)
+        return K.linear(g, wt, x2=v, alg_k2=ops.r), None
+
+
+def lora_linear(x, W, b, A, B, s: float, owner=None):
+    """y[..., out] = x W^T + b + s (x A^T) B^T with the HIP forward/backward (any leading shape); `owner` keeps the
+    augmented operands of a frozen W across calls."""
     x2 = x.reshape(-1, x.shape[-1])
-    y = LoRALinearFn.apply(x2, W, b, A, B, s)
+    y = LoRALinearFn.apply(x2, W, b, A, B, s, owner)
     return y.view(x.shape[:-1] + (W.shape[0],))
 
 
@@ -140,7 +229,11 @@ class LayerNormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         x2d, gamma = ctx.saved_tensors
-        dx, dgam, dbet = K.layer_norm_bwd(x2d, g.to(BF16).contiguous(), gamma.detach().float().contiguous(), ctx.eps)
+        affine = bool(ctx.needs_input_grad[1] or ctx.needs_input_grad[2])  # frozen spatial norms: dx only
+        dx, dgam, dbet = K.layer_norm_bwd(x2d, g.to(BF16).contiguous(), gamma.detach().float().contiguous(), ctx.eps,
+                                          need_affine=affine)
+        if not affine:
+            return dx, None, None, None, None, None, None
         return dx, dgam.to(gamma.dtype), dbet.to(ctx.beta_dtype), None, None, None, None
 
 
@@ -155,43 +248,52 @@ def _deinterleave32(t: torch.Tensor) -> torch.Tensor:
     return t.reshape(two_nh // 64, 2, 32, *t.shape[1:]).transpose(0, 1).reshape(t.shape)
 
 
+def _geglu_wt(geglu):
+    """(interleaved GEGLU weight)^T, cached on the module per weight version."""
+    w = geglu.proj.weight
+    key = (w.data_ptr(), w._version)
+    c = geglu.__dict__.get("_vst_geglu_wt")
+    if c is None or c[0] != key:
+        c = (key, K.transpose(geglu.geglu_ops()[0]))
+        geglu.__dict__["_vst_geglu_wt"] = c
+    return c[1]
+
+
 class GEGLUFn(torch.autograd.Function):
     """diffusers GEGLU (proj = Linear(C, 2 Nh); out = h * gelu(gate)) of the motion / spatial FF: forward is the
-    fused GEGLU GEMM; backward recomputes p = x W^T + b, then vst_geglu_bwd -> dp, dX = dp W, dW = dp^T x,
-    db = dp^T 1, all in the 32-interleaved column order (de-interleaved for the parameters)."""
+    fused GEGLU GEMM on the module's interleaved operands (unet_motion.GEGLU.geglu_ops, cached per weight version);
+    backward recomputes p = x W^T + b, then vst_geglu_bwd -> dp, dX = dp W (cached W^T), dW = dp^T x, db = dp^T 1,
+    in the 32-interleaved column order (de-interleaved for the parameters)."""
 
     @staticmethod
-    def forward(ctx, x2d, W, b):
+    def forward(ctx, x2d, W, b, geglu):
         if W.shape[0] % 64 or x2d.shape[1] % 8:
             raise ValueError("GEGLUFn: 2*Nh must be a multiple of 64")
         x2d = x2d.to(BF16).contiguous()
-        Wi = _interleave32(W.detach().to(BF16)).contiguous()
-        bi = _interleave32(b.detach().float()).contiguous()
+        Wi, bi = geglu.geglu_ops()
         y = K.linear(x2d, Wi, bi, geglu=True)
-        ctx.save_for_backward(x2d, Wi, bi)
+        ctx.save_for_backward(x2d)
+        ctx.geglu = geglu
         ctx.w_dtype, ctx.b_dtype = W.dtype, b.dtype
         return y
 
     @staticmethod
     def backward(ctx, g):
-        x2d, Wi, bi = ctx.saved_tensors
+        (x2d,) = ctx.saved_tensors
+        Wi, bi = ctx.geglu.geglu_ops()
         M = x2d.shape[0]
         p = K.linear(x2d, Wi, bi)                                              # [M, 2Nh] pre-activation
         dp = K.geglu_bwd(p, g.to(BF16).contiguous())
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
         dX = dW = db = None
         if need_x:
-            dX = K.linear(dp, K.transpose(Wi))                                  # [M, C] = dp W
-        if need_w or need_b:
+            dX = K.linear(dp, _geglu_wt(ctx.geglu))                            # [M, C] = dp W
+        if need_w:
             Mp = (M + 7) // 8 * 8
-            dpT = _transpose_padded(dp, Mp)                                    # [2Nh, Mp]
-            if need_w:
-                dW = _deinterleave32(K.linear(dpT, _transpose_padded(x2d, Mp))).to(ctx.w_dtype)
-            if need_b:
-                ones = torch.zeros(32, Mp, device=dp.device, dtype=BF16)
-                ones[0, :M].fill_(1.0)
-                db = _deinterleave32(K.linear(dpT, ones)[:, 0].float()).to(ctx.b_dtype)
-        return dX, dW, db
+            dW = _deinterleave32(K.linear(_transpose_padded(dp, Mp), _transpose_padded(x2d, Mp))).to(ctx.w_dtype)
+        if need_b:
+            db = _deinterleave32(dp.float().sum(0)).to(ctx.b_dtype)
+        return dX, dW, db, None
 
 
 class TemporalAttentionFn(torch.autograd.Function):
@@ -288,7 +390,17 @@ def _proj_parts(lins, scale: float = 1.0):
         else:
             As.append(base.weight.new_zeros(0, base.in_features, dtype=torch.float32))
             Bs.append(base.weight.new_zeros(base.out_features, 0, dtype=torch.float32))
-    W = Ws[0] if len(Ws) == 1 else torch.cat(Ws, 0)
+    if len(Ws) == 1:
+        W = Ws[0]
+    elif any(w.requires_grad for w in Ws):
+        W = torch.cat(Ws, 0)
+    else:  # frozen bases (temporal LoRA q/k/v): concatenate once per weight version
+        key = tuple((w.data_ptr(), w._version) for w in Ws)
+        c = lins[0].__dict__.get("_vst_wcat")
+        if c is None or c[0] != key:
+            c = (key, torch.cat([w.detach() for w in Ws], 0))
+            lins[0].__dict__["_vst_wcat"] = c
+        W = c[1]
     b = None
     if any(x is not None for x in bs):
         b = torch.cat([x.float() if x is not None else torch.zeros(w.shape[0], device=w.device) for w, x in zip(Ws, bs)])
@@ -298,8 +410,17 @@ def _proj_parts(lins, scale: float = 1.0):
 
 
 def proj_train(lins, x2d, scale: float = 1.0):
+    """Projections sharing the input x2d on the training path: all frozen -> FrozenProjFn (inference operands, dX
+    only); one plain trainable linear -> PlainLinearFn; otherwise (temporal LoRA, trainable mergers) LoRALinearFn
+    over the concatenated parameters, with the frozen base's augmented operands kept on lins[0]."""
+    from .lora_linear import build_ops
+    from .temporal_lora import TemporalLoRALinear
+    if not any(p.requires_grad for lin in lins for p in lin.parameters()):
+        return FrozenProjFn.apply(x2d, build_ops(lins, scale))
+    if len(lins) == 1 and not isinstance(lins[0], TemporalLoRALinear) and getattr(lins[0], "lora_layer", None) is None:
+        return PlainLinearFn.apply(x2d, lins[0].weight, lins[0].bias)
     W, b, A, B = _proj_parts(lins, scale)
-    return LoRALinearFn.apply(x2d, W, b, A, B, 1.0)
+    return LoRALinearFn.apply(x2d, W, b, A, B, 1.0, lins[0])
 
 
 def transformer2d_train(t2d, x2d, nimg: int, H: int, W: int, enc=None, frames_per_text: int = 1, scale: float = 1.0):
@@ -329,7 +450,7 @@ def transformer2d_train(t2d, x2d, nimg: int, H: int, W: int, enc=None, frames_pe
         o = SpatialAttentionFn.apply(q, kv[:, :inner], kv[:, inner:], nimg, a2.heads, HW, L, frames_per_text)
         h = AddFn.apply(h, proj_train([a2.to_out[0]], o, scale))
         n = LayerNormFn.apply(h, blk.norm3.weight, blk.norm3.bias, blk.norm3.eps)
-        f = GEGLUFn.apply(n, blk.ff.net[0].proj.weight, blk.ff.net[0].proj.bias)
+        f = GEGLUFn.apply(n, blk.ff.net[0].proj.weight, blk.ff.net[0].proj.bias, blk.ff.net[0])
         h = AddFn.apply(h, proj_train([blk.ff.net[2]], f))
     return AddFn.apply(x2d, proj_train([t2d.proj_out], h))
 
@@ -350,7 +471,7 @@ def motion_module_train(mm, x2d, nclip: int, F: int, HW: int):
             o = TemporalAttentionFn.apply(qkv, nclip, F, HW, attn.heads)
             h = AddFn.apply(h, proj_train([attn.to_out[0]], o))
         n = LayerNormFn.apply(h, blk.norm3.weight, blk.norm3.bias, blk.norm3.eps)
-        f = GEGLUFn.apply(n, blk.ff.net[0].proj.weight, blk.ff.net[0].proj.bias)
+        f = GEGLUFn.apply(n, blk.ff.net[0].proj.weight, blk.ff.net[0].proj.bias, blk.ff.net[0])
         h = AddFn.apply(h, proj_train([blk.ff.net[2]], f))
     return AddFn.apply(x2d, proj_train([mm.proj_out], h))
 
@@ -420,6 +541,21 @@ class CatFn(torch.autograd.Function):
         return g[:, :ctx.ca].contiguous(), g[:, ctx.ca:].contiguous()
 
 
+def _conv1x1_ops(sc):
+    """ProjOps of a frozen 1x1 conv shortcut (kernel weight [Cout, Cin] bf16, fp32 bias), cached per version."""
+    from .lora_linear import ProjOps
+    from .unet_motion import f32
+    if sc.weight.requires_grad:
+        raise NotImplementedError("conv shortcut: frozen (spatial path) only")
+    key = (sc.weight.data_ptr(), sc.weight._version, sc.bias.data_ptr(), sc.bias._version)
+    c = sc.__dict__.get("_vst_train_ops")
+    if c is None or c[0] != key:
+        w = sc.kernel_weight()
+        c = (key, ProjOps(w, None, f32(sc.bias), w.shape[1], w.shape[0], 0))
+        sc.__dict__["_vst_train_ops"] = c
+    return c[1]
+
+
 def resnet_train(rb, x2d, nimg: int, H: int, W: int, temb_rows=None, rows_per_bias: int = 1):
     """ResnetBlock2D (frozen spatial path) forward on autograd Functions, so the gradient w.r.t. its input flows back
     on HIP kernels: GN+SiLU -> conv1 (+temb row bias) -> GN+SiLU -> conv2 -> + shortcut.
@@ -430,11 +566,7 @@ def resnet_train(rb, x2d, nimg: int, H: int, W: int, temb_rows=None, rows_per_bi
     h = GroupNormFn.apply(h, rb.norm2.weight, rb.norm2.bias, nimg, HW, rb.norm2.num_groups, rb.norm2.eps, True)
     h = Conv3x3Fn.apply(h, rb.conv2, nimg, H, W)
     if rb.conv_shortcut is not None:
-        sc = rb.conv_shortcut
-        Wsc = sc.weight.reshape(sc.weight.shape[0], -1)
-        A0 = Wsc.new_zeros(0, Wsc.shape[1], dtype=torch.float32)
-        B0 = Wsc.new_zeros(Wsc.shape[0], 0, dtype=torch.float32)
-        x2d = LoRALinearFn.apply(x2d, Wsc, sc.bias, A0, B0, 1.0)
+        x2d = FrozenProjFn.apply(x2d, _conv1x1_ops(rb.conv_shortcut))
     return AddFn.apply(x2d, h)
 
 

@@ -270,6 +270,10 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) if (e < nv) v[e] += p.bias[n + e];
       }
+      if (p.rbias || p.R) {  // same rounding points as the ring kernel: bf16 linear output, then the adds
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = round_bf(v[e]);
+      }
       if (p.rbias) {
         const float* rb = p.rbias + (size_t)(m / p.rbias_div) * p.ldrb + n;
 #pragma unroll
@@ -304,7 +308,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
         float h = Cs[row * BN + cc * 8 + e];
         float g = Cs[row * BN + 64 + cc * 8 + e];
         if (p.bias) { h += p.bias[n0 + cc * 8 + e]; g += p.bias[n0 + 64 + cc * 8 + e]; }
-        v[e] = h * gelu_erf(g);
+        v[e] = round_bf(h) * gelu_erf(round_bf(g));  // bf16 projection output, as the ring kernel stages it
       }
       *reinterpret_cast<u32x4*>(p.C + (size_t)m * p.ldc + (n0 >> 1) + cc * 8) = pack8(v);
     }
@@ -440,6 +444,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(GemmArgs p, int
       }
       for (int e = 0; e < nv; ++e) {
         if (p.bias) v[e] += p.bias[n + e];
+        if (p.rbias || p.R) v[e] = round_bf(v[e]);  // rounding points of the ring kernel's epilogue
         if (p.rbias) v[e] += p.rbias[(size_t)(m / p.rbias_div) * p.ldrb + n + e];
         if (p.R) v[e] += bf2f(p.R[(size_t)m * p.ldr + n + e]);
         if (p.act) v[e] = gelu_erf(v[e]);
@@ -458,7 +463,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(GemmArgs p, int
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         if (p.bias) { h[e] += p.bias[hc + e]; g[e] += p.bias[gc + e]; }
-        v[e] = h[e] * gelu_erf(g[e]);
+        v[e] = round_bf(h[e]) * gelu_erf(round_bf(g[e]));
       }
     }
     bf16_t* dst = p.C + (size_t)m * p.ldc + n;

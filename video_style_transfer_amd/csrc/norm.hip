@@ -667,6 +667,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const bf16_t* __rest
       }
     }
   }
+  if (!part) return;  // frozen LayerNorm (spatial path): no dgamma / dbeta
 #pragma unroll
   for (int i = 0; i < MAXCH; ++i) {
     const int cc = lane + 64 * i;
@@ -683,22 +684,26 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const bf16_t* __rest
   }
 }
 
-// 64 columns per workgroup, 4 threads per column over strided partial blocks, combined in a fixed order
+// 16 columns per workgroup x 16 partial-block stripes (a stripe reads 64 contiguous bytes), combined in a fixed
+// order through LDS (deterministic).
 __global__ __launch_bounds__(256) void layernorm_bwd_reduce_kernel(const float* __restrict__ part, int nblk, int C,
                                                                    float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  __shared__ float red[4][64];
-  const int lc = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lc;
+  __shared__ float red[16][17];
+  const int lc = threadIdx.x & 15, q = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + lc;
   float a = 0.f;
   if (c < 2 * C) {
     const int which = c / C, cc = c - which * C;
-    for (int b = q; b < nblk; b += 4) a += part[((size_t)b * 2 + which) * C + cc];
+    for (int b = q; b < nblk; b += 16) a += part[((size_t)b * 2 + which) * C + cc];
   }
   red[q][lc] = a;
   __syncthreads();
   if (q == 0 && c < 2 * C) {
     const int which = c / C, cc = c - which * C;
-    (which ? dbeta : dgamma)[cc] = red[0][lc] + red[1][lc] + red[2][lc] + red[3][lc];
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][lc];
+    (which ? dbeta : dgamma)[cc] = t;
   }
 }
 
@@ -853,7 +858,7 @@ extern "C" int vst_layernorm_lora(const void* x, int ldx, int C, int rows, const
 }
 
 // ---- LayerNorm backward (training path) ----
-static inline int lnb_grid(int rows) { return std::max(1, std::min(1024, (rows + 3) / 4)); }
+static inline int lnb_grid(int rows) { return std::max(1, std::min(512, (rows + 3) / 4)); }
 
 extern "C" size_t vst_layernorm_bwd_workspace_bytes(int C, int rows) {
   return (size_t)lnb_grid(rows) * 2 * C * sizeof(float);
@@ -862,12 +867,13 @@ extern "C" size_t vst_layernorm_bwd_workspace_bytes(int C, int rows) {
 extern "C" int vst_layernorm_bwd(const void* x, int ldx, const void* g, int ldg, int C, int rows, const float* gamma,
                                  float eps, void* dx, int lddx, float* dgamma, float* dbeta, void* workspace,
                                  void* stream) {
-  if (!x || !g || !dx || !gamma || !dgamma || !dbeta || !workspace || rows <= 0 || C <= 0 || C % 8 ||
-      (ldx & 7) || (ldg & 7) || (lddx & 7) || C > 2048)
+  // dgamma == dbeta == NULL: dx only (frozen affine), no workspace needed
+  if (!x || !g || !dx || !gamma || (!dgamma) != (!dbeta) || (dgamma && !workspace) || rows <= 0 || C <= 0 ||
+      C % 8 || (ldx & 7) || (ldg & 7) || (lddx & 7) || C > 2048)
     return VST_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int grid = lnb_grid(rows);
-  float* part = (float*)workspace;
+  float* part = dgamma ? (float*)workspace : nullptr;
   const int CH = C / 8;
 #define VST_LNB(MC)                                                                                            \
   hipLaunchKernelGGL((layernorm_bwd_kernel<MC>), dim3(grid), dim3(256), 0, s, (const bf16_t*)x, ldx, (const bf16_t*)g, \
@@ -876,8 +882,9 @@ extern "C" int vst_layernorm_bwd(const void* x, int ldx, const void* g, int ldg,
   else if (CH <= 128) VST_LNB(2);
   else VST_LNB(4);
 #undef VST_LNB
-  hipLaunchKernelGGL(layernorm_bwd_reduce_kernel, dim3((2 * C + 63) / 64), dim3(256), 0, s, part, grid, C, dgamma,
-                     dbeta);
+  if (dgamma)
+    hipLaunchKernelGGL(layernorm_bwd_reduce_kernel, dim3((2 * C + 15) / 16), dim3(256), 0, s, part, grid, C, dgamma,
+                       dbeta);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 

@@ -52,6 +52,8 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   __bf16 b = (__bf16)f;
   return *reinterpret_cast<uint16_t*>(&b);
 }
+// value of x after a bf16 store and reload (the rounding point of a bf16 tensor boundary)
+__device__ __forceinline__ float round_bf(float x) { return bf2f(f2bf(x)); }
 __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
   return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
 }

@@ -392,15 +392,19 @@ def transpose(x, out=None):
     return out
 
 
-def layer_norm_bwd(x, g, gamma, eps=1e-5):
-    """LayerNorm backward: (dx bf16 [rows, C], dgamma fp32 [C], dbeta fp32 [C])."""
+def layer_norm_bwd(x, g, gamma, eps=1e-5, need_affine=True):
+    """LayerNorm backward: (dx bf16 [rows, C], dgamma fp32 [C], dbeta fp32 [C]); need_affine=False (frozen
+    affine) computes dx only and returns (dx, None, None)."""
     _dev(x, BF16, "x")
     _dev(g, BF16, "g")
     rows, C = x.shape
     dx = torch.empty((rows, C), dtype=BF16, device=x.device)
-    dgamma = torch.empty(C, dtype=F32, device=x.device)
-    dbeta = torch.empty(C, dtype=F32, device=x.device)
-    ws = torch.empty((_lib.load().vst_layernorm_bwd_workspace_bytes(C, rows) + 3) // 4, dtype=F32, device=x.device)
+    dgamma = dbeta = ws = None
+    if need_affine:
+        dgamma = torch.empty(C, dtype=F32, device=x.device)
+        dbeta = torch.empty(C, dtype=F32, device=x.device)
+        ws = torch.empty((_lib.load().vst_layernorm_bwd_workspace_bytes(C, rows) + 3) // 4, dtype=F32,
+                         device=x.device)
     with _Rec("layernorm_bwd", 0.0, 2.0 * 3 * rows * C):
         _lib.call("vst_layernorm_bwd", _p(x), _ld(x), _p(g), _ld(g), C, rows, _p(gamma), float(eps), _p(dx), _ld(dx),
                   _p(dgamma), _p(dbeta), _p(ws), _stream())

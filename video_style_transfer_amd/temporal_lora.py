@@ -45,7 +45,7 @@ class TemporalLoRALinear(nn.Module):
                                         or self.base.weight.requires_grad):
             # training (train_animatediff.py:265-319): HIP forward + backward through autograd.LoRALinearFn
             from .autograd import lora_linear
-            return lora_linear(x, self.base.weight, self.base.bias, self.lora_A, self.lora_B, self.scale)
+            return lora_linear(x, self.base.weight, self.base.bias, self.lora_A, self.lora_B, self.scale, self)
         x2 = x.reshape(-1, self.in_features)
         out = run_ops(x2, build_ops([self], 1.0))
         return out.view(x.shape[:-1] + (self.out_features,))
