@@ -55,7 +55,7 @@ def _report(name, out, ref_bf, ref_fp32=None):
         f2, fm = rel(out, ref_fp32)
         b2, bm = rel(ref_bf, ref_fp32)
         msg += f" | vs fp32 oracle rel_l2={f2:.2e} rel_max={fm:.2e} (emulation itself vs fp32: {b2:.2e})"
-    print(msg)
+    print(msg, flush=True)
     return e2, em
 
 
@@ -116,6 +116,10 @@ def _floor(fn, out=None):
     return ref, floor
 
 
+def log(msg):
+    print(msg, flush=True)
+
+
 def _replay(P, kind, name, a, lora):
     from oracle import unet_bf16 as E
     if kind == "resnet":
@@ -135,12 +139,12 @@ def sdxl_r8(cuda):
     return cfg, unet, _params(unet)
 
 
-def test_configs2_sdxl_f16_per_layer_and_chained(cuda, sdxl_r8):
+def test_configs2_sdxl_f16_per_layer(cuda, sdxl_r8):
     """configs[2]: 16 frames, 64x64 latent, UnZipLoRA r=8 (one CFG branch, B=1).  Every ResnetBlock2D /
-    Transformer2DModel / motion module of the HIP forward replayed through the emulation on its own bf16 input
-    (per-layer gate), then the whole forward chained (end-to-end gate) and the fp32 oracle for reference."""
+    Transformer2DModel / motion module (43 layers) of the HIP forward replayed through the emulation on its own bf16
+    input.  (The chained end-to-end comparison at F=16 is test_configs1; the fp32 oracle at SDXL scale is
+    test_parity_gpu.py::test_unet_forward_sdxl_architecture_vs_oracle.)"""
     from oracle import unet as O
-    from oracle import unet_bf16 as E
     cfg, unet, P = sdxl_r8
     torch.set_num_threads(THREADS)
     lat, enc, pooled, tids = _inputs(cfg, 1, 16, 64, 31)
@@ -152,27 +156,24 @@ def test_configs2_sdxl_f16_per_layer_and_chained(cuda, sdxl_r8):
     assert {k: sum(1 for r in R.rec if r[0] == k) for k in kinds} == kinds
     worst = {}
     fails = []
+    floors = {}  # (kind, C): reassociation floor of the first layer of that kind and width above 1e-3
     t0 = time.time()
     with torch.no_grad():
         for kind, name, a, y in R.rec:
             ref = _replay(P, kind, name, a, O.LoRAState())
             e2, em = rel(y, ref)
-            floor = None
-            if e2 > 1e-3:  # only layers above the absolute bar need their reassociation floor
-                floor = _floor(lambda: _replay(P, kind, name, a, O.LoRAState()), y)[1]
-            print(f"[bf16-parity] layer {name:42s} rel_l2={e2:.2e} rel_max={em:.2e}"
-                  + ("" if floor is None else f" floor={floor:.2e}"))
+            key = (kind, y.shape[1])
+            if e2 > 1e-3 and key not in floors:
+                floors[key] = _floor(lambda: _replay(P, kind, name, a, O.LoRAState()), y)[1]
+            floor = floors.get(key) if e2 > 1e-3 else None
+            log(f"[bf16-parity] layer {name:42s} rel_l2={e2:.2e} rel_max={em:.2e}"
+                + ("" if floor is None else f" floor({kind}, C={key[1]})={floor:.2e}"))
             w = worst.setdefault(kind, [0.0, 0.0])
             w[0], w[1] = max(w[0], e2), max(w[1], em)
             if e2 > max(1e-3, 3 * (floor or 0.0)) or em > 1.6e-2:
                 fails.append((name, e2, em, floor))
-        print(f"[bf16-parity] per-layer worst {worst} (replay {time.time() - t0:.0f}s)")
-        assert not fails, fails
-        ref_bf, floor = _floor(lambda: E.unet_forward(P, cfg.to_dict(), lat, t, enc, pooled, tids), out)
-        ref32 = O.unet_forward(P, cfg.to_dict(), lat, t, enc, pooled, tids)
-    e2, em = _report("configs[2] SDXL F=16 64x64 r=8 chained", out, ref_bf, ref32)
-    print(f"[bf16-parity] configs[2] chained reassociation floor {floor:.2e}")
-    assert e2 <= max(5e-3, 3 * floor) and em <= 5e-2
+    log(f"[bf16-parity] configs[2] per-layer worst {worst} (replay {time.time() - t0:.0f}s)")
+    assert not fails, fails
 
 
 def test_configs1_sdxl_f16_no_lora_chained(cuda):
@@ -190,10 +191,11 @@ def test_configs1_sdxl_f16_no_lora_chained(cuda):
     t = torch.tensor([301.0])
     out = unet(lat.to(cuda), t.to(cuda), enc.to(cuda), added_cond_kwargs={"text_embeds": pooled.to(cuda),
                                                                          "time_ids": tids.to(cuda)}).sample
+    log("[bf16-parity] configs[1]: emulating the whole forward (+ reassociation probe) on the CPU ...")
     with torch.no_grad():
         ref_bf, floor = _floor(lambda: E.unet_forward(P, cfg.to_dict(), lat, t, enc, pooled, tids), out)
     e2, em = _report("configs[1] SDXL F=16 64x64 no LoRA chained", out, ref_bf)
-    print(f"[bf16-parity] configs[1] chained reassociation floor {floor:.2e}")
+    log(f"[bf16-parity] configs[1] chained reassociation floor {floor:.2e}")
     assert e2 <= max(5e-3, 3 * floor) and em <= 5e-2
 
 
@@ -214,11 +216,12 @@ def test_configs0_sdxl_image_unet_f1(cuda):
     t = torch.tensor([901.0, 901.0])
     out = unet(lat.to(cuda), t.to(cuda), enc.to(cuda), added_cond_kwargs={"text_embeds": pooled.to(cuda),
                                                                          "time_ids": tids.to(cuda)}).sample
+    log("[bf16-parity] configs[0]: emulation, probe and fp32 oracle on the CPU ...")
     with torch.no_grad():
         ref_bf, floor = _floor(lambda: E.unet_forward(P, cfg.to_dict(), lat, t, enc, pooled, tids), out)
         ref32 = O.unet_forward(P, cfg.to_dict(), lat, t, enc, pooled, tids)
     e2, em = _report("configs[0] SDXL image UNet F=1 32x32", out, ref_bf, ref32)
-    print(f"[bf16-parity] configs[0] reassociation floor {floor:.2e}")
+    log(f"[bf16-parity] configs[0] reassociation floor {floor:.2e}")
     assert e2 <= max(5e-3, 3 * floor) and em <= 5e-2
 
 
@@ -242,10 +245,11 @@ def test_denoise_50_steps_vs_bf16_emulation(cuda):
     assert int(den.step_idx.item()) == 0  # the device counter wrapped at the end of the schedule
     tid = tids[:1]
     torch.set_num_threads(THREADS)
+    log("[bf16-parity] denoise: 50 emulated + 50 probe + 50 fp32 oracle steps on the CPU ...")
     with torch.no_grad():
         ref_bf, floor = _floor(lambda: E.denoise(P, cfg.to_dict(), lat0, (enc[1:2], pooled[1:2]), (enc[0:1], pooled[0:1]),
                                                  tid, 50, 7.5), out)
         ref32 = O.denoise(P, cfg.to_dict(), lat0, (enc[1:2], pooled[1:2]), (enc[0:1], pooled[0:1]), tid, 50, 7.5)
     e2, em = _report("denoise 50 steps tiny F=8 16x16 (graph)", out, ref_bf, ref32)
-    print(f"[bf16-parity] denoise 50 steps reassociation floor {floor:.2e}")
+    log(f"[bf16-parity] denoise 50 steps reassociation floor {floor:.2e}")
     assert e2 <= max(5e-3, 3 * floor) and em <= 5e-2
