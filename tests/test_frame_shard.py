@@ -175,3 +175,58 @@ def test_frame_shard_unet_two_ranks_one_gpu():
     for rank, status, info in res:
         print(f"[shard] rank {rank}: {status} {info}")
         assert status == "ok", f"rank {rank}: {info}"
+
+
+def _gpu_worker_sdxl768(rank, world, port, q):
+    """BASELINE configs[3] shapes: SDXL + motion modules + UnZipLoRA r=8, 32 frames at 768x768 (96x96 latent),
+    frames split over 2 ranks (16 each) on one GPU, vs the unsharded HIP forward of the whole clip."""
+    try:
+        sys.path.insert(0, ROOT)
+        _init(rank, world, port)
+        from video_style_transfer_amd.config import UNetMotionConfig
+        from video_style_transfer_amd.frame_shard import FrameShard
+        from video_style_transfer_amd.utils import build_unet
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        cfg = UNetMotionConfig.sdxl()
+        unet = build_unet(cfg, seed=41, lora_rank=8, device=dev)
+        F, hw = 32, 96
+        g = torch.Generator().manual_seed(42)
+        lat = torch.randn(1, 4, F, hw, hw, generator=g)
+        enc = torch.randn(1, 77, cfg.cross_attention_dim, generator=g)
+        pooled = torch.randn(1, cfg.text_embed_dim, generator=g)
+        tids = torch.tensor([[768, 768, 0, 0, 768, 768]], dtype=torch.float32)
+        t = torch.tensor([501.0])
+        kw = dict(added_cond_kwargs={"text_embeds": pooled.to(dev), "time_ids": tids.to(dev)})
+        sh = FrameShard()
+        Fl, f0 = sh.local_frames(F)
+        part = unet(lat[:, :, f0:f0 + Fl].contiguous().to(dev), t.to(dev), enc.to(dev), frame_shard=sh,
+                    **kw).sample.float().cpu()
+        full = unet(lat.to(dev), t.to(dev), enc.to(dev), **kw).sample.float().cpu()[:, :, f0:f0 + Fl]
+        # chaos floor of this network: the unsharded forward of latents nudged by 2^-20 (relative), which flips a
+        # few input roundings by one bf16 ulp -- the size of perturbation fp32 reassociation makes inside
+        nudged = unet((lat * (1 + 2.0 ** -20)).to(dev), t.to(dev), enc.to(dev), **kw).sample.float().cpu()
+        floor = ((nudged[:, :, f0:f0 + Fl] - full).norm() / full.norm()).item()
+        e = ((part - full).norm() / full.norm()).item()
+        m = ((part - full).abs().max() / full.abs().max()).item()
+        # the only differences are fp32 summation orders (per-rank GroupNorm chunk partials merged across ranks),
+        # amplified through the random-weight network like any reassociation (tests/test_parity_bf16_gpu.py)
+        ok = torch.isfinite(part).all().item() and e <= max(1e-2, 3 * floor)
+        q.put((rank, "ok" if ok else "fail", f"frames {f0}..{f0 + Fl - 1}: sharded vs unsharded rel_l2={e:.2e} "
+                                             f"rel_max={m:.2e}; chaos floor (2^-20 input nudge) {floor:.2e}"))
+    except BaseException:  # noqa: BLE001
+        import traceback
+        q.put((rank, "fail", traceback.format_exc()[-2000:]))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_frame_shard_sdxl_768_32_frames_two_ranks_one_gpu():
+    if torch.cuda.device_count() == 0:
+        pytest.skip("no HIP device")
+    res = _spawn(_gpu_worker_sdxl768, 2)
+    for rank, status, info in res:
+        print(f"[shard] configs[3] rank {rank}: {status} {info}")
+        assert status == "ok", f"rank {rank}: {info}"
