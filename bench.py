@@ -59,6 +59,10 @@ def parse():
     ap.add_argument("--no-peaks", action="store_true", help="skip the MFMA / HBM ceiling probes")
     ap.add_argument("--cpu-sample-frames", type=int, default=2)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--train", action="store_true",
+                    help="BASELINE configs[4]: one train_animatediff.py optimizer step per rank (fwd+bwd on a 16-frame "
+                         "clip, orth loss, clip_grad_norm_, AdamW; RCCL gradient all-reduce for N>1) instead of the "
+                         "denoise loop")
     return ap.parse_args()
 
 
@@ -97,6 +101,11 @@ def roofline(den):
     rec = K.collect_launches()
     K.profile_launches(False)
     den.step_idx.zero_()
+    return _roofline_from(rec)
+
+
+def _roofline_from(rec):
+    """Group instrumented launches by kernel symbol; the dominant kernel's achieved rate against its roofline."""
     by = {}
     shapes = {}
     for kind, sym, fl, nb, ms, shape in rec:
@@ -184,9 +193,141 @@ def cpu_baseline(args, cfg):
         dt = time.perf_counter() - t0
     del sd
     fps = fr / (2 * args.num_inference_steps * dt)
-    return {"value": fps, "unit": "frames/s", "cores": threads, "kind": "port",
+    return {"value": fps, "unit": "frames/s", "cores": threads, "kind": "port", "cpu": _cpu_model(),
             "sample": f"1 UNet forward (one CFG branch) of a {fr}-frame {args.size}x{args.size} clip, fp32, "
                       f"{dt:.2f}s, extrapolated x{2 * args.num_inference_steps} forwards"}
+
+
+def train_cpu_baseline(args, cfg):
+    """Oracle (fp32 CPU restatement) forward + backward of the trainable motion parameters on a bounded sample
+    (`cpu_sample_frames` frames at the bench resolution), extrapolated to training frames/s."""
+    from oracle.unet import unet_forward
+    from video_style_transfer_amd.weights import synthetic_state_dict
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    sd = synthetic_state_dict(cfg, args.seed, args.lora_rank or None)
+    for k, v in sd.items():
+        v.requires_grad_("motion_modules" in k and not k.endswith(".pe"))
+    fr, h = args.cpu_sample_frames, args.size // 8
+    g = torch.Generator().manual_seed(1)
+    lat = torch.randn(1, 4, fr, h, h, generator=g)
+    enc = torch.randn(1, 77, cfg.cross_attention_dim, generator=g)
+    pooled = torch.randn(1, cfg.text_embed_dim, generator=g)
+    tids = torch.tensor([[args.size, args.size, 0, 0, args.size, args.size]], dtype=torch.float32)
+    t0 = time.perf_counter()
+    pred = unet_forward(sd, cfg.to_dict(), lat, torch.tensor([501.0]), enc, pooled, tids)
+    ((pred - torch.randn_like(pred)) ** 2).mean().backward()
+    dt = time.perf_counter() - t0
+    del sd
+    return {"value": fr / dt, "unit": "frames/s", "cores": threads, "kind": "port", "cpu": _cpu_model(),
+            "sample": f"fp32 oracle forward + backward (motion-module parameters trainable) of a {fr}-frame "
+                      f"{args.size}x{args.size} clip: {dt:.2f}s"}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def bench_train(args, world, rank, local, dev):
+    """BASELINE configs[4] (train_animatediff.py:212-319): SDXL UNet + AnimateDiff-SDXL motion modules (synthetic
+    weights), UnZipLoRA r=8 frozen on all spatial projections, temporal LoRA r=32 injected, freeze_spatial_layers,
+    one 16x512x512 clip (synthetic VAE latents) per rank per step: Euler add_noise, UNet fwd, MSE + orth loss
+    (lambda 1e-4), backward, gradient all-reduce (RCCL, N>1), clip_grad_norm_(0.5), AdamW(2e-5).  N=1: the whole
+    step is one captured HIP graph; N>1: eager steps with the bucketed all-reduce overlapping the backward."""
+    from video_style_transfer_amd import kernels as K
+    from video_style_transfer_amd.config import UNetMotionConfig
+    from video_style_transfer_amd.scheduler import EulerDiscreteScheduler
+    from video_style_transfer_amd.temporal_lora import build_spatial_lora_index, inject_temporal_lora
+    from video_style_transfer_amd.train import GradBucketAllReducer, TrainStep, broadcast_parameters
+    from video_style_transfer_amd.utils import build_unet, freeze_spatial_layers
+    cfg = UNetMotionConfig.sdxl()
+    t_build = time.perf_counter()
+    unet = build_unet(cfg, seed=args.seed, lora_rank=args.lora_rank or None, device=dev)
+    torch.manual_seed(args.seed)
+    inject_temporal_lora(unet, rank=32, alpha=1.0)
+    freeze_spatial_layers(unet)
+    if world > 1:
+        broadcast_parameters(unet)
+    params = [p for p in unet.parameters() if p.requires_grad]
+    graph = world == 1 and not args.no_graph
+    opt = torch.optim.AdamW(params, lr=2e-5, betas=(0.9, 0.999), weight_decay=1e-2, eps=1e-8, capturable=graph)
+    reducer = GradBucketAllReducer(params) if world > 1 else None
+    step = TrainStep(unet, opt, EulerDiscreteScheduler(), reducer=reducer, lambda_orth=1e-4,
+                     spatial_index=build_spatial_lora_index(unet), max_grad_norm=0.5, resolution=args.size,
+                     seed=args.seed)
+    g = torch.Generator().manual_seed(100 + rank)
+    h = args.size // 8
+    lat = torch.randn(1, 4, args.frames, h, h, generator=g).to(dev)
+    enc = torch.randn(1, 77, cfg.cross_attention_dim, generator=g)
+    pooled = torch.randn(1, cfg.text_embed_dim, generator=g)
+    unc, unp = torch.zeros_like(enc), torch.zeros_like(pooled)
+    if graph:
+        step.capture(lat, enc, pooled, uncond_prompt=unc, uncond_pooled=unp)
+        run = step.replay
+    else:
+        def run():
+            return step(lat, enc, pooled, unc, unp)
+    t_build = time.perf_counter() - t_build
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    ms_step = dt / args.steps * 1e3
+    value = args.frames * world / (ms_step * 1e-3)
+    ok = bool(torch.isfinite(out["loss"]).item())
+    rl = table = step_rl = None
+    if not args.no_roofline:
+        # one instrumented eager step (HIP events around every launch on its stream)
+        K.profile_launches(True)
+        step(lat, enc, pooled)
+        rl, table = _roofline_from(K.collect_launches())
+        K.profile_launches(False)
+        fl = rl.pop("step_flops")
+        step_rl = {"alg_tflop": round(fl / 1e12, 2), "achieved_tflops": round(fl / (ms_step * 1e-3) / 1e12, 1),
+                   "frac": round(fl / (ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4)}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        del step, opt, unet
+        torch.cuda.empty_cache()
+        cpu = train_cpu_baseline(args, cfg)
+    if rank == 0:
+        print(json.dumps({
+            "metric": f"train frames/sec (fwd+bwd+AdamW step), {args.frames}x{args.size}x{args.size} clip per GPU, "
+                      f"AnimateDiff-XL temporal LoRA",
+            "value": round(value, 3), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "config": {"workload": f"BASELINE configs[4]: train_animatediff.py step, {args.frames}x{args.size}x"
+                                   f"{args.size} clip/GPU, temporal LoRA r=32, UnZipLoRA r={args.lora_rank} frozen, "
+                                   f"orth loss 1e-4, clip 0.5, AdamW",
+                       "model": "SDXL UNet + AnimateDiff-SDXL motion modules (synthetic weights)",
+                       "global_batch": world, "frames": args.frames, "resolution": args.size,
+                       "parallelism": f"dp{world}" + (" (RCCL bucketed all-reduce)" if world > 1 else ""),
+                       "graph": graph, "trainable_params": sum(p.numel() for p in params)},
+            "loss": round(float(out["loss"]), 5), "finite": ok,
+            "roofline": rl, "step_roofline": step_rl, "cpu_baseline": cpu, "kernels": table,
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1), "setup_s": round(t_build, 1)}))
 
 
 def main():
@@ -208,6 +349,8 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if args.train:
+        return bench_train(args, world, rank, local, dev)
 
     from video_style_transfer_amd.config import UNetMotionConfig
     from video_style_transfer_amd.lora_linear import set_lora_mode

@@ -25,8 +25,10 @@ BF16 = torch.bfloat16
 
 
 def _wt(W: torch.Tensor) -> torch.Tensor:
-    """W^T (bf16, [in, out]), cached on the parameter per version: frozen weights transpose once, trained ones once
-    per optimizer step."""
+    """W^T (bf16, [in, out]), cached on the parameter per version while it is frozen; a trained weight is transposed
+    on every call (HIP-graph replay updates it without a version bump, so a cache would go stale)."""
+    if W.requires_grad:
+        return K.transpose(W.detach().to(BF16).contiguous())
     key = (W.data_ptr(), W._version)
     c = W.__dict__.get("_vst_wt")
     if c is None or c[0] != key:
@@ -249,8 +251,10 @@ def _deinterleave32(t: torch.Tensor) -> torch.Tensor:
 
 
 def _geglu_wt(geglu):
-    """(interleaved GEGLU weight)^T, cached on the module per weight version."""
+    """(interleaved GEGLU weight)^T, cached on the module per weight version while frozen."""
     w = geglu.proj.weight
+    if w.requires_grad:
+        return K.transpose(geglu.geglu_ops()[0])
     key = (w.data_ptr(), w._version)
     c = geglu.__dict__.get("_vst_geglu_wt")
     if c is None or c[0] != key:

@@ -122,8 +122,11 @@ def build_ops(lins: Sequence[nn.Module], scale: float = 1.0, mode: Optional[str]
     mode = mode or _LORA_MODE
     key = (tuple(id(l) for l in lins), float(scale), mode)
     skey = tuple(_state_key(l, scale, mode) for l in lins)
+    # operands of parameters that train are rebuilt per call: HIP-graph replay of a training step updates them
+    # without a version bump, so a version-keyed cache would go stale
+    cacheable = not any(p.requires_grad for l in lins for p in l.parameters())
     cache = lins[0].__dict__.setdefault("_vst_ops_cache", {})
-    hit = cache.get(key)
+    hit = cache.get(key) if cacheable else None
     if hit is not None and hit[0] == skey:
         return hit[1]
     with torch.no_grad():
@@ -169,7 +172,8 @@ def build_ops(lins: Sequence[nn.Module], scale: float = 1.0, mode: Optional[str]
             bias = torch.cat([b if b is not None else torch.zeros(w.shape[0], device=dev) for w, b in zip(Ws, bs)])
             bias = bias.contiguous()
         ops = ProjOps(W_all.to(torch.bfloat16).contiguous(), a_bf, bias, K1, N, R if a_bf is not None else 0)
-    cache[key] = (skey, ops)
+    if cacheable:
+        cache[key] = (skey, ops)
     return ops
 
 

@@ -49,9 +49,13 @@ class EulerDiscreteScheduler:
         return sample / ((self.sigmas[step_index] ** 2 + 1) ** 0.5)
 
     def add_noise(self, original_samples, noise, timesteps):
-        """Training noising (train_animatediff.py:234-236): x + sigma(t) * eps (no input scaling)."""
-        sig_all = ((1 - self.alphas_cumprod) / self.alphas_cumprod) ** 0.5
-        s = sig_all.to(original_samples.device)[timesteps.long()].to(original_samples.dtype)
+        """Training noising (train_animatediff.py:234-236): x + sigma(t) * eps (no input scaling).  The sigma table
+        is kept on the samples' device, so the call issues no host copy (graph-capturable)."""
+        dev = original_samples.device
+        cache = self.__dict__.setdefault("_sig_dev", {})
+        if dev not in cache:
+            cache[dev] = (((1 - self.alphas_cumprod) / self.alphas_cumprod) ** 0.5).to(dev)
+        s = cache[dev][timesteps.long()].to(original_samples.dtype)
         while s.dim() < original_samples.dim():
             s = s.unsqueeze(-1)
         return original_samples + s * noise

@@ -148,11 +148,27 @@ class TrainStep:
         rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
         self.gen = torch.Generator(device="cpu").manual_seed(seed + 1000003 * rank)
 
-    def __call__(self, latents: torch.Tensor, prompt, pooled, uncond_prompt=None, uncond_pooled=None, *,
-                 noise: Optional[torch.Tensor] = None, timesteps: Optional[torch.Tensor] = None,
-                 use_uncond: Optional[bool] = None) -> Dict:
-        """noise / timesteps / use_uncond override the step's random draws (tests compare a data-parallel step
-        with a single-process step on the concatenated batch)."""
+    def _draw(self, latents, noise=None, timesteps=None, use_uncond=None, has_uncond=False):
+        """The step's random draws (train_animatediff.py:228-254) from this rank's generator; overrides win."""
+        B = latents.shape[0]
+        draw_noise = torch.randn(latents.shape, generator=self.gen)                         # :228
+        draw_t = torch.randint(0, self.sched.num_train_timesteps, (B,), generator=self.gen)  # :229-232
+        draw_u = float(torch.rand(1, generator=self.gen)) < self.p_uncond                  # :248-254
+        noise = draw_noise if noise is None else noise
+        t = draw_t if timesteps is None else timesteps
+        return noise, t.cpu(), has_uncond and (draw_u if use_uncond is None else use_uncond)
+
+    def _text(self, prompt, pooled, B, dev):
+        enc = prompt.to(dev, BF16)
+        pool = pooled.to(dev, BF16)
+        enc = enc.expand(B, -1, -1).reshape(-1, enc.shape[-1]).contiguous()               # .repeat(B, 1, 1)
+        pool = pool.expand(B, -1).contiguous()
+        return enc, pool
+
+    def _body(self, latents, noise, t, enc, pool) -> Dict:
+        """Forward, losses, backward, gradient averaging, clipping and the optimizer step on device tensors only (no
+        host synchronisation: the body is what TrainStep.capture records into a HIP graph).  Gradients must be
+        None or zero on entry."""
         from . import kernels as K
         from .autograd import unet_train_tokens
         from .temporal_lora import compute_orth_loss
@@ -160,25 +176,13 @@ class TrainStep:
         unet = self.unet
         B, Cl, F, h, w = latents.shape
         dev = latents.device
-        draw_noise = torch.randn(latents.shape, generator=self.gen)                         # :228
-        draw_t = torch.randint(0, self.sched.num_train_timesteps, (B,), generator=self.gen)  # :229-232
-        draw_u = float(torch.rand(1, generator=self.gen)) < self.p_uncond                  # :248-254
-        noise = (draw_noise if noise is None else noise).to(dev, torch.float32)
-        t = (draw_t if timesteps is None else timesteps).cpu()
         # add_noise with the clip's timestep on every frame (:233-236); sigma broadcasts over (C, F, h, w)
-        noisy = self.sched.add_noise(latents, noise, t.to(dev)).contiguous()
-        use_uncond = uncond_prompt is not None and (draw_u if use_uncond is None else use_uncond)
-        enc = (uncond_prompt if use_uncond else prompt).to(dev, BF16)
-        pool = (uncond_pooled if use_uncond else pooled).to(dev, BF16)
-        enc = enc.expand(B, -1, -1).reshape(-1, enc.shape[-1]).contiguous()               # .repeat(B, 1, 1)
-        pool = pool.expand(B, -1).contiguous()
-        r = float(self.resolution)
-        tids = torch.tensor([[r, r, 0.0, 0.0, r, r]], device=dev).expand(B, -1).contiguous()  # :256-262
-
+        noisy = self.sched.add_noise(latents, noise, t).contiguous()
+        tids = self._tids(B, dev)                                                          # :256-262
         x = torch.empty(B * F * h * w, Cl, dtype=BF16, device=dev)
         K.pack_latents(noisy, x)
         with torch.no_grad():
-            emb = unet.embed(t.to(dev, torch.float32), pool, tids, B)
+            emb = unet.embed(t.to(torch.float32), pool, tids, B)
         pred = unet_train_tokens(unet, x, B, F, h, w, emb, enc)                            # :265-273
         target = noise.permute(0, 2, 3, 4, 1).reshape(-1, Cl)                              # epsilon, :276-277
         loss_mse = torch.mean((pred.float() - target) ** 2)                                # :298-300
@@ -187,13 +191,84 @@ class TrainStep:
         else:
             loss_orth = torch.zeros((), device=dev)
         loss = loss_mse + loss_orth
-        self.opt.zero_grad(set_to_none=True)
         loss.backward()                                                                    # :314
         if self.reducer is not None:
             self.reducer.finish()
         gnorm = torch.nn.utils.clip_grad_norm_(self.params, self.max_grad_norm)           # :316
         self.opt.step()                                                                    # :317
+        return {"loss": loss.detach(), "loss_mse": loss_mse.detach(), "loss_orth": loss_orth.detach(),
+                "grad_norm": gnorm.detach()}
+
+    def _tids(self, B, dev):
+        key = (B, dev)
+        c = self.__dict__.setdefault("_tids_cache", {})
+        if key not in c:
+            r = float(self.resolution)
+            c[key] = torch.tensor([[r, r, 0.0, 0.0, r, r]], device=dev).expand(B, -1).contiguous()
+        return c[key]
+
+    def __call__(self, latents: torch.Tensor, prompt, pooled, uncond_prompt=None, uncond_pooled=None, *,
+                 noise: Optional[torch.Tensor] = None, timesteps: Optional[torch.Tensor] = None,
+                 use_uncond: Optional[bool] = None) -> Dict:
+        """noise / timesteps / use_uncond override the step's random draws (tests compare a data-parallel step
+        with a single-process step on the concatenated batch)."""
+        dev = latents.device
+        B = latents.shape[0]
+        noise, t, use_uncond = self._draw(latents, noise, timesteps, use_uncond, uncond_prompt is not None)
+        enc, pool = self._text(uncond_prompt if use_uncond else prompt, uncond_pooled if use_uncond else pooled, B,
+                               dev)
+        self.opt.zero_grad(set_to_none=True)
+        out = self._body(latents, noise.to(dev, torch.float32), t.to(dev), enc, pool)
         if self.lr_scheduler is not None:
             self.lr_scheduler.step()                                                       # :318
-        return {"loss": loss.detach(), "loss_mse": loss_mse.detach(), "loss_orth": loss_orth.detach(),
-                "grad_norm": gnorm.detach(), "uncond": use_uncond, "timesteps": t}
+        out.update(uncond=use_uncond, timesteps=t)
+        return out
+
+    # ---- HIP-graph capture of the whole step (single process) ------------------------------------------------
+    def capture(self, latents: torch.Tensor, prompt, pooled, warmup: int = 2, uncond_prompt=None, uncond_pooled=None):
+        """Record one whole training step (forward, backward, clipping, AdamW) into a HIP graph on static buffers,
+        after `warmup` eager steps on a side stream (they fill every frozen-operand cache).  The optimizer must be
+        built with capturable=True; per-step host work left outside the graph: the random draws (copied into the
+        static noise / timestep buffers) and the lr schedule.  Single-process only (the reducer's collectives stay
+        eager)."""
+        if self.reducer is not None and self.reducer.world > 1:
+            raise NotImplementedError("TrainStep.capture: data-parallel steps run eagerly")
+        dev = latents.device
+        B = latents.shape[0]
+        self.s_lat = latents.detach().clone()
+        self.s_noise = torch.zeros_like(self.s_lat)
+        self.s_t = torch.zeros(B, dtype=torch.long, device=dev)
+        self.s_enc, self.s_pool = self._text(prompt, pooled, B, dev)
+        # the two text conditions a step can draw (:248-254), copied into the static buffers before each replay
+        self.text_cond = (self.s_enc.clone(), self.s_pool.clone())
+        self.text_uncond = None if uncond_prompt is None else self._text(uncond_prompt, uncond_pooled, B, dev)
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                noise, t, _ = self._draw(self.s_lat)
+                self.s_noise.copy_(noise)
+                self.s_t.copy_(t)
+                self.opt.zero_grad(set_to_none=True)
+                self._body(self.s_lat, self.s_noise, self.s_t, self.s_enc, self.s_pool)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        self.opt.zero_grad(set_to_none=True)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.s_out = self._body(self.s_lat, self.s_noise, self.s_t, self.s_enc, self.s_pool)
+        return self.graph
+
+    def replay(self, latents: Optional[torch.Tensor] = None) -> Dict:
+        """One captured step on new latents (or the static ones) with fresh noise / timestep draws."""
+        if latents is not None:
+            self.s_lat.copy_(latents)
+        noise, t, use_uncond = self._draw(self.s_lat, has_uncond=self.text_uncond is not None)
+        self.s_noise.copy_(noise)
+        self.s_t.copy_(t)
+        enc, pool = self.text_uncond if use_uncond else self.text_cond
+        self.s_enc.copy_(enc)
+        self.s_pool.copy_(pool)
+        self.graph.replay()
+        if self.lr_scheduler is not None:
+            self.lr_scheduler.step()
+        return self.s_out

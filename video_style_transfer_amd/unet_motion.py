@@ -42,6 +42,8 @@ class _F32Cache:
 
     @staticmethod
     def get(p: torch.Tensor) -> torch.Tensor:
+        if p.requires_grad:  # trained parameters change under graph replay without a version bump: no cache
+            return p.detach().float().contiguous()
         key = (p.data_ptr(), p._version)
         c = p.__dict__.get("_vst_f32")
         if c is None or c[0] != key:
@@ -138,17 +140,25 @@ class GEGLU(nn.Module):
         self.proj = Linear(dim_in, dim_out * 2)
 
     def geglu_ops(self):
-        """proj weight with hidden/gate rows interleaved per 32-output block (GEMM GEGLU epilogue)."""
+        """proj weight with hidden/gate rows interleaved per 32-output block (GEMM GEGLU epilogue).  Cached per
+        parameter version while the weights are frozen; trained weights are re-interleaved on every call (a cache
+        keyed on the version would go stale under HIP-graph replay, which updates parameters without Python)."""
         w, b = self.proj.weight, self.proj.bias
+        if w.requires_grad or b.requires_grad:
+            return self._interleaved(w, b)
         key = (w.data_ptr(), w._version, b.data_ptr(), b._version)
         c = self.__dict__.get("_vst_geglu")
         if c is None or c[0] != key:
-            inner = w.shape[0] // 2
-            idx = torch.arange(inner, device=w.device).view(-1, 32)
-            idx = torch.cat([idx, idx + inner], 1).reshape(-1)
-            c = (key, (w.detach()[idx].to(BF16).contiguous(), b.detach()[idx].float().contiguous()))
+            c = (key, self._interleaved(w, b))
             self.__dict__["_vst_geglu"] = c
         return c[1]
+
+    @staticmethod
+    def _interleaved(w, b):
+        inner = w.shape[0] // 2
+        idx = torch.arange(inner, device=w.device).view(-1, 32)
+        idx = torch.cat([idx, idx + inner], 1).reshape(-1)
+        return w.detach()[idx].to(BF16).contiguous(), b.detach()[idx].float().contiguous()
 
 
 class FeedForward(nn.Module):
