@@ -83,6 +83,26 @@ def test_gemm_underfilled_grids(cuda, K, M, N, Kd, K2):
         check(out, ref, name=f"gemm {name} {M}x{N}x{Kd + K2}")
 
 
+@pytest.mark.parametrize("M,N,K1,K2,geglu", [(8192, 1280, 1280, 32, False), (2000, 640, 320, 0, False),
+                                             (4096, 2560, 640, 64, True), (1024, 320, 2048, 0, False)])
+def test_gemm_8phase_bitwise_equals_ring(cuda, K, M, N, K1, K2, geglu):
+    """The 8-phase 256x256x64 kernel (gemm_p8.hip, tile 8) accumulates every output over k in the same MFMA order as
+    the ring kernel (tile 3, no split): identical bits, tails in M / N / K (LoRA columns) included."""
+    g = torch.Generator().manual_seed(M + N + K1)
+    x, x2 = rnd(M, K1, gen=g).to(cuda), (rnd(M, K2, gen=g).to(cuda) if K2 else None)
+    w = rnd(N, K1 + K2, scale=(K1 + K2) ** -0.5, gen=g).to(cuda)
+    b = torch.randn(N, generator=g).to(cuda)
+    r = None if geglu else rnd(M, N, gen=g).to(cuda)
+    outs = []
+    for tile in (3, 8):
+        K.GEMM_POLICY.update(tile=tile, splits=1)
+        try:
+            outs.append(K.linear(x, w, b, x2=x2, residual=r, geglu=geglu))
+        finally:
+            K.GEMM_POLICY.update(tile=0, splits=0)
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_conv_underfilled_grid(cuda, K):
     g = torch.Generator().manual_seed(77)
     n, Ci, Co, H, W = 16, 320, 1280, 16, 16
@@ -96,7 +116,7 @@ def test_conv_underfilled_grid(cuda, K):
 
 
 @pytest.mark.parametrize("tile,splits", [(1, 1), (2, 1), (1, 3), (2, 5), (0, 0), (3, 1), (4, 1), (6, 1), (6, 3),
-                                         (7, 1), (7, 2)])
+                                         (7, 1), (7, 2), (8, 1)])
 @pytest.mark.parametrize("geglu", [False, True])
 def test_gemm_tile_and_splitk_variants(cuda, K, tile, splits, geglu):
     g = torch.Generator().manual_seed(tile * 10 + splits)

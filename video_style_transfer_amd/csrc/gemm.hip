@@ -507,10 +507,12 @@ static void choose(int M, int N, int K, int geglu, int conv, size_t ws_bytes, in
     else if (t256 >= kCUs / 4) tile = 3;
     else tile = 1;
   }
+  if (tile == 8 && conv) tile = 3;
   if (geglu && (tile == 2 || tile == 6)) tile = 1;
   const int t160 = mb * ((N + 159) / 160);
   const int t192 = ((M + 191) / 192) * ((N + 255) / 256);
-  const int tiles = tile == 1 ? t128 : tile == 2 ? t64 : tile == 3 ? t256 : tile == 6 ? t160 : tile == 7 ? t192 : t256n;
+  const int tiles = tile == 1 ? t128 : tile == 2 ? t64 : (tile == 3 || tile == 8) ? t256 : tile == 6 ? t160
+                    : tile == 7 ? t192 : t256n;
   if (splits == 0) {
     splits = 1;
     if (tiles < kCUs / 2 && nk32 >= 8) {
@@ -518,6 +520,7 @@ static void choose(int M, int N, int K, int geglu, int conv, size_t ws_bytes, in
       if (splits < 2) splits = 1;
     }
   }
+  if (tile == 8) splits = 1;  // the 8-phase kernel has no split-K slab epilogue
   if (splits > nk32) splits = nk32;
   if (splits > 1) {
     const size_t need = (size_t)splits * M * N * sizeof(float);
@@ -527,6 +530,36 @@ static void choose(int M, int N, int K, int geglu, int conv, size_t ws_bytes, in
 }
 
 int launch_gemm_ring(const GemmArgs& a, int amode, int epi, int tile, int splits, hipStream_t s);
+int launch_gemm_p8(const GemmArgs& a, int epi, hipStream_t s);
+
+// 8-phase 256x256x64 kernel (gemm_p8.hip) for plain / LoRA-augmented projections and GEGLU (see p8_auto).
+static int gemm_p8_env() {
+  static int v = -2;
+  if (v == -2) {
+    const char* e = getenv("VST_GEMM_P8");
+    v = e ? atoi(e) : -1;
+  }
+  return v;
+}
+
+// Automatic choice of the 8-phase kernel (tile 0).  Measured in the denoise step (tools/p8_bench.sh, VST_BENCH_SHAPES,
+// one MI355X): it beats the ring on every projection / GEGLU shape with K < 2048 -- the 16x16-level out-projection
+// 8192x1280x1312 9.53 -> 8.55 ms per step, GEGLU 8192x10240x1280 14.29 -> 13.93, the K = 320 shapes of the 64x64
+// level 3-7 % -- and loses 2-6 % at K >= 2048 (ff.net.2), where the ring's 5-stage LDS-DMA lookahead pays.
+// VST_GEMM_P8 = 0 off, 1 every full-grid shape, unset = that rule.
+static bool p8_auto(int M, int N, int K, bool geglu) {
+  (void)geglu;
+  const int e = gemm_p8_env();
+  if (e == 0) return false;
+  const int t256 = ((M + 255) / 256) * ((N + 255) / 256);
+  return t256 >= kCUs / 4 && K >= 128 && (e == 1 || K < 2048);
+}
+
+// tile code 8: AMODE 0, no split-K, a 64-aligned A source split, 256x256 tiles
+static bool p8_applies(int M, int N, int K1, bool two_src) {
+  (void)M; (void)N;
+  return !two_src || (K1 & 63) == 0;
+}
 // Workspace layout (caller-owned, zero-filled once): [split-K slabs | stream-K partial slots ...]
 // followed by kFlagBytes of stream-K flags at the very end (kept zero between launches).
 constexpr size_t kFlagBytes = 4096;
@@ -612,6 +645,11 @@ static int run_gemm(GemmArgs& a, int amode, int geglu, int tile, int splits, hip
   const int pe = gemm_persist_env();
   a.persist = (pe > 0 || (pe < 0 && geglu)) ? device_cus() : 0;
   if (tile == 5) return launch_skinny(a, s);
+  if (tile == 8) {
+    if (amode != 0 || splits > 1) return VST_ERR_ARG;
+    a.splits = 1;
+    return launch_gemm_p8(a, geglu ? 1 : (a.act ? 3 : 0), s);
+  }
   if (amode == 2) {  // scalar-gather conv (conv_in): register-staged kernel, no split
     a.splits = 1;
     return launch_one<2, 0, 64>(a, s, 1);
@@ -656,8 +694,10 @@ extern "C" const char* vst_gemm_kernel_name(int M, int N, int K, int kind, int t
                                        "gemm_ring<256x160,splitk>", "gemm_ring<192x256,splitk>"};
   if (kind == 3) return "gemm_kernel<conv_in>";
   if (kind == 0 && (tile == 5 || (tile == 0 && N <= 64 && M >= 1024))) return "gemm_skinny";  // no-epilogue calls
-  if (kind < 0 || kind > 3 || tile < 0 || tile > 7 || tile == 5 || splits < 0) return "";
+  if (kind < 0 || kind > 3 || tile < 0 || tile > 8 || tile == 5 || splits < 0) return "";
+  if (tile == 0 && kind <= 1 && p8_auto(M, N, K, kind == 1)) tile = 8;
   choose(M, N, K, kind == 1, kind == 2, ws_bytes > kFlagBytes ? ws_bytes - kFlagBytes : 0, tile, splits);
+  if (tile == 8) return kind == 1 ? "gemm_p8<256x256,geglu>" : "gemm_p8<256x256>";
   if (splits > 1) return split_names[tile - 1];
   int it = 0, gr = 0;
   if (tile == 3 && kind != 1 && plan_stream_k(M, N, K, ws_bytes, it, gr))
@@ -681,7 +721,8 @@ extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int
   if (epilogue == 2 && (R || row_bias)) return VST_ERR_ARG;  // GELU: bias only
   if (R && (ldr & 7)) return VST_ERR_ARG;
   if (row_bias && row_bias_div <= 0) return VST_ERR_ARG;
-  if (tile < 0 || tile > 7 || splits < 0) return VST_ERR_ARG;
+  if (tile < 0 || tile > 8 || splits < 0) return VST_ERR_ARG;
+  if (tile == 8 && !p8_applies(M, N, K1, A2 != nullptr)) return VST_ERR_ARG;
   const bool skinny_ok = N <= 64 && !A2 && !bias && !row_bias && !R && epilogue == 0;
   if (tile == 5 && !skinny_ok) return VST_ERR_ARG;
   GemmArgs a{};
@@ -700,6 +741,7 @@ extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int
   if (tile == 0 && skinny_ok && M >= 1024) tile = 5;  // LoRA down-projection: skinny kernel
   if (tile == 5) return run_gemm(a, 0, 0, 5, 1, (hipStream_t)stream);
   const size_t slab_bytes = (workspace && ws_bytes > kFlagBytes) ? ws_bytes - kFlagBytes : 0;
+  if (tile == 0 && splits == 0 && p8_auto(M, N, K, epilogue == 1) && p8_applies(M, N, K1, A2 != nullptr)) tile = 8;
   choose(M, N, K, epilogue == 1, 0, slab_bytes, tile, splits);
   if (slab_bytes) apply_stream_k(a, tile, splits, epilogue == 1 ? 1 : 0, workspace, ws_bytes);
   return run_gemm(a, 0, epilogue == 1, tile, splits, (hipStream_t)stream);

@@ -1,0 +1,126 @@
+// Shared GEMM tile epilogue (gemm_big.hip ring kernel, gemm_p8.hip 8-phase kernel): bias (+GELU), the bf16 tile
+// staged once in LDS, then per-frame row bias / residual add (after that rounding, as the reference's separate add
+// does) or GEGLU, written as full 16-B chunks.  acc[i][j][r] = C[m0 + wr*WM + i*16 + (lane&15)][n0 + wc*WN + j*16 +
+// 4*(lane>>4) + r] (the W fragment is the MFMA's A operand).
+#pragma once
+#include "gemm_common.h"
+
+namespace vst {
+
+template <class Cfg, int EPI>
+__device__ __forceinline__ void tile_epilogue(const GemmArgs& p, char* smem, const int m0, const int n0,
+                                              f32x4 (&acc)[Cfg::MI][Cfg::NJ], const int wr, const int wc) {
+  constexpr int BM = Cfg::BM, BN = Cfg::BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int lrow0 = wr * Cfg::WM + fr;          // + i*16
+  const int lcol0 = wc * Cfg::WN + 4 * fq;      // + j*16
+  constexpr int LROW = BN * 2 + 16;  // staged bf16 row (16-B pad: conflict-light b64 writes)
+  static_assert(BM * LROW <= Cfg::LDS, "epilogue staging must fit in the ring's LDS");
+  constexpr int CPR = BN / 8;  // 16-B output chunks per row
+  constexpr int TOT = BM * CPR;
+  constexpr int ITEMS = (TOT + Cfg::THREADS - 1) / Cfg::THREADS;
+  const auto rr = make_rsrc(p.R ? p.R : p.Wt, p.R ? p.r_bytes : 0u);
+  // residual chunks are fetched first (the fragment registers are dead now): their HBM latency
+  // overlaps the bias add and the LDS staging below instead of stalling the store pass.
+  u32x4 res[EPI == 0 ? ITEMS : 1];
+  if (EPI == 0 && p.R) {
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+      const int idx = tid + k * Cfg::THREADS;
+      const int row = idx / CPR, n = n0 + (idx - row * CPR) * 8, m = m0 + row;
+      res[k] = buf_load16(rr, (idx < TOT && m < p.M && n + 8 <= p.N) ? (m * p.ldr + n) * 2 : kOOB);
+    }
+  }
+  if (p.bias) {
+#pragma unroll
+    for (int j = 0; j < Cfg::NJ; ++j) {
+      const int n = n0 + lcol0 + j * 16;
+      f32x4 b4;
+      if (n + 4 <= p.N) {
+        b4 = *reinterpret_cast<const f32x4*>(p.bias + n);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) b4[e] = n + e < p.N ? p.bias[n + e] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < Cfg::MI; ++i) acc[i][j] += b4;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < Cfg::MI; ++i)
+#pragma unroll
+    for (int j = 0; j < Cfg::NJ; ++j) {
+      f32x4 a4 = acc[i][j];
+      if constexpr (EPI == 3) {  // GELU(erf) of the biased fp32 accumulator, before the bf16 rounding
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a4[e] = gelu_erf(a4[e]);
+      }
+      u32x2 v;
+      v[0] = pack2bf(a4[0], a4[1]);
+      v[1] = pack2bf(a4[2], a4[3]);
+      *reinterpret_cast<u32x2*>(smem + (lrow0 + i * 16) * LROW + (lcol0 + j * 16) * 2) = v;
+    }
+  // publish the staged tile; a raw barrier (no vmcnt drain) keeps the residual loads in flight
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if constexpr (EPI == 0 || EPI == 3) {
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+      const int idx = tid + k * Cfg::THREADS;
+      const int row = idx / CPR, cc = idx - row * CPR;
+      const int m = m0 + row, n = n0 + cc * 8;
+      const int nv = min(8, p.N - n);
+      if (idx >= TOT || m >= p.M || nv <= 0) continue;
+      float v[8];
+      unpack8(*reinterpret_cast<const u32x4*>(smem + row * LROW + cc * 16), v);
+      if (EPI == 0 && p.rbias) {
+        const float* rb = p.rbias + (size_t)(m / p.rbias_div) * p.ldrb + n;
+        if (nv == 8) {
+          const f32x4 r0 = *reinterpret_cast<const f32x4*>(rb);
+          const f32x4 r1 = *reinterpret_cast<const f32x4*>(rb + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { v[e] += r0[e]; v[e + 4] += r1[e]; }
+        } else {
+          for (int e = 0; e < nv; ++e) v[e] += rb[e];
+        }
+      }
+      if (nv == 8) {
+        if (EPI == 0 && p.R) {
+          float r8[8];
+          unpack8(res[k], r8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += r8[e];
+        }
+        *reinterpret_cast<u32x4*>(p.C + (size_t)m * p.ldc + n) = pack8(v);
+      } else {
+        for (int e = 0; e < nv; ++e) {
+          float x = v[e];
+          if (EPI == 0 && p.R) x += bf2f(p.R[(size_t)m * p.ldr + n + e]);
+          p.C[(size_t)m * p.ldc + n + e] = f2bf(x);
+        }
+      }
+    }
+  } else {  // GEGLU: per 64 weight rows [32 hidden | 32 gate] -> 32 outputs, bias already in
+    constexpr int GPR = BN / 16;                // 8-output chunks per row
+    constexpr int RSTEP = Cfg::THREADS / GPR;
+    constexpr int GITEMS = BM / RSTEP;
+    static_assert(Cfg::THREADS % GPR == 0 && BM % RSTEP == 0, "item split");
+    const int oc = tid % GPR, row0 = tid / GPR;
+    const int blk = oc >> 2, c = (oc & 3) * 8;
+    const int nh = n0 + blk * 64 + c;
+#pragma unroll
+    for (int k = 0; k < GITEMS; ++k) {
+      const int row = row0 + k * RSTEP, m = m0 + row;
+      if (m >= p.M || nh >= p.N) continue;
+      float h[8], g[8], v[8];
+      unpack8(*reinterpret_cast<const u32x4*>(smem + row * LROW + (blk * 64 + c) * 2), h);
+      unpack8(*reinterpret_cast<const u32x4*>(smem + row * LROW + (blk * 64 + 32 + c) * 2), g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = h[e] * gelu_erf(g[e]);
+      *reinterpret_cast<u32x4*>(p.C + (size_t)m * p.ldc + (n0 >> 1) + blk * 32 + c) = pack8(v);
+    }
+  }
+}
+
+}  // namespace vst

@@ -1,0 +1,224 @@
+// 8-phase 256x256x64 GEMM (projections / GEGLU FF of the denoise path; same GemmArgs contract and epilogues as the
+// ring kernel in gemm_big.hip, AMODE 0 only: A = [A1 | A2] split at K1, W row-major [N][K]).
+//
+// Why: the ring kernel runs 32-deep k-steps with two barriers per 32 MFMAs per wave; its MFMA + barrier skeleton
+// alone reaches ~60 % of peak.  This kernel takes 64-deep k-tiles, two LDS buffers, and splits each
+// buffer into four half-tile SLOTS so a slot is refilled as soon as its last reader is done, which keeps every
+// operand byte ~6 phases (≈1.5 k-tiles) ahead of its use with 128 KiB of LDS:
+//   slot Amq0 = A rows {0-63, 128-191}   (the first 64-row quadrant of both wave rows)
+//   slot Amq1 = A rows {64-127, 192-255}
+//   slot Bnq0 = W rows {wc*64 + 0..31}   (the first 32 output columns of every wave column)
+//   slot Bnq1 = W rows {wc*64 + 32..63}
+// each [128 rows][64 k] bf16, 128-B rows, 16-B chunk c of row r at (c ^ ((r >> 1) & 7)) (conflict-free
+// ds_read_b128 fragment reads), filled by `buffer_load ... lds` (16 B per lane, lane-linear 1-KiB pieces, the
+// inverse permutation applied to the source address).
+//
+// 8 waves = 2 (M) x 4 (N), wave tile 128 x 64 = 8 x 4 accumulators (16x16).  A k-tile is four phases; phase p
+// multiplies one quadrant of the wave tile (16 MFMAs of 16x16x32):
+//   p0: read A(mq0) + B(nq0), Q(0,0)      p1: read B(nq1), Q(0,1)      p2: read A(mq1), Q(1,1)      p3: Q(1,0)
+// Each phase = {fragment reads, counted vmcnt wait, LDS-DMA issue} barrier {16 MFMAs} barrier; waves 4-7 run one
+// barrier behind waves 0-3, so on every SIMD one wave's MFMAs overlap its partner's reads and DMA issue.
+// DMA of tile t+2 into the buffer of tile t: Amq0 + Bnq0 in p2 of tile t, Bnq1 in p3 of tile t, Amq1 in p0 of
+// tile t+1 -- each slot right after the barrier that retires its last reads (WAR), and each is waited for
+// (s_waitcnt vmcnt(8): exactly 4 younger slots of 2 DMAs each are in flight) one phase before its first read
+// (RAW).  Past the last k-tile the same DMAs are issued with out-of-range offsets (zeros), so the count is the same
+// at every phase; they are drained before the epilogue reuses the LDS.
+#include "gemm_common.h"
+#include "gemm_epilogue.h"
+
+namespace vst {
+
+struct P8Cfg {  // the epilogue's view of the tile (same wave tiling as RingCfg<256, 256, 2, 4, S>)
+  static constexpr int BM = 256, BN = 256, WAVES_M = 2, WAVES_N = 4, NWAVES = 8, THREADS = 512;
+  static constexpr int WM = 128, WN = 64, MI = 8, NJ = 4;
+  static constexpr int SLOT = 128 * 64 * 2;  // 16 KiB
+  static constexpr int BUF = 4 * SLOT;
+  static constexpr int EPI_BYTES = BM * (BN * 2 + 16);
+  static constexpr int LDS = 2 * BUF > EPI_BYTES ? 2 * BUF : EPI_BYTES;
+};
+static_assert(P8Cfg::LDS <= 160 * 1024, "LDS budget");
+
+typedef __attribute__((address_space(3))) void p8_lds_void;
+
+__device__ __forceinline__ void p8_dma16(__amdgpu_buffer_rsrc_t r, char* lds_piece, int off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(
+      r, (p8_lds_void*)((__attribute__((address_space(3))) char*)(uintptr_t)lds_piece), 16, off, 0, 0, 0);
+}
+
+__device__ __forceinline__ int p8_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+
+__device__ __forceinline__ void p8_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int SLOT = P8Cfg::SLOT, BUF = P8Cfg::BUF;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nbm = (p.M + 255) / 256, nbn = (p.N + 255) / 256;
+  int bm, bn;
+  {
+    const int t = xcd_remap(blockIdx.x, nbm * nbn);
+    const int GROUP_M = 8, in_group = GROUP_M * nbn;
+    const int gid = t / in_group, first_m = gid * GROUP_M;
+    const int gsize = min(nbm - first_m, GROUP_M);
+    bm = first_m + (t - gid * in_group) % gsize;
+    bn = (t - gid * in_group) / gsize;
+  }
+  const int m0 = bm * 256, n0 = bn * 256;
+  const auto ra1 = make_rsrc(p.A1, p.a1_bytes);
+  const auto ra2 = make_rsrc(p.A2 ? p.A2 : p.A1, p.A2 ? p.a2_bytes : 0u);
+  const auto rw = make_rsrc(p.Wt, p.w_bytes);
+  const int nk = (p.K + 63) / 64;
+  const bool ktail = (p.K & 63) != 0;
+
+  // ---- per-lane DMA descriptors: slot s in {Amq0, Amq1, Bnq0, Bnq1}, piece pc in {0, 1} = slot rows
+  //      8*(wid + 8*pc) + (lane >> 3); this lane moves chunk c = (lane & 7) ^ ((row >> 1) & 7) of that row.
+  uint32_t base1[4][2], base2[2][2];
+  int c8[4][2];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int pc = 0; pc < 2; ++pc) {
+      const int r = 8 * (wid + 8 * pc) + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      c8[s][pc] = c * 8;
+      if (s < 2) {
+        const int m = m0 + (r >> 6) * 128 + s * 64 + (r & 63);
+        base1[s][pc] = m < p.M ? (uint32_t)(m * p.lda1 + c * 8) * 2u : (uint32_t)kOOB;
+        base2[s][pc] = m < p.M ? (uint32_t)(m * p.lda2 + c * 8) * 2u : (uint32_t)kOOB;
+      } else {
+        const int n = n0 + (r >> 5) * 64 + (s - 2) * 32 + (r & 31);
+        base1[s][pc] = n < p.N ? (uint32_t)(n * p.ldw + c * 8) * 2u : (uint32_t)kOOB;
+      }
+    }
+  // slot s of k-tile kt into buffer (kt & 1); kt >= nk: out-of-range offsets (zeros), keeps vmcnt counts uniform
+  auto dma_slot = [&](int s, int kt) {
+    char* dst = smem + (kt & 1) * BUF + s * SLOT + wid * 1024;
+    const int k0 = kt * 64;
+    const bool live = kt < nk;
+    if (s < 2) {
+      const bool second = k0 >= p.K1;
+      const uint32_t kb = (uint32_t)(second ? k0 - p.K1 : k0) * 2u;
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc) {
+        const bool kin = live && (!ktail || k0 + c8[s][pc] < p.K);
+        const int off = kin ? (int)((second ? base2[s][pc] : base1[s][pc]) + kb) : kOOB;
+        p8_dma16(second ? ra2 : ra1, dst + pc * 8192, off);
+      }
+    } else {
+      const uint32_t kb = (uint32_t)k0 * 2u;
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc) {
+        const bool kin = live && (!ktail || k0 + c8[s][pc] < p.K);
+        p8_dma16(rw, dst + pc * 8192, kin ? (int)(base1[s][pc] + kb) : kOOB);
+      }
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 fa[4][2];         // A fragments of the current row quadrant (mq): 4 x 16 rows x 2 k-halves
+  bf16x8 fb0[2][2], fb1[2][2];  // W fragments of column quadrants nq0 / nq1
+  auto read_a = [&](int buf, int mq) {
+    const char* S = smem + buf * BUF + mq * SLOT;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) fa[i][h] = *reinterpret_cast<const bf16x8*>(S + p8_off(wr * 64 + i * 16 + fr, h * 4 + fq));
+  };
+  auto read_b = [&](int buf, int nq, bf16x8 (&fb)[2][2]) {
+    const char* S = smem + buf * BUF + (2 + nq) * SLOT;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) fb[j][h] = *reinterpret_cast<const bf16x8*>(S + p8_off(wc * 32 + j * 16 + fr, h * 4 + fq));
+  };
+#define VST_P8_QUAD(MQ, NQ, FB)                                                                        \
+  {                                                                                                  \
+    __builtin_amdgcn_s_setprio(1);                                                                   \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j)      \
+        _Pragma("unroll") for (int h = 0; h < 2; ++h) acc[(MQ) * 4 + i][(NQ) * 2 + j] =              \
+        __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j][h], fa[i][h], acc[(MQ) * 4 + i][(NQ) * 2 + j], 0, 0, 0); \
+    __builtin_amdgcn_s_setprio(0);                                                                   \
+  }
+
+  // ---- prologue: k-tile 0 complete, k-tile 1 except Amq1 (issued in phase 0 of tile 0) ----
+  dma_slot(0, 0); dma_slot(2, 0); dma_slot(3, 0); dma_slot(1, 0);
+  dma_slot(0, 1); dma_slot(2, 1); dma_slot(3, 1);
+  asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // Amq0(0), Bnq0(0) landed
+  p8_barrier();
+  const bool late = wid >= 4;
+  if (late) p8_barrier();
+
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    // phase 0: Q(0,0)
+    read_a(buf, 0);
+    read_b(buf, 0, fb0);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Bnq1(t) landed
+    dma_slot(1, t + 1);
+    p8_barrier();
+    VST_P8_QUAD(0, 0, fb0)
+    p8_barrier();
+    // phase 1: Q(0,1)
+    read_b(buf, 1, fb1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Amq1(t) landed
+    p8_barrier();
+    VST_P8_QUAD(0, 1, fb1)
+    p8_barrier();
+    // phase 2: Q(1,1)
+    read_a(buf, 1);
+    dma_slot(0, t + 2);
+    dma_slot(2, t + 2);
+    p8_barrier();
+    VST_P8_QUAD(1, 1, fb1)
+    p8_barrier();
+    // phase 3: Q(1,0)
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Amq0(t+1), Bnq0(t+1) landed
+    dma_slot(3, t + 2);
+    p8_barrier();
+    VST_P8_QUAD(1, 0, fb0)
+    p8_barrier();
+  }
+#undef VST_P8_QUAD
+  if (!late) p8_barrier();
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the trailing zero DMAs land before LDS reuse
+  p8_barrier();
+  tile_epilogue<P8Cfg, EPI>(p, smem, m0, n0, acc, wr, wc);
+}
+
+template <int EPI>
+static int launch_p8_epi(const GemmArgs& a, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_p8_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              P8Cfg::LDS);
+    attr = true;
+  }
+  const int nwg = ((a.M + 255) / 256) * ((a.N + 255) / 256);
+  hipLaunchKernelGGL((gemm_p8_kernel<EPI>), dim3(nwg), dim3(512), P8Cfg::LDS, s, a);
+  return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+}
+
+// epi: 0 bias / row bias / residual, 1 GEGLU, 3 bias + GELU
+int launch_gemm_p8(const GemmArgs& a, int epi, hipStream_t s) {
+  if (a.A2 && (a.K1 & 63)) return VST_ERR_ARG;  // a 64-deep k-tile must not straddle the two A sources
+  switch (epi) {
+    case 0: return launch_p8_epi<0>(a, s);
+    case 1: return launch_p8_epi<1>(a, s);
+    case 3: return launch_p8_epi<3>(a, s);
+    default: return VST_ERR_ARG;
+  }
+}
+
+}  // namespace vst
