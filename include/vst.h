@@ -161,7 +161,8 @@ int vst_spatial_attention_bwd(const void* q, int ldq, const void* k, const void*
 int vst_zero_insert(const void* x, int nimg, int h, int w, int C, void* y, void* stream);
 int vst_sumpool2x2(const void* x, int nimg, int h, int w, int C, void* y, void* stream);
 /* vst_temporal_attention_bwd: gradients of vst_temporal_attention (same token layout and q/k/v views) from dO; dq/dk/dv
- * are written with row stride lddqkv (e.g. column views of one [tokens, 3C] buffer).  F <= 32, head_dim <= 256. */
+ * are written with row stride lddqkv (e.g. column views of one [tokens, 3C] buffer).  F <= 32, head_dim one of
+ * 8/16/32/40/64/80/160 (the forward's set; SDXL motion modules: 40/80/160), MFMA tiles as the forward. */
 int vst_temporal_attention_bwd(const void* q, const void* k, const void* v, int ldqkv, const void* dout, int lddo,
                                void* dq, void* dk, void* dv, int lddqkv, int nclip, int F, int HW, int heads,
                                int head_dim, float scale, void* stream);

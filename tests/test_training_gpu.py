@@ -144,7 +144,8 @@ def test_geglu_fn_grads(cuda, M, C, Nh):
         assert e < 2e-2, (name, e)
 
 
-@pytest.mark.parametrize("nclip,Fr,HW,C", [(2, 16, 8, 320), (1, 32, 4, 640), (1, 16, 2, 1280), (3, 5, 7, 64)])
+@pytest.mark.parametrize("nclip,Fr,HW,C", [(2, 16, 8, 320), (1, 32, 4, 640), (1, 16, 2, 1280), (3, 5, 7, 64),
+                                           (1, 32, 4, 1280), (2, 24, 3, 128), (1, 16, 5, 512)])
 def test_temporal_attention_fn_grads(cuda, nclip, Fr, HW, C):
     import math
     from video_style_transfer_amd.autograd import TemporalAttentionFn

@@ -48,6 +48,12 @@ def main():
                                                  out=out))
         by = 2.0 * 4 * nclip * Fr * HW * C
         print(json.dumps({"shape": name, "us": round(ms * 1e3, 1), "gbs": round(by / ms / 1e6, 1)}), flush=True)
+        dout = torch.randn(nclip * Fr * HW, C, device=dev).to(BF)
+        grad = torch.empty(nclip * Fr * HW, 3 * C, device=dev, dtype=BF)
+        ms = timeit(lambda: K.temporal_attention_bwd(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], dout, nclip, Fr, HW,
+                                                     8, C // 8, out=grad))
+        by = 2.0 * 7 * nclip * Fr * HW * C
+        print(json.dumps({"shape": name + "_bwd", "us": round(ms * 1e3, 1), "gbs": round(by / ms / 1e6, 1)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -11,6 +11,11 @@ from video_style_transfer_amd import kernels as K  # noqa: E402
 
 BF = torch.bfloat16
 SHAPES = [  # name, M, N, K1, K2, geglu, residual, bias
+    ("tr1280_out_lora", 4096, 1280, 1280, 32, False, True, True),
+    ("tr1280_ff2", 4096, 1280, 5120, 0, False, True, True),
+    ("tr1280_dx", 4096, 1280, 1280, 0, False, False, False),
+    ("tr1280_dw", 1280, 1280, 4096, 0, False, False, False),
+    ("tr1280_dx_ff", 4096, 5120, 1280, 0, False, False, False),
     ("sp1280_out_lora", 8192, 1280, 1280, 32, False, True, True),
     ("sp1280_ff2", 8192, 1280, 5120, 0, False, True, True),
     ("sp1280_proj", 8192, 1280, 1280, 0, False, False, True),
@@ -20,15 +25,15 @@ SHAPES = [  # name, M, N, K1, K2, geglu, residual, bias
     ("sp640_ff2", 32768, 640, 2560, 0, False, True, True),
     ("mm320_ff2", 131072, 320, 1280, 0, False, True, True),
 ]
-TILES = [3, 4, 6, 7, 8]
+TILES = [(0, 0), (8, 1), (3, 1), (3, 0), (1, 1), (1, 0), (4, 1), (4, 0), (6, 1), (7, 1)]  # (tile, splits), 0 = auto
 
 
 def run(x, x2, w, b, r, geglu, tile):
-    K.GEMM_POLICY["tile"] = tile
+    K.GEMM_POLICY["tile"], K.GEMM_POLICY["splits"] = tile
     try:
         return K.linear(x, w, b, x2=x2, residual=r, geglu=geglu)
     finally:
-        K.GEMM_POLICY["tile"] = 0
+        K.GEMM_POLICY["tile"], K.GEMM_POLICY["splits"] = 0, 0
 
 
 def timeit(fn, iters=20):
@@ -54,19 +59,19 @@ def main():
         w = (torch.randn(N, Kt, device=dev, generator=g) * Kt ** -0.5).to(BF)
         b = torch.randn(N, device=dev, generator=g) * 0.1 if bias else None
         r = torch.randn(M, N, device=dev, generator=g).to(BF) if res else None
-        ref = run(x, x2, w, b, r, geglu, 3).float()
+        ref = run(x, x2, w, b, r, geglu, (3, 1)).float()
         fl = 2.0 * M * N * Kt
         best = {}
         for rnd in range(3):
             for t in TILES:
-                if t == 8 and K2 and (K1 % 64):
+                if t[0] == 8 and K2 and (K1 % 64):
                     continue
                 us = timeit(lambda: run(x, x2, w, b, r, geglu, t)) * 1e3
                 best[t] = min(best.get(t, 1e9), us)
         errs = {t: ((run(x, x2, w, b, r, geglu, t).float() - ref).norm() / ref.norm()).item() for t in best}
-        line = "  ".join(f"t{t}:{us:7.1f}us {fl / us / 1e6:6.1f}TF" + ("" if errs[t] < 1e-2 else f"(ERR {errs[t]:.1e})")
+        line = "  ".join(f"t{t[0]}s{t[1]}:{us:6.1f}us {fl / us / 1e6:6.1f}TF" + ("" if errs[t] < 1e-2 else f"(ERR {errs[t]:.1e})")
                          for t, us in best.items())
-        print(f"{name:16s} {M}x{N}x{Kt}  {line}", flush=True)
+        print(f"{name:16s} {M}x{N}x{Kt} auto={K.gemm_kernel_name(M, N, Kt, 1 if geglu else 0)}\n   {line}", flush=True)
 
 
 if __name__ == "__main__":

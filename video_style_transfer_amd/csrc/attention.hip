@@ -361,76 +361,202 @@ __global__ __launch_bounds__(512) void temporal_attn_kernel(
 }
 
 
-// Temporal attention backward (training path): one wave per (clip, pixel, head), F <= 32.
-// q/k/v/dO rows are staged in LDS (fp32), then with P = softmax(scale Q K^T) recomputed:
-//   dP = dO V^T,  D_i = sum_j P_ij dP_ij,  dS = P * (dP - D),  dQ = scale dS K,  dK = scale dS^T Q,  dV = P^T dO.
-// Scalar VALU (the F x F x d work per unit is small; the kernel is HBM-bound on q/k/v/dO in, dq/dk/dv out).
-__global__ __launch_bounds__(64) void temporal_attn_bwd_kernel(
+// Temporal attention backward (training path): one wave per (clip, pixel, head), F <= 32, on the
+// forward's v_mfma_f32_16x16x32_bf16 tiles.  P = softmax(scale Q K^T) is recomputed; with dP = dO V^T,
+// D_i = sum_j P_ij dP_ij and dS = P * (dP - D):  dQ = scale dS K,  dK = scale dS^T Q,  dV = P^T dO.
+// The three products need the score tiles with the query as the accumulator column (dQ^T = K^T dS^T) and with the key
+// as the column (dK^T = Q^T dS, dV^T = dO^T P), so S and dP are formed both ways from the same row fragments
+// (swapping the MFMA operands); the softmax statistics live in the transposed (query-column) tiles and reach the
+// key-column tiles by one ds_bpermute per row.  The d-major A operands (K^T, Q^T, dO^T) come from ds_read_b64_tr_b16
+// reads of the wave's own LDS copy of those rows, exactly like the forward's V^T.
+template <int NT, int D>
+__global__ __launch_bounds__(512) void temporal_attn_bwd_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V, int ldqkv,
     const bf16_t* __restrict__ dO, int lddo, bf16_t* __restrict__ dQ, bf16_t* __restrict__ dK,
-    bf16_t* __restrict__ dV, int lddqkv, int nclip, int F, int HW, int heads, int D, float scale) {
-  extern __shared__ float tsm[];
-  float* qs = tsm;                 // [F][D]
-  float* ks = qs + F * D;
-  float* vs = ks + F * D;
-  float* os = vs + F * D;          // dO
-  float* P = os + F * D;           // [F][F]
-  float* dS = P + F * F;           // [F][F]
-  float* Dv = dS + F * F;          // [F]
-  const int lane = threadIdx.x;
-  const int unit = blockIdx.x;
-  const int h = unit % heads, bp = unit / heads;
+    bf16_t* __restrict__ dV, int lddqkv, int nclip, int F, int HW, int heads, float scale, float scale_log2,
+    uint32_t qkv_bytes, uint32_t do_bytes) {
+  constexpr int KS = (D + 31) / 32;  // 32-deep k-steps over d
+  constexpr int DB = (D + 15) / 16;  // 16-wide d blocks of the outputs
+  constexpr int NF = 16 * NT;
+  constexpr int VROW = DB * 32;      // bytes per staged row
+  constexpr int CPR = VROW / 16;
+  constexpr int ARR = NF * VROW;     // one staged operand
+  extern __shared__ __attribute__((aligned(16))) char tbm[];  // [waves][K, Q, dO][NF * VROW]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int unit = blockIdx.x * (blockDim.x >> 6) + wid;
+  if (unit >= nclip * HW * heads) return;  // whole wave exits (unit is wave-uniform); no workgroup barriers below
+  const int h = unit % heads;
+  const int bp = unit / heads;
   const int b = bp / HW, p = bp - b * HW;
-  auto row = [&](int f) { return (size_t)((b * F + f) * HW + p); };
-  for (int idx = lane; idx < F * D; idx += 64) {
-    const int f = idx / D, d = idx - f * D;
-    const size_t o = row(f) * ldqkv + h * D + d;
-    qs[idx] = bf2f(Q[o]);
-    ks[idx] = bf2f(K[o]);
-    vs[idx] = bf2f(V[o]);
-    os[idx] = bf2f(dO[row(f) * lddo + h * D + d]);
+  const int fr = lane & 15, g = lane >> 4;
+  const auto rq = make_rsrc(Q, qkv_bytes);
+  const auto rk = make_rsrc(K, qkv_bytes);
+  const auto rv = make_rsrc(V, qkv_bytes);
+  const auto ro = make_rsrc(dO, do_bytes);
+  auto row_of = [&](int f) { return (b * F + f) * HW + p; };
+
+  // ---- stage K, Q, dO rows (zero rows >= F, columns >= D) for the transposed reads ----
+  char* ks = tbm + wid * 3 * ARR;
+  char* qs = ks + ARR;
+  char* os = qs + ARR;
+  for (int idx = lane; idx < NF * CPR; idx += 64) {
+    const int f = idx / CPR, c = idx - f * CPR;
+    const bool in = f < F && c * 8 < D;
+    const int off = in ? (row_of(f) * ldqkv + h * D + c * 8) * 2 : kOOB;
+    const int ooff = in ? (row_of(f) * lddo + h * D + c * 8) * 2 : kOOB;
+    *reinterpret_cast<u32x4*>(ks + f * VROW + c * 16) = buf_load16(rk, off);
+    *reinterpret_cast<u32x4*>(qs + f * VROW + c * 16) = buf_load16(rq, off);
+    *reinterpret_cast<u32x4*>(os + f * VROW + c * 16) = buf_load16(ro, ooff);
   }
-  __syncthreads();
-  for (int idx = lane; idx < F * F; idx += 64) {
-    const int i = idx / F, j = idx - i * F;
-    float sq = 0.f, sp = 0.f;
-    for (int d = 0; d < D; ++d) {
-      sq += qs[i * D + d] * ks[j * D + d];
-      sp += os[i * D + d] * vs[j * D + d];
+
+  // ---- scores both ways: st = S^T [key][query], sn = S [query][key]; dpt = dP^T, dpn = dP ----
+  f32x4 st[NT][NT], sn[NT][NT], dpt[NT][NT], dpn[NT][NT];
+#pragma unroll
+  for (int a = 0; a < NT; ++a)
+#pragma unroll
+    for (int c = 0; c < NT; ++c) {
+      st[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+      sn[a][c] = st[a][c];
+      dpt[a][c] = st[a][c];
+      dpn[a][c] = st[a][c];
     }
-    P[idx] = sq * scale;
-    dS[idx] = sp;  // dP for now
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    const int d0 = kk * 32 + g * 8;
+    bf16x8 kf[NT], qf[NT], vf[NT], of[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+      const int f = tt * 16 + fr;
+      const bool in = f < F && d0 < D;
+      const int off = in ? (row_of(f) * ldqkv + h * D + d0) * 2 : kOOB;
+      const int ooff = in ? (row_of(f) * lddo + h * D + d0) * 2 : kOOB;
+      kf[tt] = __builtin_bit_cast(bf16x8, buf_load16(rk, off));
+      qf[tt] = __builtin_bit_cast(bf16x8, buf_load16(rq, off));
+      vf[tt] = __builtin_bit_cast(bf16x8, buf_load16(rv, off));
+      of[tt] = __builtin_bit_cast(bf16x8, buf_load16(ro, ooff));
+    }
+#pragma unroll
+    for (int a = 0; a < NT; ++a)
+#pragma unroll
+      for (int c = 0; c < NT; ++c) {
+        st[a][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[a], qf[c], st[a][c], 0, 0, 0);
+        sn[a][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[a], kf[c], sn[a][c], 0, 0, 0);
+        dpt[a][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[a], of[c], dpt[a][c], 0, 0, 0);
+        dpn[a][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(of[a], vf[c], dpn[a][c], 0, 0, 0);
+      }
   }
-  __syncthreads();
-  if (lane < F) {
-    const int i = lane;
-    float m = -INFINITY;
-    for (int j = 0; j < F; ++j) m = fmaxf(m, P[i * F + j]);
-    float l = 0.f;
-    for (int j = 0; j < F; ++j) { const float e = __expf(P[i * F + j] - m); P[i * F + j] = e; l += e; }
-    const float inv = 1.0f / l;
+  // mask keys >= F: rows of st, columns (whole lanes) of sn
+#pragma unroll
+  for (int a = 0; a < NT; ++a)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (a * 16 + g * 4 + i >= F) {
+#pragma unroll
+        for (int c = 0; c < NT; ++c) st[a][c][i] = -INFINITY;
+      }
+#pragma unroll
+  for (int c = 0; c < NT; ++c)
+    if (c * 16 + fr >= F) {
+#pragma unroll
+      for (int a = 0; a < NT; ++a) sn[a][c] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    }
+
+  // ---- softmax statistics per query column; P^T and dS^T = P^T (dP^T - D) in place ----
+  float mb[NT], inv[NT], dd[NT];
+#pragma unroll
+  for (int c = 0; c < NT; ++c) {
+    float mx = -INFINITY;
+#pragma unroll
+    for (int a = 0; a < NT; ++a)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) mx = fmaxf(mx, st[a][c][i]);
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    mb[c] = mx * scale_log2;
+    float ls = 0.f;
+#pragma unroll
+    for (int a = 0; a < NT; ++a)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float e = fast_exp2(st[a][c][i] * scale_log2 - mb[c]);
+        st[a][c][i] = e;
+        ls += e;
+      }
+    ls += __shfl_xor(ls, 16);
+    ls += __shfl_xor(ls, 32);
+    inv[c] = 1.0f / ls;
     float di = 0.f;
-    for (int j = 0; j < F; ++j) { P[i * F + j] *= inv; di += P[i * F + j] * dS[i * F + j]; }
-    Dv[i] = di;
+#pragma unroll
+    for (int a = 0; a < NT; ++a)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        st[a][c][i] *= inv[c];
+        di += st[a][c][i] * dpt[a][c][i];
+      }
+    di += __shfl_xor(di, 16);
+    di += __shfl_xor(di, 32);
+    dd[c] = di;
+#pragma unroll
+    for (int a = 0; a < NT; ++a)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dpt[a][c][i] = st[a][c][i] * (dpt[a][c][i] - di);
   }
-  __syncthreads();
-  for (int idx = lane; idx < F * F; idx += 64) {
-    const int i = idx / F;
-    dS[idx] = P[idx] * (dS[idx] - Dv[i]);
-  }
-  __syncthreads();
-  for (int idx = lane; idx < F * D; idx += 64) {
-    const int f = idx / D, d = idx - f * D;
-    float gq = 0.f, gk = 0.f, gv = 0.f;
-    for (int j = 0; j < F; ++j) {
-      gq += dS[f * F + j] * ks[j * D + d];   // row f of dS
-      gk += dS[j * F + f] * qs[j * D + d];   // column f of dS
-      gv += P[j * F + f] * os[j * D + d];    // column f of P
+  // ---- key-column tiles: row (query) 16a + 4g + i takes its statistics from lane 4g + i ----
+#pragma unroll
+  for (int a = 0; a < NT; ++a)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int src = g * 4 + i;
+      const float m = __shfl(mb[a], src), iv = __shfl(inv[a], src), di = __shfl(dd[a], src);
+#pragma unroll
+      for (int c = 0; c < NT; ++c) {
+        const float pv = fast_exp2(sn[a][c][i] * scale_log2 - m) * iv;
+        sn[a][c][i] = pv;
+        dpn[a][c][i] = pv * (dpn[a][c][i] - di);
+      }
     }
-    const size_t o = row(f) * lddqkv + h * D + d;
-    dQ[o] = f2bf(gq * scale);
-    dK[o] = f2bf(gk * scale);
-    dV[o] = f2bf(gv);
+
+  // ---- B operands (32-deep k = the 16 or 32 frames; upper half zero for NT = 1) ----
+  bf16x8 bq[NT], bk[NT], bv[NT];
+#pragma unroll
+  for (int c = 0; c < NT; ++c) {
+    const int a1 = NT - 1;
+    const float z = NT == 2 ? 1.f : 0.f;
+    bq[c] = pack_p8(dpt[0][c][0], dpt[0][c][1], dpt[0][c][2], dpt[0][c][3], z * dpt[a1][c][0], z * dpt[a1][c][1],
+                    z * dpt[a1][c][2], z * dpt[a1][c][3]);
+    bk[c] = pack_p8(dpn[0][c][0], dpn[0][c][1], dpn[0][c][2], dpn[0][c][3], z * dpn[a1][c][0], z * dpn[a1][c][1],
+                    z * dpn[a1][c][2], z * dpn[a1][c][3]);
+    bv[c] = pack_p8(sn[0][c][0], sn[0][c][1], sn[0][c][2], sn[0][c][3], z * sn[a1][c][0], z * sn[a1][c][1],
+                    z * sn[a1][c][2], z * sn[a1][c][3]);
+  }
+  // the staging stores (this wave only) complete before the transposed reads
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+
+  // ---- dQ^T = K^T dS^T, dK^T = Q^T dS, dV^T = dO^T P, per 16-wide d block ----
+  const int li = lane & 15;
+  const int r0 = g * 4 + (li >> 2);
+#pragma unroll
+  for (int db = 0; db < DB; ++db) {
+    const int colb = (db * 16 + (li & 3) * 4) * 2;
+    const s16x4 z4{0, 0, 0, 0};
+    const bf16x8 kT = cat_tr(ds_read_tr(ks + r0 * VROW + colb), NT == 2 ? ds_read_tr(ks + (r0 + 16) * VROW + colb) : z4);
+    const bf16x8 qT = cat_tr(ds_read_tr(qs + r0 * VROW + colb), NT == 2 ? ds_read_tr(qs + (r0 + 16) * VROW + colb) : z4);
+    const bf16x8 oT = cat_tr(ds_read_tr(os + r0 * VROW + colb), NT == 2 ? ds_read_tr(os + (r0 + 16) * VROW + colb) : z4);
+    const int d = db * 16 + g * 4;
+#pragma unroll
+    for (int c = 0; c < NT; ++c) {
+      const f32x4 z{0.f, 0.f, 0.f, 0.f};
+      const f32x4 gq = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kT, bq[c], z, 0, 0, 0) * scale;
+      const f32x4 gk = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qT, bk[c], z, 0, 0, 0) * scale;
+      const f32x4 gv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oT, bv[c], z, 0, 0, 0);
+      const int f = c * 16 + fr;
+      if (f < F && d < D) {
+        const size_t o = (size_t)row_of(f) * lddqkv + h * D + d;
+        *reinterpret_cast<u32x2*>(dQ + o) = u32x2{pack2bf(gq[0], gq[1]), pack2bf(gq[2], gq[3])};
+        *reinterpret_cast<u32x2*>(dK + o) = u32x2{pack2bf(gk[0], gk[1]), pack2bf(gk[2], gk[3])};
+        *reinterpret_cast<u32x2*>(dV + o) = u32x2{pack2bf(gv[0], gv[1]), pack2bf(gv[2], gv[3])};
+      }
+    }
   }
 }
 
@@ -844,17 +970,40 @@ extern "C" int vst_temporal_attention(const void* q, const void* k, const void* 
 extern "C" int vst_temporal_attention_bwd(const void* q, const void* k, const void* v, int ldqkv, const void* dout,
                                           int lddo, void* dq, void* dk, void* dv, int lddqkv, int nclip, int F, int HW,
                                           int heads, int head_dim, float scale, void* stream) {
-  if (!q || !k || !v || !dout || !dq || !dk || !dv || nclip <= 0 || F <= 0 || F > 32 || HW <= 0 || heads <= 0 ||
-      head_dim <= 0 || head_dim > 256)
+  if (!q || !k || !v || !dout || !dq || !dk || !dv || nclip <= 0 || F <= 0 || F > 32 || HW <= 0 || heads <= 0)
     return VST_ERR_ARG;
+  if ((ldqkv & 7) || (lddo & 7) || (lddqkv & 3) || (head_dim & 7)) return VST_ERR_ARG;
   const size_t units = (size_t)nclip * HW * heads;
   if (units > 0x7fffffffULL) return VST_ERR_ARG;
-  const size_t lds = (size_t)(4 * F * head_dim + 2 * F * F + F) * sizeof(float);
-  if (lds > 64 * 1024) return VST_ERR_ARG;
-  hipLaunchKernelGGL(temporal_attn_bwd_kernel, dim3((unsigned)units), dim3(64), lds, (hipStream_t)stream,
-                     (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ldqkv, (const bf16_t*)dout, lddo,
-                     (bf16_t*)dq, (bf16_t*)dk, (bf16_t*)dv, lddqkv, nclip, F, HW, heads, head_dim, scale);
-  return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+  const uint32_t qkvb = clampb(((size_t)(nclip * F * HW - 1) * ldqkv + heads * head_dim) * 2);
+  const uint32_t dob = clampb(((size_t)(nclip * F * HW - 1) * lddo + heads * head_dim) * 2);
+  const float sl2 = scale * 1.4426950408889634f;
+  hipStream_t s = (hipStream_t)stream;
+  const bf16_t *Q = (const bf16_t*)q, *K = (const bf16_t*)k, *V = (const bf16_t*)v, *G = (const bf16_t*)dout;
+  bf16_t *GQ = (bf16_t*)dq, *GK = (bf16_t*)dk, *GV = (bf16_t*)dv;
+  auto launch = [&](auto kern, int nf, int D) {
+    const int wave_bytes = 3 * nf * ((D + 15) / 16) * 32;  // K, Q, dO rows
+    // all heads of a (clip, pixel) in one workgroup when they fit in 64 KiB, else as many units as do
+    const int wpg = heads * wave_bytes <= 64 * 1024 ? std::min(heads, 8) : std::max(1, 64 * 1024 / wave_bytes);
+    hipLaunchKernelGGL(kern, dim3((unsigned)((units + wpg - 1) / wpg)), dim3(64 * wpg), wpg * wave_bytes, s, Q, K, V,
+                       ldqkv, G, lddo, GQ, GK, GV, lddqkv, nclip, F, HW, heads, scale, sl2, qkvb, dob);
+    return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+  };
+#define VST_TAB(D)                                                                              \
+  case D:                                                                                       \
+    return F <= 16 ? launch(temporal_attn_bwd_kernel<1, D>, 16, D) : launch(temporal_attn_bwd_kernel<2, D>, 32, D);
+  switch (head_dim) {
+    VST_TAB(8)
+    VST_TAB(16)
+    VST_TAB(32)
+    VST_TAB(40)
+    VST_TAB(64)
+    VST_TAB(80)
+    VST_TAB(160)
+    default:
+      return VST_ERR_ARG;
+  }
+#undef VST_TAB
 }
 
 // D = dO . O per query (written by the dQ kernel, read by the dK/dV kernel)

@@ -502,9 +502,11 @@ static void choose(int M, int N, int K, int geglu, int conv, size_t ws_bytes, in
   // quarter-wave of tiles, including the under-filled M = 8192, N = 1280 grids (160 tiles on 256 CUs:
   // 38 us vs 56 us for 192x256 at K = 1312, 116 vs 190 us at K = 5120; whole step 88.6 vs 92.9 ms);
   // tiny-M GEMMs (text states, temb) use 128x128 with split-K; conv_out (Cout = 4) 128x64.
+  // Below half a wave of 256x256 tiles (the training step's 16x16 level: M = 4096, N = 1280 -> 80 tiles) the
+  // 128x128 tile's 4x larger grid wins (tools/tile_ab.py: 4096x1280x1312 44.6 -> 30.7 us, x5120 112 -> 82 us).
   if (tile == 0) {
     if (conv && N <= 64) tile = 2;
-    else if (t256 >= kCUs / 4) tile = 3;
+    else if (t256 >= kCUs / 2) tile = 3;
     else tile = 1;
   }
   if (tile == 8 && conv) tile = 3;
@@ -552,7 +554,7 @@ static bool p8_auto(int M, int N, int K, bool geglu) {
   const int e = gemm_p8_env();
   if (e == 0) return false;
   const int t256 = ((M + 255) / 256) * ((N + 255) / 256);
-  return t256 >= kCUs / 4 && K >= 128 && (e == 1 || K < 2048);
+  return t256 >= kCUs / 2 && K >= 128 && (e == 1 || K < 2048);
 }
 
 // tile code 8: AMODE 0, no split-K, a 64-aligned A source split, 256x256 tiles
