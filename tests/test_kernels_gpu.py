@@ -6,6 +6,8 @@ We assert max|err| / max|ref| <= 1e-2 and rel-L2 <= 5e-3 per op.
 """
 import math
 
+import os
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -104,6 +106,41 @@ def test_gemm_8phase_bitwise_equals_ring(cuda, K, M, N, K1, K2, geglu):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("M,N,K1,K2,geglu", [(8192, 1280, 1280, 32, False), (8192, 1280, 5120, 0, False),
+                                             (6000, 1504, 640, 64, False), (4608, 2560, 1280, 0, True),
+                                             (7000, 1280, 256, 0, False)])
+def test_gemm_8phase_stream_k(cuda, K, M, N, K1, K2, geglu):
+    """(Opt-in, VST_P8_SK=1; skipped otherwise.)  Stream-K 8-phase GEMM (one workgroup per CU over equal k-shares, partial tiles summed by their owner) on
+    one-partial-round grids: equals the plain 8-phase tiling up to fp32 reassociation, is bitwise reproducible from
+    launch to launch (fixed summation order; the flags reset themselves), and leaves the flags zero."""
+    if os.environ.get("VST_P8_SK", "0") == "0":
+        pytest.skip("stream-K 8-phase GEMM is opt-in (VST_P8_SK=1)")
+    g = torch.Generator().manual_seed(M + N + K1 + 7)
+    x, x2 = rnd(M, K1, gen=g).to(cuda), (rnd(M, K2, gen=g).to(cuda) if K2 else None)
+    w = rnd(N, K1 + K2, scale=(K1 + K2) ** -0.5, gen=g).to(cuda)
+    b = torch.randn(N, generator=g).to(cuda)
+    r = None if geglu else rnd(M, N, gen=g).to(cuda)
+    kind = 1 if geglu else 0
+    outs = {}
+    for splits in (1, 0, 0):
+        K.GEMM_POLICY.update(tile=8, splits=splits)
+        try:
+            name = K.gemm_kernel_name(M, N, K1 + K2, kind)
+            assert ("streamk" in name) == (splits == 0), name
+            outs.setdefault(splits, []).append(K.linear(x, w, b, x2=x2, residual=r, geglu=geglu))
+        finally:
+            K.GEMM_POLICY.update(tile=0, splits=0)
+    plain, sk0, sk1 = outs[1][0], outs[0][0], outs[0][1]
+    assert torch.equal(sk0, sk1)
+    check(sk0, plain.float(), name="stream-K vs plain")
+    xx = x.float() if x2 is None else torch.cat([x, x2], 1).float()
+    h = xx @ w.float().t() + b
+    if not geglu:
+        check(sk0, h + r.float(), name="stream-K vs fp32")
+    ws = K._workspace(x.device)
+    assert int(ws.view(torch.int32)[-1024:].abs().sum()) == 0
+
+
 def test_conv_underfilled_grid(cuda, K):
     g = torch.Generator().manual_seed(77)
     n, Ci, Co, H, W = 16, 320, 1280, 16, 16
@@ -117,7 +154,7 @@ def test_conv_underfilled_grid(cuda, K):
 
 
 @pytest.mark.parametrize("tile,splits", [(1, 1), (2, 1), (1, 3), (2, 5), (0, 0), (3, 1), (4, 1), (6, 1), (6, 3),
-                                         (7, 1), (7, 2), (8, 1)])
+                                         (7, 1), (7, 2), (8, 1), (8, 0)])
 @pytest.mark.parametrize("geglu", [False, True])
 def test_gemm_tile_and_splitk_variants(cuda, K, tile, splits, geglu):
     g = torch.Generator().manual_seed(tile * 10 + splits)

@@ -548,13 +548,20 @@ static int gemm_p8_env() {
 // one MI355X): it beats the ring on every projection / GEGLU shape with K < 2048 -- the 16x16-level out-projection
 // 8192x1280x1312 9.53 -> 8.55 ms per step, GEGLU 8192x10240x1280 14.29 -> 13.93, the K = 320 shapes of the 64x64
 // level 3-7 % -- and loses 2-6 % at K >= 2048 (ff.net.2), where the ring's 5-stage LDS-DMA lookahead pays.
-// VST_GEMM_P8 = 0 off, 1 every full-grid shape, unset = that rule.
+// VST_GEMM_P8 = 0 off, 1 every full-grid shape, unset = that rule (plus any K when stream-K applies, below).
+static int device_cus();
+static bool p8_sk_on();
+static bool p8_sk_shape(int M, int N, int K) {
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256), cus = device_cus();
+  return p8_sk_on() && tiles < cus && 2 * tiles >= cus && (K + 63) / 64 >= 4 &&
+         (long long)tiles * ((K + 63) / 64) < (1LL << 30) && cus * (int)sizeof(int) <= 4096;
+}
 static bool p8_auto(int M, int N, int K, bool geglu) {
   (void)geglu;
   const int e = gemm_p8_env();
   if (e == 0) return false;
   const int t256 = ((M + 255) / 256) * ((N + 255) / 256);
-  return t256 >= kCUs / 2 && K >= 128 && (e == 1 || K < 2048);
+  return t256 >= kCUs / 2 && K >= 128 && (e == 1 || K < 2048 || p8_sk_shape(M, N, K));
 }
 
 // tile code 8: AMODE 0, no split-K, a 64-aligned A source split, 256x256 tiles
@@ -599,6 +606,29 @@ static bool plan_stream_k(int M, int N, int K, size_t ws_bytes, int& iters, int&
   iters = (int)((total + cus - 1) / cus);
   grid = cus;
   return true;
+}
+
+// Stream-K for the 8-phase kernel (gemm_p8.hip): one partial round of 256x256 tiles (half or more of the CUs, fewer
+// tiles than CUs: the 16x16 level's M = 8192, N = 1280 grids) runs on one workgroup per CU over equal k-shares.
+// Opt-in (VST_P8_SK=1): measured slower in the denoise step (tools/p8_bench.sh: 8192x1280x1312 8.56 -> 11.1 ms per
+// step, 8192x1280x5120 8.69 (ring) -> 9.51 ms).  At K = 1312 a tile's operands are 1.3 MB while each split tile adds
+// ~0.8 MB of fp32 partial traffic (written + read back), and every share pays two pipeline fills for ~13 k-tiles.
+static bool p8_sk_on() {
+  static int v = -2;
+  if (v == -2) {
+    const char* e = getenv("VST_P8_SK");
+    v = e ? atoi(e) : 0;
+  }
+  return v != 0;
+}
+
+static void apply_p8_sk(GemmArgs& a, void* ws, size_t ws_bytes) {
+  const int cus = device_cus();
+  if (!ws || !p8_sk_shape(a.M, a.N, a.K)) return;
+  if (ws_bytes < (size_t)cus * 256 * 256 * sizeof(float) + kFlagBytes) return;
+  a.sk_grid = cus;
+  a.sk_ws = (float*)ws;
+  a.sk_flags = (int*)((char*)ws + ws_bytes - kFlagBytes);
 }
 
 static void apply_stream_k(GemmArgs& a, int tile, int splits, int epi, void* ws, size_t ws_bytes) {
@@ -697,9 +727,15 @@ extern "C" const char* vst_gemm_kernel_name(int M, int N, int K, int kind, int t
   if (kind == 3) return "gemm_kernel<conv_in>";
   if (kind == 0 && (tile == 5 || (tile == 0 && N <= 64 && M >= 1024))) return "gemm_skinny";  // no-epilogue calls
   if (kind < 0 || kind > 3 || tile < 0 || tile > 8 || tile == 5 || splits < 0) return "";
+  const int splits_in = splits;
   if (tile == 0 && kind <= 1 && p8_auto(M, N, K, kind == 1)) tile = 8;
   choose(M, N, K, kind == 1, kind == 2, ws_bytes > kFlagBytes ? ws_bytes - kFlagBytes : 0, tile, splits);
-  if (tile == 8) return kind == 1 ? "gemm_p8<256x256,geglu>" : "gemm_p8<256x256>";
+  if (tile == 8) {
+    const bool sk = splits_in != 1 && p8_sk_shape(M, N, K) &&
+                    ws_bytes >= (size_t)device_cus() * 256 * 256 * sizeof(float) + kFlagBytes;
+    if (sk) return kind == 1 ? "gemm_p8<256x256,geglu,streamk>" : "gemm_p8<256x256,streamk>";
+    return kind == 1 ? "gemm_p8<256x256,geglu>" : "gemm_p8<256x256>";
+  }
   if (splits > 1) return split_names[tile - 1];
   int it = 0, gr = 0;
   if (tile == 3 && kind != 1 && plan_stream_k(M, N, K, ws_bytes, it, gr))
@@ -743,9 +779,11 @@ extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int
   if (tile == 0 && skinny_ok && M >= 1024) tile = 5;  // LoRA down-projection: skinny kernel
   if (tile == 5) return run_gemm(a, 0, 0, 5, 1, (hipStream_t)stream);
   const size_t slab_bytes = (workspace && ws_bytes > kFlagBytes) ? ws_bytes - kFlagBytes : 0;
+  const int splits_in = splits;  // tile 8: splits 1 = plain tiling, 0 = stream-K where it applies
   if (tile == 0 && splits == 0 && p8_auto(M, N, K, epilogue == 1) && p8_applies(M, N, K1, A2 != nullptr)) tile = 8;
   choose(M, N, K, epilogue == 1, 0, slab_bytes, tile, splits);
   if (slab_bytes) apply_stream_k(a, tile, splits, epilogue == 1 ? 1 : 0, workspace, ws_bytes);
+  if (tile == 8 && splits_in != 1) apply_p8_sk(a, workspace, ws_bytes);
   return run_gemm(a, 0, epilogue == 1, tile, splits, (hipStream_t)stream);
 }
 

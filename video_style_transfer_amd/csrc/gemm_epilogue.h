@@ -9,9 +9,10 @@ namespace vst {
 
 template <class Cfg, int EPI>
 __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, char* smem, const int m0, const int n0,
-                                              f32x4 (&acc)[Cfg::MI][Cfg::NJ], const int wr, const int wc) {
+                                              f32x4 (&acc)[Cfg::MI][Cfg::NJ], const int wr, const int wc,
+                                              const int tid = threadIdx.x) {
   constexpr int BM = Cfg::BM, BN = Cfg::BN;
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int lane = tid & 63;
   const int fr = lane & 15, fq = lane >> 4;
   const int lrow0 = wr * Cfg::WM + fr;          // + i*16
   const int lcol0 = wc * Cfg::WN + 4 * fq;      // + j*16

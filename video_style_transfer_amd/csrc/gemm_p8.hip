@@ -53,7 +53,14 @@ __device__ __forceinline__ void p8_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int EPI>
+// SK = stream-K: one workgroup per CU, each taking an equal share of the (tile, k-tile) iteration space, so grids of
+// 160 tiles (M = 8192, N = 1280: 62 % of the CUs under plain tiling) keep every CU busy.  A tile split between
+// workgroups is finished by its OWNER (the workgroup that runs its k-tile 0; that is always the owner's last
+// segment); the others (whose first segment starts mid-tile) store their fp32 accumulators in fragment order to
+// their partial slot, then raise their flag (agent-scope release).  The owner adds the partials in workgroup order
+// (deterministic), clears the flags for the next launch, and runs the epilogue.  Only owners wait, and only on
+// higher-numbered workgroups that wait on nobody, and the grid is at most one workgroup per CU: no cycle.
+template <int EPI, bool SK>
 __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int SLOT = P8Cfg::SLOT, BUF = P8Cfg::BUF;
@@ -62,47 +69,48 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   const int wr = wid >> 2, wc = wid & 3;
   const int fr = lane & 15, fq = lane >> 4;
   const int nbm = (p.M + 255) / 256, nbn = (p.N + 255) / 256;
-  int bm, bn;
-  {
-    const int t = xcd_remap(blockIdx.x, nbm * nbn);
+  const int ntiles = nbm * nbn;
+  auto tile_origin = [&](int t, int& m0, int& n0) {
     const int GROUP_M = 8, in_group = GROUP_M * nbn;
     const int gid = t / in_group, first_m = gid * GROUP_M;
     const int gsize = min(nbm - first_m, GROUP_M);
-    bm = first_m + (t - gid * in_group) % gsize;
-    bn = (t - gid * in_group) / gsize;
-  }
-  const int m0 = bm * 256, n0 = bn * 256;
+    m0 = (first_m + (t - gid * in_group) % gsize) * 256;
+    n0 = ((t - gid * in_group) / gsize) * 256;
+  };
   const auto ra1 = make_rsrc(p.A1, p.a1_bytes);
   const auto ra2 = make_rsrc(p.A2 ? p.A2 : p.A1, p.A2 ? p.a2_bytes : 0u);
   const auto rw = make_rsrc(p.Wt, p.w_bytes);
   const int nk = (p.K + 63) / 64;
   const bool ktail = (p.K & 63) != 0;
+  const bool late = wid >= 4;
 
   // ---- per-lane DMA descriptors: slot s in {Amq0, Amq1, Bnq0, Bnq1}, piece pc in {0, 1} = slot rows
   //      8*(wid + 8*pc) + (lane >> 3); this lane moves chunk c = (lane & 7) ^ ((row >> 1) & 7) of that row.
   uint32_t base1[4][2], base2[2][2];
   int c8[4][2];
+  auto setup_tile = [&](int m0, int n0) {
 #pragma unroll
-  for (int s = 0; s < 4; ++s)
+    for (int s = 0; s < 4; ++s)
 #pragma unroll
-    for (int pc = 0; pc < 2; ++pc) {
-      const int r = 8 * (wid + 8 * pc) + (lane >> 3);
-      const int c = (lane & 7) ^ ((r >> 1) & 7);
-      c8[s][pc] = c * 8;
-      if (s < 2) {
-        const int m = m0 + (r >> 6) * 128 + s * 64 + (r & 63);
-        base1[s][pc] = m < p.M ? (uint32_t)(m * p.lda1 + c * 8) * 2u : (uint32_t)kOOB;
-        base2[s][pc] = m < p.M ? (uint32_t)(m * p.lda2 + c * 8) * 2u : (uint32_t)kOOB;
-      } else {
-        const int n = n0 + (r >> 5) * 64 + (s - 2) * 32 + (r & 31);
-        base1[s][pc] = n < p.N ? (uint32_t)(n * p.ldw + c * 8) * 2u : (uint32_t)kOOB;
+      for (int pc = 0; pc < 2; ++pc) {
+        const int r = 8 * (wid + 8 * pc) + (lane >> 3);
+        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        c8[s][pc] = c * 8;
+        if (s < 2) {
+          const int m = m0 + (r >> 6) * 128 + s * 64 + (r & 63);
+          base1[s][pc] = m < p.M ? (uint32_t)(m * p.lda1 + c * 8) * 2u : (uint32_t)kOOB;
+          base2[s][pc] = m < p.M ? (uint32_t)(m * p.lda2 + c * 8) * 2u : (uint32_t)kOOB;
+        } else {
+          const int n = n0 + (r >> 5) * 64 + (s - 2) * 32 + (r & 31);
+          base1[s][pc] = n < p.N ? (uint32_t)(n * p.ldw + c * 8) * 2u : (uint32_t)kOOB;
+        }
       }
-    }
-  // slot s of k-tile kt into buffer (kt & 1); kt >= nk: out-of-range offsets (zeros), keeps vmcnt counts uniform
-  auto dma_slot = [&](int s, int kt) {
+  };
+  // slot s of k-tile kt into buffer (kt & 1); kt >= kend: out-of-range offsets (zeros), keeps vmcnt counts uniform
+  auto dma_slot = [&](int s, int kt, int kend) {
     char* dst = smem + (kt & 1) * BUF + s * SLOT + wid * 1024;
     const int k0 = kt * 64;
-    const bool live = kt < nk;
+    const bool live = kt < kend;
     if (s < 2) {
       const bool second = k0 >= p.K1;
       const uint32_t kb = (uint32_t)(second ? k0 - p.K1 : k0) * 2u;
@@ -123,10 +131,6 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   };
 
   f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 fa[4][2];         // A fragments of the current row quadrant (mq): 4 x 16 rows x 2 k-halves
   bf16x8 fb0[2][2], fb1[2][2];  // W fragments of column quadrants nq0 / nq1
   auto read_a = [&](int buf, int mq) {
@@ -152,71 +156,146 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     __builtin_amdgcn_s_setprio(0);                                                                   \
   }
 
-  // ---- prologue: k-tile 0 complete, k-tile 1 except Amq1 (issued in phase 0 of tile 0) ----
-  dma_slot(0, 0); dma_slot(2, 0); dma_slot(3, 0); dma_slot(1, 0);
-  dma_slot(0, 1); dma_slot(2, 1); dma_slot(3, 1);
-  asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // Amq0(0), Bnq0(0) landed
-  p8_barrier();
-  const bool late = wid >= 4;
-  if (late) p8_barrier();
+  // k-tiles [kb, ke) of the current tile into acc (zeroed here); ends with the LDS drained and free for reuse
+  auto run_segment = [&](int kb, int ke) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // ---- prologue: k-tile kb complete, k-tile kb+1 except Amq1 (issued in phase 0 of tile kb) ----
+    dma_slot(0, kb, ke); dma_slot(2, kb, ke); dma_slot(3, kb, ke); dma_slot(1, kb, ke);
+    dma_slot(0, kb + 1, ke); dma_slot(2, kb + 1, ke); dma_slot(3, kb + 1, ke);
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // Amq0(kb), Bnq0(kb) landed
+    p8_barrier();
+    if (late) p8_barrier();
 
-  for (int t = 0; t < nk; ++t) {
-    const int buf = t & 1;
-    // phase 0: Q(0,0)
-    read_a(buf, 0);
-    read_b(buf, 0, fb0);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Bnq1(t) landed
-    dma_slot(1, t + 1);
+    for (int t = kb; t < ke; ++t) {
+      const int buf = t & 1;
+      // phase 0: Q(0,0)
+      read_a(buf, 0);
+      read_b(buf, 0, fb0);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Bnq1(t) landed
+      dma_slot(1, t + 1, ke);
+      p8_barrier();
+      VST_P8_QUAD(0, 0, fb0)
+      p8_barrier();
+      // phase 1: Q(0,1)
+      read_b(buf, 1, fb1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Amq1(t) landed
+      p8_barrier();
+      VST_P8_QUAD(0, 1, fb1)
+      p8_barrier();
+      // phase 2: Q(1,1)
+      read_a(buf, 1);
+      dma_slot(0, t + 2, ke);
+      dma_slot(2, t + 2, ke);
+      p8_barrier();
+      VST_P8_QUAD(1, 1, fb1)
+      p8_barrier();
+      // phase 3: Q(1,0)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Amq0(t+1), Bnq0(t+1) landed
+      dma_slot(3, t + 2, ke);
+      p8_barrier();
+      VST_P8_QUAD(1, 0, fb0)
+      p8_barrier();
+    }
+    if (!late) p8_barrier();
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the trailing zero DMAs land before LDS reuse
     p8_barrier();
-    VST_P8_QUAD(0, 0, fb0)
-    p8_barrier();
-    // phase 1: Q(0,1)
-    read_b(buf, 1, fb1);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Amq1(t) landed
-    p8_barrier();
-    VST_P8_QUAD(0, 1, fb1)
-    p8_barrier();
-    // phase 2: Q(1,1)
-    read_a(buf, 1);
-    dma_slot(0, t + 2);
-    dma_slot(2, t + 2);
-    p8_barrier();
-    VST_P8_QUAD(1, 1, fb1)
-    p8_barrier();
-    // phase 3: Q(1,0)
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Amq0(t+1), Bnq0(t+1) landed
-    dma_slot(3, t + 2);
-    p8_barrier();
-    VST_P8_QUAD(1, 0, fb0)
-    p8_barrier();
-  }
+  };
 #undef VST_P8_QUAD
-  if (!late) p8_barrier();
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the trailing zero DMAs land before LDS reuse
-  p8_barrier();
-  tile_epilogue<P8Cfg, EPI>(p, smem, m0, n0, acc, wr, wc);
+
+  if constexpr (!SK) {
+    int m0, n0;
+    tile_origin(xcd_remap(blockIdx.x, ntiles), m0, n0);
+    setup_tile(m0, n0);
+    run_segment(0, nk);
+    tile_epilogue<P8Cfg, EPI>(p, smem, m0, n0, acc, wr, wc);
+  } else {
+    // Launched only with fewer tiles than workgroups, so a workgroup's share (< nk k-tiles) meets at most two
+    // tiles: first the tail of one (contributor, unless the share starts on a tile boundary), then the head of the
+    // next (owner).  Straight-line code: an outer segment loop keeps epilogue addressing live across the k-loop.
+    // Partial slot layout: [register r = 4 i + j][thread] f32x4 (fragment order, 16 B per lane, coalesced).
+    constexpr int PSLOT = 256 * 256;  // floats
+    // scalars (readfirstlane): divisions are VALU sequences, and a VGPR loop bound would make the whole k-loop's
+    // control and DMA addressing per-lane.  Shares: q or q + 1 k-tiles, start(v) = v q + min(v, r), no 64-bit divide.
+    const int G = gridDim.x;
+    const int w = xcd_remap(blockIdx.x, G);
+    const int T = ntiles * nk;  // host-checked < 2^31
+    const int q = T / G, r = T - q * G;
+    auto start_of = [&](int v) { return v * q + min(v, r); };
+    int g = __builtin_amdgcn_readfirstlane(start_of(w));
+    const int g1 = __builtin_amdgcn_readfirstlane(start_of(w + 1));
+    int m0, n0;
+    auto origin = [&](int tile) {
+      tile_origin(tile, m0, n0);
+      m0 = __builtin_amdgcn_readfirstlane(m0);
+      n0 = __builtin_amdgcn_readfirstlane(n0);
+    };
+    if (g < g1 && g % nk != 0) {  // contributor: k-tiles [kb, ke) of a tile owned by a lower workgroup
+      const int tile = __builtin_amdgcn_readfirstlane(g / nk);
+      const int kb = g - tile * nk;
+      const int ke = min(nk, kb + (g1 - g));
+      origin(tile);
+      setup_tile(m0, n0);
+      run_segment(kb, ke);
+      f32x4* slot = reinterpret_cast<f32x4*>(p.sk_ws + (size_t)w * PSLOT);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) slot[(i * 4 + j) * 512 + tid] = acc[i][j];
+      __syncthreads();  // every wave's stores have reached L2
+      if (tid == 0) __hip_atomic_store(p.sk_flags + w, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      g += ke - kb;
+    }
+    if (g < g1) {  // owner: k-tiles [0, ke) of this tile, then the later k-ranges from the next workgroups
+      int tl;      // laundered: nothing of the owner's addressing is computed before (and live across) its k-loop
+      tl = tid;
+      const int tile = __builtin_amdgcn_readfirstlane(g / nk), ke = g1 - g;
+      origin(tile);
+      setup_tile(m0, n0);
+      run_segment(0, ke);
+      const int te = (tile + 1) * nk;
+      for (int c = w + 1; c < G && start_of(c) < te; ++c) {
+        if (tl == 0)
+          while (__hip_atomic_load(p.sk_flags + c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0)
+            __builtin_amdgcn_s_sleep(2);
+        __syncthreads();
+        const f32x4* slot = reinterpret_cast<const f32x4*>(p.sk_ws + (size_t)c * PSLOT);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] += slot[(i * 4 + j) * 512 + tl];
+          asm volatile("" ::: "memory");  // 4 loads in flight at a time: acc already holds 128 registers
+        }
+        if (tl == 0) __hip_atomic_store(p.sk_flags + c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      tile_epilogue<P8Cfg, EPI>(p, smem, m0, n0, acc, wr, wc, tl);
+    }
+  }
 }
 
-template <int EPI>
+template <int EPI, bool SK>
 static int launch_p8_epi(const GemmArgs& a, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_p8_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)gemm_p8_kernel<EPI, SK>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               P8Cfg::LDS);
     attr = true;
   }
-  const int nwg = ((a.M + 255) / 256) * ((a.N + 255) / 256);
-  hipLaunchKernelGGL((gemm_p8_kernel<EPI>), dim3(nwg), dim3(512), P8Cfg::LDS, s, a);
+  const int nwg = SK ? a.sk_grid : ((a.M + 255) / 256) * ((a.N + 255) / 256);
+  hipLaunchKernelGGL((gemm_p8_kernel<EPI, SK>), dim3(nwg), dim3(512), P8Cfg::LDS, s, a);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 
 // epi: 0 bias / row bias / residual, 1 GEGLU, 3 bias + GELU
 int launch_gemm_p8(const GemmArgs& a, int epi, hipStream_t s) {
   if (a.A2 && (a.K1 & 63)) return VST_ERR_ARG;  // a 64-deep k-tile must not straddle the two A sources
+  const bool sk = a.sk_grid > 0 && a.sk_ws && a.sk_flags;
   switch (epi) {
-    case 0: return launch_p8_epi<0>(a, s);
-    case 1: return launch_p8_epi<1>(a, s);
-    case 3: return launch_p8_epi<3>(a, s);
+    case 0: return sk ? launch_p8_epi<0, true>(a, s) : launch_p8_epi<0, false>(a, s);
+    case 1: return sk ? launch_p8_epi<1, true>(a, s) : launch_p8_epi<1, false>(a, s);
+    case 3: return sk ? launch_p8_epi<3, true>(a, s) : launch_p8_epi<3, false>(a, s);
     default: return VST_ERR_ARG;
   }
 }
