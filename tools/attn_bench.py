@@ -29,7 +29,10 @@ def timeit(fn, iters=20):
 
 def main():
     dev = torch.device("cuda")
+    only = sys.argv[1:]  # optional shape names (profiling passes)
     for name, nb, heads, Nq, Nk, kv_div in SPATIAL:
+        if only and name not in only:
+            continue
         C = heads * 64
         q = torch.randn(nb * Nq, 3 * C, device=dev).to(BF)
         kv = torch.randn(nb // kv_div * Nk, 2 * C, device=dev).to(BF)
@@ -42,6 +45,8 @@ def main():
         fl = 4.0 * nb * heads * Nq * Nk * 64
         print(json.dumps({"shape": name, "us": round(ms * 1e3, 1), "tflops": round(fl / ms / 1e9, 1)}), flush=True)
     for name, nclip, Fr, HW, C in TEMPORAL:
+        if only and name not in only:
+            continue
         qkv = torch.randn(nclip * Fr * HW, 3 * C, device=dev).to(BF)
         out = torch.empty(nclip * Fr * HW, C, device=dev, dtype=BF)
         ms = timeit(lambda: K.temporal_attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], nclip, Fr, HW, 8, C // 8,

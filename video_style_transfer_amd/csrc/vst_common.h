@@ -54,8 +54,12 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
 }
 // value of x after a bf16 store and reload (the rounding point of a bf16 tensor boundary)
 __device__ __forceinline__ float round_bf(float x) { return bf2f(f2bf(x)); }
+// one v_cvt_pk_bf16_f32 (RNE, lo -> bits 0-15): the scalar casts + shift + or cost 4 VALU per pair
 __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  typedef float vst_f2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 vst_b2 __attribute__((ext_vector_type(2)));
+  const vst_f2 v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, vst_b2));
 }
 __device__ __forceinline__ void unpack8(const u32x4& v, float* f) {
 #pragma unroll
