@@ -29,6 +29,20 @@ __device__ __forceinline__ s16x4 ds_read_tr(const char* p) {
       (lds_s16x4*)((__attribute__((address_space(3))) char*)(uintptr_t)(p)));
 }
 
+// max over the four 16-lane groups (lanes i, i^16, i^32, i^48) with two VALU lane swaps instead of two LDS
+// ds_bpermute round trips; v_max_f32 as asm keeps the compiler from adding canonicalising maxes around the swaps
+__device__ __forceinline__ float vmax_raw(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float group_max(float x) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = vmax_raw(__uint_as_float(p[0]), __uint_as_float(p[1]));
+  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return vmax_raw(__uint_as_float(q[0]), __uint_as_float(q[1]));
+}
+
 __device__ __forceinline__ bf16x8 cat_tr(s16x4 lo, s16x4 hi) {
   typedef short s16x8 __attribute__((ext_vector_type(8)));
   s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -117,6 +131,13 @@ __global__ __launch_bounds__(256, 2) void spatial_attn_kernel(
   float lrun[2] = {0.f, 0.f};
 
   const int nt = (Nk + SA_KT - 1) / SA_KT;
+  // V^T fragment reads: lane 4q'+p' of group g reads row 4g + q' (+16, +32, +48), cols 16db + 4p'
+  int voff[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) {
+    const int li = lane & 15, r0 = g * 4 + (li >> 2), col = db * 16 + (li & 3) * 4;
+    voff[db] = v_off(r0, col >> 3) + (col & 7) * 2;
+  }
   load_kv(0);
   store_kv(0);
   __syncthreads();
@@ -162,8 +183,7 @@ __global__ __launch_bounds__(256, 2) void spatial_attn_kernel(
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) mx = fmaxf(mx, s[kt][qb][i]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16));
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      mx = group_max(mx);
       const float mnew = fmaxf(mrun[qb], mx);
       alpha[qb] = fast_exp2((mrun[qb] - mnew) * scale_log2);
       mrun[qb] = mnew;
@@ -184,27 +204,23 @@ __global__ __launch_bounds__(256, 2) void spatial_attn_kernel(
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb) o[d][qb] *= alpha[qb];
 
-    // ---- O^T += V^T P^T ----
+    // ---- O^T += V^T P^T: two 32-key k-steps st (P tiles 2st -> elements 0-3, 2st+1 -> 4-7) ----
+    bf16x8 pf[2][2];
 #pragma unroll
-    for (int st = 0; st < 2; ++st) {  // 32-key k-steps: tiles 2st (elements 0-3) and 2st+1 (4-7)
-      bf16x8 pf[2];
+    for (int st = 0; st < 2; ++st)
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb)
-        pf[qb] = pack_p8(s[2 * st][qb][0], s[2 * st][qb][1], s[2 * st][qb][2], s[2 * st][qb][3],
-                         s[2 * st + 1][qb][0], s[2 * st + 1][qb][1], s[2 * st + 1][qb][2], s[2 * st + 1][qb][3]);
+        pf[st][qb] = pack_p8(s[2 * st][qb][0], s[2 * st][qb][1], s[2 * st][qb][2], s[2 * st][qb][3],
+                             s[2 * st + 1][qb][0], s[2 * st + 1][qb][1], s[2 * st + 1][qb][2], s[2 * st + 1][qb][3]);
 #pragma unroll
-      for (int db = 0; db < 4; ++db) {
-        // lane 4q'+p' of group g: row (32st + 4g + q'), cols 16db + 4p'
-        const int li = lane & 15;
-        const int r0 = st * 32 + g * 4 + (li >> 2);
-        const int col = db * 16 + (li & 3) * 4;
-        const int ch = col >> 3, within = (col & 7) * 2;
-        const s16x4 lo = ds_read_tr(Vs + v_off(r0, ch) + within);
-        const s16x4 hi = ds_read_tr(Vs + v_off(r0 + 16, ch) + within);
-        const bf16x8 vf = cat_tr(lo, hi);
+    for (int db = 0; db < 4; ++db) {
+      const char* vp = Vs + voff[db];  // rows +16 / +32 keep the swizzle: immediate offsets 2048 / 4096
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const bf16x8 vf = cat_tr(ds_read_tr(vp + st * 4096), ds_read_tr(vp + st * 4096 + 2048));
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb)
-          o[db][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qb], o[db][qb], 0, 0, 0);
+          o[db][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[st][qb], o[db][qb], 0, 0, 0);
       }
     }
     if (t + 1 < nt) store_kv(cur ^ 1);
