@@ -73,17 +73,31 @@ def _lib_md5():
         return hashlib.md5(f.read()).hexdigest()
 
 
+def src_hash():
+    """sha256 over the library's sources and build recipe (csrc/*.hip, *.h, include/vst.h, Makefile): the hipcc
+    build is deterministic, so equal hashes mean the same libvst_hip.so even after a rebuild."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "video_style_transfer_amd", "csrc", "*")))
+    files += [os.path.join(ROOT, "include", "vst.h"), os.path.join(ROOT, "Makefile")]
+    for fn in files:
+        with open(fn, "rb") as f:
+            h.update(os.path.basename(fn).encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
 def pmc_traffic(symbol):
     """HBM bytes per launch of `symbol` from the newest profiles/pmc_traffic_*.json (tools/pmc_traffic.py:
     rocprofv3 FETCH_SIZE / WRITE_SIZE passes with the gfx950 corrections), only if it was measured on
-    this exact libvst_hip.so.  (bytes, source) or (None, reason)."""
+    this exact libvst_hip.so (same md5, or same source hash).  (bytes, source) or (None, reason)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic_*.json")), key=os.path.getmtime)
     if not files:
         return None, "no PMC profile"
     with open(files[-1]) as f:
         d = json.load(f)
-    if d.get("lib_md5") != _lib_md5():
+    if d.get("lib_md5") != _lib_md5() and d.get("src_hash") != src_hash():
         return None, f"{os.path.basename(files[-1])} was measured on another build of libvst_hip.so"
     k = d.get("kernels", {}).get(symbol)
     if k is None:

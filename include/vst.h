@@ -168,6 +168,32 @@ int vst_temporal_attention_bwd(const void* q, const void* k, const void* v, int 
                                int head_dim, float scale, void* stream);
 int vst_geglu_bwd(const void* p, int ldp, const void* g, int ldg, int M, int Nh, void* dp, int lddp, void* stream);
 
+/* ---- SDXL VAE (diffusers AutoencoderKL, fp32 in the reference: inference_animatediff.py:164-169) decode of the
+ * denoised clip (inference_animatediff.py:137-144) and encode of training frames (train_animatediff.py:219-224),
+ * SURVEY §8(f) rank 4.  Convs, GroupNorm(+SiLU) and the 1x1 projections reuse the entries above. */
+/* vst_conv3x3_down_pad0: diffusers Downsample2D(padding=0) of DownEncoderBlock2D = F.pad(x, (0,1,0,1)) then a 3x3
+ * stride-2 conv without padding.  Output [nimg, (H-2)/2+1, (W-2)/2+1, Cout], row stride ldc. */
+int vst_conv3x3_down_pad0(const void* x, int C, int nimg, int H, int W, const void* Wt, int Cout, const float* bias,
+                          void* out, int ldc, void* workspace, size_t ws_bytes, void* stream);
+/* vst_gemm_f32out: C[M][N] = A[M][K] . W[N][K]^T left in fp32 (row stride N).  The mid-block attention's scores
+ * (one head of dim 512 over the latent's h*w tokens) feed vst_softmax_rows unrounded, as the fp32 reference's do. */
+int vst_gemm_f32out(const void* A, int lda, const void* W, int ldw, int M, int N, int K, float* C, void* stream);
+/* vst_softmax_rows: P[r][j] = softmax_j(scale * S[r][j]) (fp32 math, bf16 out) -- diffusers Attention.get_attention_scores
+ * + softmax of the VAE mid-block (AttnProcessor2_0's SDPA math, scale = head_dim^-0.5). */
+int vst_softmax_rows(const float* S, int lds, int rows, int n, float scale, void* P, int ldp, void* stream);
+/* Layout at the fp32 NCHW tensor boundary of vae.decode / vae.encode:
+ * vst_nchw_to_nhwc: dst[(i*HW+p)*ldd + c] = bf16(src[(i*C+c)*HW+p] * mul), channels C..ldd-1 zero-filled
+ *   (decode input: latents / scaling_factor, inference_animatediff.py:137; encode input: frames in [-1, 1]);
+ * vst_nhwc_to_nchw: bf16 NHWC (row stride ld) -> fp32 NCHW (DecoderOutput.sample);
+ * vst_frames_to_u8: (x / 2 + 0.5).clamp(0, 1) * 255 truncated to uint8, HWC per frame (inference_animatediff.py:141-143);
+ * vst_vae_sample: DiagonalGaussianDistribution(moments).sample() * mul (train_animatediff.py:222-223): moments NHWC
+ *   [n*HW][ld] bf16 (mean = ch 0-3, logvar = ch 4-7 clamped to [-30, 20]), eps fp32 NCHW (null: the mode), out fp32
+ *   NCHW (n, 4, HW). */
+int vst_nchw_to_nhwc(const float* src, int n, int C, int HW, float mul, void* dst, int ldd, void* stream);
+int vst_nhwc_to_nchw(const void* src, int ld, int n, int C, int HW, float* dst, void* stream);
+int vst_frames_to_u8(const void* src, int ld, int n, int C, int HW, void* dst, void* stream);
+int vst_vae_sample(const void* moments, int ld, int n, int HW, const float* eps, float mul, float* out, void* stream);
+
 /* Ceiling probes (no reference counterpart; bench.py's measured peaks next to the vendor figures,
  * SURVEY §8(d)).  vst_probe_mfma: `grid` workgroups x 8 waves, each wave `iters` x 16 independent
  * 16x16x32 bf16 MFMAs (flops = grid*8*iters*16*16384).  vst_probe_hbm_read: streams `bytes` of `src`

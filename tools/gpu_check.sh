@@ -6,7 +6,7 @@ TAG=${1:-r1}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 if [ -z "$SKIP_TESTS" ]; then
-timeout -k 10 480 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread \
+timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread \
   > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
 tail -3 gpurun_out/pytest_gpu_$TAG.log
 fi
@@ -20,7 +20,7 @@ if [ -n "$PMC" ]; then
   python tools/pmc_traffic.py gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE gpurun_out/pmc_so.md5 \
     > gpurun_out/pmc_traffic_$TAG.json || exit 1
   rm -rf gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE
-  cp gpurun_out/pmc_traffic_$TAG.json profiles/pmc_traffic_r1.json  # the bench below reads it (same .so)
+  cp gpurun_out/pmc_traffic_$TAG.json profiles/pmc_traffic_$TAG.json  # the bench below reads the newest (same .so)
   echo pmc done
 fi
 VST_BENCH_SHAPES=1 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err \

@@ -29,6 +29,12 @@ def bench_symbol(name: str) -> str:
         tag = {("0", "0"): "", ("0", "1"): ",geglu", ("1", "0"): ",conv", ("0", "2"): ",splitk",
                ("1", "2"): ",splitk"}.get((amode, epi), f",a{amode}e{epi}")
         return f"gemm_ring<{bm}x{bn}{tag}{',streamk' if sk == 'true' else ''}>"
+    m = re.search(r"gemm_p8_kernel<(\d), (true|false)>", name)
+    if m:
+        epi, sk = m.groups()
+        return f"gemm_p8<256x256{',geglu' if epi == '1' else ''}{',streamk' if sk == 'true' else ''}>"
+    if "layernorm_lora_kernel" in name:
+        return "layernorm_lora"
     for k, v in (("gemm_skinny", "gemm_skinny"), ("spatial_attn_kernel", "spatial_attn_kernel"),
                  ("temporal_attn_kernel", "temporal_attn_kernel"), ("layernorm_kernel", "layernorm_kernel"),
                  ("gn_", "gn_stats/gn_finalize/gn_apply"), ("gemm_kernel<2", "gemm_kernel<conv_in>")):
@@ -58,7 +64,9 @@ def main():
     fetch = read_counter(sys.argv[1], "FETCH_SIZE")
     write = read_counter(sys.argv[2], "WRITE_SIZE")
     lib_md5 = open(sys.argv[3]).read().split()[0] if len(sys.argv) > 3 else None
-    out = {"lib_md5": lib_md5, "note": "bytes per launch; fetch = 2 x 1024 x FETCH_SIZE (gfx950 wide-read correction), "
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import src_hash
+    out = {"lib_md5": lib_md5, "src_hash": src_hash(), "note": "bytes per launch; fetch = 2 x 1024 x FETCH_SIZE (gfx950 wide-read correction), "
                    "write = 1024 x WRITE_SIZE; memory-side requests (L2 misses incl. Infinity-Cache hits)",
            "kernels": {}}
     for k in sorted(set(fetch) | set(write)):

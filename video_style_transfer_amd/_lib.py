@@ -57,6 +57,13 @@ SIGNATURES = {
     "vst_zero_insert": (_I, [_P, _I, _I, _I, _I, _P, _P]),
     "vst_sumpool2x2": (_I, [_P, _I, _I, _I, _I, _P, _P]),
     "vst_temporal_attention_bwd": (_I, [_P, _P, _P, _I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P]),
+    "vst_conv3x3_down_pad0": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P, _S, _P]),
+    "vst_gemm_f32out": (_I, [_P, _I, _P, _I, _I, _I, _I, _P, _P]),
+    "vst_softmax_rows": (_I, [_P, _I, _I, _I, _F, _P, _I, _P]),
+    "vst_nchw_to_nhwc": (_I, [_P, _I, _I, _I, _F, _P, _I, _P]),
+    "vst_nhwc_to_nchw": (_I, [_P, _I, _I, _I, _I, _P, _P]),
+    "vst_frames_to_u8": (_I, [_P, _I, _I, _I, _I, _P, _P]),
+    "vst_vae_sample": (_I, [_P, _I, _I, _I, _P, _F, _P, _P]),
     "vst_probe_mfma": (_I, [_I, _I, _P, _P]),
     "vst_probe_hbm_read": (_I, [_P, _S, _I, _P, _P]),
     "vst_version": (ctypes.c_char_p, []),

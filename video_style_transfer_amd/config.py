@@ -72,3 +72,30 @@ class UNetMotionConfig:
             if k in d:
                 d[k] = tuple(d[k])
         return cls(**d)
+
+
+@dataclass
+class VAEConfig:
+    """diffusers AutoencoderKL config of stabilityai/stable-diffusion-xl-base-1.0/vae (loaded fp32 by the reference:
+    inference_animatediff.py:164-169, train_animatediff.py:67-72): 4 DownEncoderBlock2D / UpDecoderBlock2D levels,
+    2 resnets per down level (3 per up level), GroupNorm(32, eps 1e-6), one single-head attention in each mid block,
+    latent 4 channels, scaling_factor 0.13025."""
+    in_channels: int = 3
+    out_channels: int = 3
+    latent_channels: int = 4
+    block_out_channels: Tuple[int, ...] = (128, 256, 512, 512)
+    layers_per_block: int = 2
+    norm_num_groups: int = 32
+    scaling_factor: float = 0.13025
+
+    def to_dict(self):
+        return asdict(self)
+
+    @classmethod
+    def sdxl(cls) -> "VAEConfig":
+        return cls()
+
+    @classmethod
+    def tiny(cls) -> "VAEConfig":
+        """Same topology at test scale (channels multiples of 64 for the implicit-GEMM convs)."""
+        return cls(block_out_channels=(64, 128, 128))

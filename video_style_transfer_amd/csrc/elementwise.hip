@@ -292,6 +292,114 @@ __global__ void step_advance_kernel(int* step, int num_steps) {
   }
 }
 
+
+// ---- SDXL VAE (AutoencoderKL) glue: layout conversions at the fp32 NCHW boundary, latent sampling, frame output,
+// and the row softmax of the mid-block attention (head_dim 512: scores come fp32 from vst_gemm_f32out) ----
+
+// dst[(img*HW + p)*ldd + c] = bf16(src[(img*C + c)*HW + p] * mul) for c < C, 0 for C <= c < ldd
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ src, int n, int C, int HW, float mul,
+                                    bf16_t* __restrict__ dst, int ldd) {
+  const size_t total = (size_t)n * HW * ldd;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % ldd);
+    const size_t t = i / ldd;  // img * HW + p
+    const int p = (int)(t % HW);
+    const size_t img = t / HW;
+    dst[i] = c < C ? f2bf(src[(img * C + c) * HW + p] * mul) : (bf16_t)0;
+  }
+}
+
+// dst[(img*C + c)*HW + p] = src[(img*HW + p)*ld + c]  (bf16 NHWC -> fp32 NCHW)
+__global__ void nhwc_to_nchw_kernel(const bf16_t* __restrict__ src, int ld, int n, int C, int HW,
+                                    float* __restrict__ dst) {
+  const size_t total = (size_t)n * C * HW;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int p = (int)(i % HW);
+    const size_t t = i / HW;  // img * C + c
+    const int c = (int)(t % C);
+    const size_t img = t / C;
+    dst[i] = bf2f(src[(img * HW + p) * ld + c]);
+  }
+}
+
+// inference_animatediff.py:141-143: (x / 2 + 0.5).clamp(0, 1), then (x * 255).astype(np.uint8) (truncation), HWC
+__global__ void frames_to_u8_kernel(const bf16_t* __restrict__ src, int ld, int n, int C, int HW,
+                                    uint8_t* __restrict__ dst) {
+  const size_t total = (size_t)n * HW * C;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const size_t t = i / C;
+    const float v = fminf(fmaxf(bf2f(src[t * ld + c]) / 2.f + 0.5f, 0.f), 1.f);
+    dst[i] = (uint8_t)(int)(v * 255.f);
+  }
+}
+
+// DiagonalGaussianDistribution(moments).sample() * scaling_factor (train_animatediff.py:222-223): moments NHWC
+// [n*HW][ld] bf16 with mean = channels 0..3, logvar = 4..7; logvar clamped to [-30, 20]; eps fp32 NCHW (n, 4, HW);
+// out fp32 NCHW.  eps == nullptr: the distribution's mode (mean).
+__global__ void vae_sample_kernel(const bf16_t* __restrict__ mom, int ld, int n, int HW, const float* __restrict__ eps,
+                                  float mul, float* __restrict__ out) {
+  const size_t total = (size_t)n * 4 * HW;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int p = (int)(i % HW);
+    const size_t t = i / HW;
+    const int c = (int)(t % 4);
+    const size_t img = t / 4;
+    const bf16_t* m = mom + (img * HW + p) * ld;
+    float v = bf2f(m[c]);
+    if (eps) {
+      const float lv = fminf(fmaxf(bf2f(m[4 + c]), -30.f), 20.f);
+      v += expf(0.5f * lv) * eps[i];
+    }
+    out[i] = v * mul;
+  }
+}
+
+// P[r][:] = softmax(scale * S[r][:]) in fp32, stored bf16.  One wave per row: an online (max, sum) pass, then the
+// normalised exponentials (the second read of the row is an L2 hit).
+__global__ __launch_bounds__(256) void softmax_rows_kernel(const float* __restrict__ S, int lds, int rows, int n,
+                                                           float scale_log2, bf16_t* __restrict__ P, int ldp) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const float* s = S + (size_t)r * lds;
+  float m = -INFINITY, l = 0.f;
+  for (int j = lane * 4; j < n; j += 256) {
+    float v[4];
+    if (j + 4 <= n) {
+      const f32x4 q = *reinterpret_cast<const f32x4*>(s + j);
+      v[0] = q[0]; v[1] = q[1]; v[2] = q[2]; v[3] = q[3];
+    } else {
+      for (int e = 0; e < 4; ++e) v[e] = j + e < n ? s[j + e] : -INFINITY;
+    }
+    float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])) * scale_log2;
+    const float mn = fmaxf(m, mx);
+    l *= exp2f(m - mn);
+    for (int e = 0; e < 4; ++e) l += exp2f(v[e] * scale_log2 - mn);
+    m = mn;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const float mo = __shfl_xor(m, o), lo = __shfl_xor(l, o);
+    const float mn = fmaxf(m, mo);
+    if (mn != -INFINITY) {  // lanes past n hold (-inf, 0)
+      l = (m == -INFINITY ? 0.f : l * exp2f(m - mn)) + (mo == -INFINITY ? 0.f : lo * exp2f(mo - mn));
+      m = mn;
+    }
+  }
+  const float inv = 1.f / l;
+  bf16_t* p = P + (size_t)r * ldp;
+  for (int j = lane * 4; j < n; j += 256) {
+    if (j + 4 <= n) {
+      const f32x4 q = *reinterpret_cast<const f32x4*>(s + j);
+      u32x2 w{pack2bf(exp2f(q[0] * scale_log2 - m) * inv, exp2f(q[1] * scale_log2 - m) * inv),
+              pack2bf(exp2f(q[2] * scale_log2 - m) * inv, exp2f(q[3] * scale_log2 - m) * inv)};
+      *reinterpret_cast<u32x2*>(p + j) = w;
+    } else {
+      for (int e = 0; j + e < n; ++e) p[j + e] = f2bf(exp2f(s[j + e] * scale_log2 - m) * inv);
+    }
+  }
+}
+
 }  // namespace vst
 
 using namespace vst;
@@ -427,6 +535,44 @@ extern "C" int vst_sumpool2x2(const void* x, int nimg, int h, int w, int C, void
   const int grid = (int)std::min<size_t>((total + 255) / 256, 16384);
   hipLaunchKernelGGL(sumpool2x2_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, nimg, h, w,
                      C, (bf16_t*)y);
+  return ok();
+}
+
+static inline int grid_for(size_t total) { return (int)std::min<size_t>((total + 255) / 256, 16384); }
+
+extern "C" int vst_nchw_to_nhwc(const float* src, int n, int C, int HW, float mul, void* dst, int ldd, void* stream) {
+  if (!src || !dst || n <= 0 || C <= 0 || HW <= 0 || ldd < C) return VST_ERR_ARG;
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid_for((size_t)n * HW * ldd)), dim3(256), 0, (hipStream_t)stream, src,
+                     n, C, HW, mul, (bf16_t*)dst, ldd);
+  return ok();
+}
+
+extern "C" int vst_nhwc_to_nchw(const void* src, int ld, int n, int C, int HW, float* dst, void* stream) {
+  if (!src || !dst || n <= 0 || C <= 0 || HW <= 0 || ld < C) return VST_ERR_ARG;
+  hipLaunchKernelGGL(nhwc_to_nchw_kernel, dim3(grid_for((size_t)n * C * HW)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)src, ld, n, C, HW, dst);
+  return ok();
+}
+
+extern "C" int vst_frames_to_u8(const void* src, int ld, int n, int C, int HW, void* dst, void* stream) {
+  if (!src || !dst || n <= 0 || C <= 0 || HW <= 0 || ld < C) return VST_ERR_ARG;
+  hipLaunchKernelGGL(frames_to_u8_kernel, dim3(grid_for((size_t)n * HW * C)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)src, ld, n, C, HW, (uint8_t*)dst);
+  return ok();
+}
+
+extern "C" int vst_vae_sample(const void* moments, int ld, int n, int HW, const float* eps, float mul, float* out,
+                              void* stream) {
+  if (!moments || !out || n <= 0 || HW <= 0 || ld < 8) return VST_ERR_ARG;
+  hipLaunchKernelGGL(vae_sample_kernel, dim3(grid_for((size_t)n * 4 * HW)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)moments, ld, n, HW, eps, mul, out);
+  return ok();
+}
+
+extern "C" int vst_softmax_rows(const float* S, int lds, int rows, int n, float scale, void* P, int ldp, void* stream) {
+  if (!S || !P || rows <= 0 || n <= 0 || lds < n || ldp < n || (lds & 3) || (ldp & 3)) return VST_ERR_ARG;
+  hipLaunchKernelGGL(softmax_rows_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream, S, lds, rows, n,
+                     scale * 1.4426950408889634f, (bf16_t*)P, ldp);
   return ok();
 }
 

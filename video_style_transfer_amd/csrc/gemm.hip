@@ -136,7 +136,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
           ok = ok && uy >= 0 && uy < 2 * p.H && ux >= 0 && ux < 2 * p.W;
           iy = uy >> 1; ix = ux >> 1;
         } else {
-          iy = oyv[i] * p.stride + ky - 1; ix = oxv[i] * p.stride + kx - 1;
+          iy = oyv[i] * p.stride + ky - 1 + p.pad0; ix = oxv[i] * p.stride + kx - 1 + p.pad0;
           ok = ok && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
         }
         const int off = ok ? (((rowA[i] * p.H + iy) * p.W + ix) * cs + ci) * 2 : kOOB;
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
             ok = ok && uy >= 0 && uy < 2 * p.H && ux >= 0 && ux < 2 * p.W;
             iy = uy >> 1; ix = ux >> 1;
           } else {
-            iy = oyv[i] * p.stride + ky - 1; ix = oxv[i] * p.stride + kx - 1;
+            iy = oyv[i] * p.stride + ky - 1 + p.pad0; ix = oxv[i] * p.stride + kx - 1 + p.pad0;
             ok = ok && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
           }
           const int off = ok ? (((rowA[i] * p.H + iy) * p.W + ix) * p.C1 + ci) * 2 : kOOB;
@@ -797,11 +797,12 @@ extern "C" int vst_gemm(const void* A, int lda, const void* A2, int lda2, int K1
 // 3x3 conv, padding 1, NHWC.  x1: [nimg,H,W,C1], optional x2: [nimg,H,W,C2] concatenated
 // on channels.  Wt: [Cout][3][3][C1+C2].  stride 1 or 2; upsample=1 applies nearest 2x to
 // the input first (output 2H x 2W).  Output [nimg, OH, OW, Cout] with row stride ldc.
-extern "C" int vst_conv3x3_ex(const void* x1, int C1, const void* x2, int C2, int nimg, int H, int W, int stride,
-                              int upsample, const void* Wt, int Cout, const float* bias, const float* row_bias,
-                              int row_bias_div, int ld_row_bias, const void* R, int ldr, void* out, int ldc, int tile,
-                              int splits, void* workspace, size_t ws_bytes, void* stream) {
+static int conv3x3_impl(const void* x1, int C1, const void* x2, int C2, int nimg, int H, int W, int stride,
+                        int upsample, int pad0, const void* Wt, int Cout, const float* bias, const float* row_bias,
+                        int row_bias_div, int ld_row_bias, const void* R, int ldr, void* out, int ldc, int tile,
+                        int splits, void* workspace, size_t ws_bytes, void* stream) {
   if (!x1 || !Wt || !out || nimg <= 0 || H <= 0 || W <= 0 || Cout <= 0) return VST_ERR_ARG;
+  if (pad0 && (stride != 2 || H < 2 || W < 2)) return VST_ERR_ARG;
   if (stride != 1 && stride != 2) return VST_ERR_ARG;
   if (upsample && stride != 1) return VST_ERR_ARG;
   if (tile < 0 || tile > 7 || tile == 5 || splits < 0) return VST_ERR_ARG;
@@ -809,8 +810,9 @@ extern "C" int vst_conv3x3_ex(const void* x1, int C1, const void* x2, int C2, in
   const bool vec = (Ct % BK == 0) && (C1 % 8 == 0);
   if (x2 && !vec) return VST_ERR_ARG;
   GemmArgs a{};
-  a.OH = upsample ? 2 * H : (stride == 2 ? (H + 1) / 2 : H);
-  a.OW = upsample ? 2 * W : (stride == 2 ? (W + 1) / 2 : W);
+  a.OH = upsample ? 2 * H : pad0 ? (H - 2) / 2 + 1 : (stride == 2 ? (H + 1) / 2 : H);
+  a.OW = upsample ? 2 * W : pad0 ? (W - 2) / 2 + 1 : (stride == 2 ? (W + 1) / 2 : W);
+  a.pad0 = pad0;
   a.A1 = (const bf16_t*)x1; a.A2 = (const bf16_t*)x2; a.C1 = C1; a.C2 = x2 ? C2 : 0;
   a.H = H; a.W = W; a.stride = stride; a.up = upsample;
   a.K = 9 * Ct; a.K1 = a.K;
@@ -832,6 +834,44 @@ extern "C" int vst_conv3x3_ex(const void* x1, int C1, const void* x2, int C2, in
   choose(a.M, a.N, a.K, 0, 1, slab_bytes, tile, splits);
   if (slab_bytes && vec) apply_stream_k(a, tile, splits, 0, workspace, ws_bytes);
   return run_gemm(a, vec ? 1 : 2, 0, tile, splits, (hipStream_t)stream);
+}
+
+extern "C" int vst_conv3x3_ex(const void* x1, int C1, const void* x2, int C2, int nimg, int H, int W, int stride,
+                              int upsample, const void* Wt, int Cout, const float* bias, const float* row_bias,
+                              int row_bias_div, int ld_row_bias, const void* R, int ldr, void* out, int ldc, int tile,
+                              int splits, void* workspace, size_t ws_bytes, void* stream) {
+  return conv3x3_impl(x1, C1, x2, C2, nimg, H, W, stride, upsample, 0, Wt, Cout, bias, row_bias, row_bias_div,
+                      ld_row_bias, R, ldr, out, ldc, tile, splits, workspace, ws_bytes, stream);
+}
+
+// 3x3 stride-2 conv with padding (0,1,0,1): diffusers Downsample2D(padding=0) = F.pad(x, (0, 1, 0, 1)) + conv(k3, s2,
+// p0), the downsampler of the SDXL VAE encoder's DownEncoderBlock2D.  Output [nimg, (H-2)/2+1, (W-2)/2+1, Cout].
+extern "C" int vst_conv3x3_down_pad0(const void* x, int C, int nimg, int H, int W, const void* Wt, int Cout,
+                                     const float* bias, void* out, int ldc, void* workspace, size_t ws_bytes,
+                                     void* stream) {
+  return conv3x3_impl(x, C, nullptr, 0, nimg, H, W, 2, 0, 1, Wt, Cout, bias, nullptr, 1, 0, nullptr, 0, out, ldc, 0,
+                      0, workspace, ws_bytes, stream);
+}
+
+// C[M][N] (fp32, row stride N) = A[M][K] . W[N][K]^T with no rounding of the accumulator: the ring kernel's split-K slab
+// epilogue with one split.  For attention scores whose softmax must see fp32 logits (the SDXL VAE mid-block attention,
+// head_dim 512, fp32 in the reference: inference_animatediff.py:164-169).
+extern "C" int vst_gemm_f32out(const void* A, int lda, const void* W, int ldw, int M, int N, int K, float* C,
+                               void* stream) {
+  if (!A || !W || !C || M <= 0 || N <= 0 || K <= 0) return VST_ERR_ARG;
+  if ((K & 7) || (lda & 7) || (ldw & 7) || (N & 3)) return VST_ERR_ARG;
+  GemmArgs a{};
+  a.A1 = (const bf16_t*)A; a.lda1 = lda; a.lda2 = lda; a.K1 = K;
+  a.Wt = (const bf16_t*)W; a.ldw = ldw; a.M = M; a.N = N; a.K = K;
+  a.C = nullptr; a.ldc = N; a.ws = C; a.splits = 1; a.stride = 1;
+  a.a1_bytes = clamp_bytes(((size_t)(M - 1) * lda + K) * 2);
+  a.w_bytes = clamp_bytes(((size_t)(N - 1) * ldw + K) * 2);
+  int tile = 0, splits = 1;
+  choose(M, N, K, 0, 0, 0, tile, splits);
+  if (tile == 8) tile = 3;
+  a.ablate = gemm_ablate_env();
+  a.group_m = gemm_group_env();
+  return launch_gemm_ring(a, 0, 2, tile, 1, (hipStream_t)stream);
 }
 
 extern "C" int vst_conv3x3(const void* x1, int C1, const void* x2, int C2, int nimg, int H, int W, int stride,

@@ -197,7 +197,7 @@ __device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const i
         ok = ok && uy >= 0 && uy < 2 * p.H && ux >= 0 && ux < 2 * p.W;
         iy = uy >> 1; ix = ux >> 1;
       } else {
-        iy = oyv[q] * p.stride + ky - 1; ix = oxv[q] * p.stride + kx - 1;
+        iy = oyv[q] * p.stride + ky - 1 + p.pad0; ix = oxv[q] * p.stride + kx - 1 + p.pad0;
         ok = ok && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
       }
       bA[q] = ok ? (uint32_t)(((rowA[q] * p.H + iy) * p.W + ix) * cs + lchunk * 8) * 2u : (uint32_t)kOOB;

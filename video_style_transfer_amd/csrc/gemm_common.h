@@ -9,6 +9,7 @@ struct GemmArgs {
   int lda1, lda2, K1;
   // conv geometry (AMODE 1/2): input NHWC [nimg, H, W, C1 (+C2)] -> output [nimg, OH, OW, N]
   int H, W, C1, C2, OH, OW, stride, up;
+  int pad0;  // 1: no top/left padding (F.pad (0,1,0,1) + stride-2 conv of diffusers Downsample2D(padding=0))
   const bf16_t* Wt; int ldw;
   int M, N, K;
   const float* bias;

@@ -565,3 +565,95 @@ def probe_hbm_read_gbs(device, nbytes=4 << 30, grid=4096, reps=3):
         best = max(best, nbytes / (s.elapsed_time(e) * 1e-3) / 1e9)
     del buf
     return best
+
+
+# ---- SDXL VAE (AutoencoderKL) pieces (vae.py) ----
+def conv3x3_down_pad0(x: torch.Tensor, nimg: int, H: int, W: int, w: torch.Tensor, bias: torch.Tensor | None,
+                      out: torch.Tensor | None = None) -> torch.Tensor:
+    """diffusers Downsample2D(padding=0): F.pad(x, (0,1,0,1)) + 3x3 stride-2 conv, NHWC.  Returns
+    [nimg*((H-2)//2+1)*((W-2)//2+1), Cout]."""
+    _dev(x, BF16, "x")
+    _dev(w, BF16, "w")
+    C, Cout = x.shape[1], w.shape[0]
+    if not x.is_contiguous() or x.shape[0] != nimg * H * W or w.shape[1] != 9 * C or C % 64:
+        raise _lib.VstError("conv3x3_down_pad0: x [nimg*H*W, C] contiguous, C % 64 == 0, w [Cout, 9C]")
+    OH, OW = (H - 2) // 2 + 1, (W - 2) // 2 + 1
+    M = nimg * OH * OW
+    if out is None:
+        out = torch.empty((M, Cout), dtype=BF16, device=x.device)
+    if bias is not None and (bias.dtype != F32 or bias.numel() != Cout):
+        raise _lib.VstError("conv3x3_down_pad0: bias must be fp32 [Cout]")
+    with _Rec("conv3x3", 2.0 * M * Cout * 9 * C, 2.0 * (nimg * H * W * C + Cout * 9 * C + M * Cout),
+              lambda: gemm_kernel_name(M, Cout, 9 * C, 2), (M, Cout, 9 * C)):
+        ws = _workspace(x.device)
+        _lib.call("vst_conv3x3_down_pad0", _p(x), C, nimg, H, W, _p(w), Cout, _p(bias), _p(out), _ld(out), _p(ws),
+                  _WS_BYTES, _stream())
+    return out
+
+
+def gemm_f32out(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """fp32 [M, N] = a[M, K] @ w[N, K]^T without rounding the accumulator."""
+    _dev(a, BF16, "a")
+    _dev(w, BF16, "w")
+    M, K = a.shape
+    N = w.shape[0]
+    if w.shape[1] != K:
+        raise _lib.VstError(f"gemm_f32out: a {tuple(a.shape)} vs w {tuple(w.shape)}")
+    if out is None:
+        out = torch.empty((M, N), dtype=F32, device=a.device)
+    if out.dtype != F32 or not out.is_contiguous() or out.shape != (M, N):
+        raise _lib.VstError("gemm_f32out: out must be contiguous fp32 [M, N]")
+    with _Rec("gemm_f32out", 2.0 * M * N * K, 2.0 * (M * K + N * K) + 4.0 * M * N,
+              lambda: gemm_kernel_name(M, N, K, 0), (M, N, K)):
+        _lib.call("vst_gemm_f32out", _p(a), _ld(a), _p(w), _ld(w), M, N, K, _p(out), _stream())
+    return out
+
+
+def softmax_rows(s: torch.Tensor, scale: float, out: torch.Tensor | None = None) -> torch.Tensor:
+    """bf16 softmax(scale * s) over the last dim of an fp32 [rows, n] matrix."""
+    if not s.is_cuda or s.dtype != F32 or s.dim() != 2 or s.stride(1) != 1:
+        raise _lib.VstError("softmax_rows: s must be an fp32 2-D row-major device view")
+    rows, n = s.shape
+    if out is None:
+        out = torch.empty((rows, n), dtype=BF16, device=s.device)
+    _dev(out, BF16, "out")
+    with _Rec("softmax", 0.0, 4.0 * rows * n + 2.0 * rows * n):
+        _lib.call("vst_softmax_rows", _p(s), _ld(s), rows, n, float(scale), _p(out), _ld(out), _stream())
+    return out
+
+
+def nchw_to_nhwc(x: torch.Tensor, mul: float = 1.0, ldd: int | None = None) -> torch.Tensor:
+    """fp32 (n, C, H, W) -> bf16 [n*H*W, ldd] (channels >= C zero)."""
+    if not x.is_cuda or x.dtype != F32 or x.dim() != 4 or not x.is_contiguous():
+        raise _lib.VstError("nchw_to_nhwc: x must be a contiguous fp32 (n, C, H, W) device tensor")
+    n, C, H, W = x.shape
+    ldd = ldd or C
+    out = torch.empty((n * H * W, ldd), dtype=BF16, device=x.device)
+    _lib.call("vst_nchw_to_nhwc", _p(x), n, C, H * W, float(mul), _p(out), ldd, _stream())
+    return out
+
+
+def nhwc_to_nchw(x: torch.Tensor, n: int, C: int, H: int, W: int) -> torch.Tensor:
+    """bf16 [n*H*W, >=C] -> fp32 (n, C, H, W)."""
+    _dev(x, BF16, "x")
+    out = torch.empty((n, C, H, W), dtype=F32, device=x.device)
+    _lib.call("vst_nhwc_to_nchw", _p(x), _ld(x), n, C, H * W, _p(out), _stream())
+    return out
+
+
+def frames_to_u8(x: torch.Tensor, n: int, C: int, H: int, W: int) -> torch.Tensor:
+    """bf16 [n*H*W, >=C] decoder output -> uint8 (n, H, W, C) frames (inference_animatediff.py:141-143)."""
+    _dev(x, BF16, "x")
+    out = torch.empty((n, H, W, C), dtype=torch.uint8, device=x.device)
+    _lib.call("vst_frames_to_u8", _p(x), _ld(x), n, C, H * W, _p(out), _stream())
+    return out
+
+
+def vae_sample(moments: torch.Tensor, n: int, H: int, W: int, eps: torch.Tensor | None, mul: float) -> torch.Tensor:
+    """moments bf16 [n*H*W, >=8] -> fp32 (n, 4, H, W) = (mean + exp(logvar/2) * eps) * mul (eps None: mean * mul)."""
+    _dev(moments, BF16, "moments")
+    if eps is not None and (eps.dtype != F32 or not eps.is_contiguous() or eps.shape != (n, 4, H, W)):
+        raise _lib.VstError("vae_sample: eps must be contiguous fp32 (n, 4, H, W)")
+    out = torch.empty((n, 4, H, W), dtype=F32, device=moments.device)
+    _lib.call("vst_vae_sample", _p(moments), _ld(moments), n, H * W, _p(eps), float(mul), _p(out), _stream())
+    return out

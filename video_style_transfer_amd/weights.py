@@ -194,3 +194,61 @@ def synthetic_state_dict(cfg: UNetMotionConfig, seed: int = 0, lora_rank: int | 
     for name, (shape, kind) in param_shapes(cfg, lora_rank).items():
         out[name] = _init_value(name, shape, kind, g, "cpu").to(dtype)
     return out
+
+
+def _vae_resnet(S, name, cin, cout):
+    _norm(S, name + ".norm1", cin)
+    _conv(S, name + ".conv1", cout, cin)
+    _norm(S, name + ".norm2", cout)
+    _conv(S, name + ".conv2", cout, cout, kind="wo")
+    if cin != cout:
+        _conv(S, name + ".conv_shortcut", cout, cin, k=1)
+
+
+def _vae_mid(S, name, C):
+    _vae_resnet(S, name + ".resnets.0", C, C)
+    a = name + ".attentions.0"
+    _norm(S, a + ".group_norm", C)
+    for p in ("to_q", "to_k", "to_v"):
+        _linear(S, f"{a}.{p}", C, C)
+    _linear(S, a + ".to_out.0", C, C, kind="wo")
+    _vae_resnet(S, name + ".resnets.1", C, C)
+
+
+def vae_param_shapes(cfg) -> "OrderedDict[str, tuple]":
+    """name -> (shape, init kind) of diffusers AutoencoderKL (encoder / decoder / quant_conv / post_quant_conv)."""
+    S: "OrderedDict[str, tuple]" = OrderedDict()
+    ch, L, n = cfg.block_out_channels, cfg.latent_channels, cfg.layers_per_block
+    _conv(S, "encoder.conv_in", ch[0], cfg.in_channels)
+    out_c = ch[0]
+    for i in range(len(ch)):
+        in_c, out_c = out_c, ch[i]
+        for j in range(n):
+            _vae_resnet(S, f"encoder.down_blocks.{i}.resnets.{j}", in_c if j == 0 else out_c, out_c)
+        if i < len(ch) - 1:
+            _conv(S, f"encoder.down_blocks.{i}.downsamplers.0.conv", out_c, out_c)
+    _vae_mid(S, "encoder.mid_block", ch[-1])
+    _norm(S, "encoder.conv_norm_out", ch[-1])
+    _conv(S, "encoder.conv_out", 2 * L, ch[-1])
+    _conv(S, "quant_conv", 2 * L, 2 * L, k=1)
+    _conv(S, "post_quant_conv", L, L, k=1)
+    _conv(S, "decoder.conv_in", ch[-1], L)
+    _vae_mid(S, "decoder.mid_block", ch[-1])
+    rch = list(reversed(ch))
+    out_c = rch[0]
+    for i in range(len(ch)):
+        prev_c, out_c = out_c, rch[i]
+        for j in range(n + 1):
+            _vae_resnet(S, f"decoder.up_blocks.{i}.resnets.{j}", prev_c if j == 0 else out_c, out_c)
+        if i < len(ch) - 1:
+            _conv(S, f"decoder.up_blocks.{i}.upsamplers.0.conv", out_c, out_c)
+    _norm(S, "decoder.conv_norm_out", ch[0])
+    _conv(S, "decoder.conv_out", cfg.out_channels, ch[0], kind="wo")
+    return S
+
+
+def vae_synthetic_state_dict(cfg, seed: int = 0, dtype: torch.dtype = torch.float32) -> "OrderedDict[str, torch.Tensor]":
+    """Seeded synthetic AutoencoderKL weights (same distributions as synthetic_state_dict; no checkpoint offline)."""
+    g = torch.Generator().manual_seed(seed)
+    return OrderedDict((name, _init_value(name, shape, kind, g, "cpu").to(dtype))
+                       for name, (shape, kind) in vae_param_shapes(cfg).items())
