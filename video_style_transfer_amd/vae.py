@@ -264,14 +264,15 @@ class AutoencoderKL(nn.Module):
         n, L, h, w = z.shape
         wq, bq = _padded_kernel_weight(self.post_quant_conv, 8, 8)
         outs = []
-        step = self._chunk(n, h, w, 8)
+        f = 2 ** (len(self.cfg.block_out_channels) - 1)
+        step = self._chunk(n, h, w, f)
         for i in range(0, n, step):
             c = min(step, n - i)
             z8 = K.nchw_to_nhwc(z[i:i + c].float().contiguous(), 1.0, ldd=8)
             z8 = K.linear(z8, wq, bq)
             y, H, W = self.decoder.run(z8, c, h, w)
             outs.append((y, c))
-        return outs, 8 * h, 8 * w
+        return outs, f * h, f * w
 
     def decode(self, z: torch.Tensor, return_dict: bool = True):
         """z: (n, latent, h, w) (already divided by scaling_factor) -> DecoderOutput(sample (n, 3, 8h, 8w) fp32)."""
