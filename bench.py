@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-peaks", action="store_true", help="skip the MFMA / HBM ceiling probes")
     ap.add_argument("--cpu-sample-frames", type=int, default=2)
+    ap.add_argument("--no-vae", action="store_true", help="skip the VAE decode record (denoise) / the per-step VAE "
+                    "encode of the training frames (--train: the step then starts from synthetic latents)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--train", action="store_true",
                     help="BASELINE configs[4]: one train_animatediff.py optimizer step per rank (fwd+bwd on a 16-frame "
@@ -186,6 +188,35 @@ def measured_peaks(dev, rl):
                       "vst_probe_hbm_read: 4 GiB streamed with 16-B non-temporal loads"}
 
 
+def vae_decode_timing(args, den, dev, ms_step):
+    """The clip's VAE decode after the loop (inference_animatediff.py:137-144; outside the metric):
+    SDXL AutoencoderKL (synthetic weights) decoding this rank's frames to uint8, timed over 3 runs, with its
+    algorithmic flops from the instrumented launches and the end-to-end rate (50 denoise steps + decode)."""
+    from video_style_transfer_amd import kernels as K
+    from video_style_transfer_amd.config import VAEConfig
+    from video_style_transfer_amd.vae import build_vae
+    vae = build_vae(VAEConfig.sdxl(), seed=args.seed, device=dev)
+    frames = den.decode(vae)  # warm-up (weight layouts, workspaces)
+    K.profile_launches(True)
+    den.decode(vae)
+    fl = sum(r[2] for r in K.collect_launches())
+    K.profile_launches(False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        frames = den.decode(vae)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / 3 * 1e3
+    n = frames.shape[0]
+    del vae
+    torch.cuda.empty_cache()
+    return {"ms_per_clip": round(ms, 2), "frames": n, "frames_per_s": round(n / (ms * 1e-3), 2),
+            "alg_tflop": round(fl / 1e12, 2), "tflops": round(fl / (ms * 1e-3) / 1e12, 1),
+            "frac": round(fl / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4), "output": list(frames.shape[1:]),
+            "end_to_end_frames_per_s": round(n / (args.num_inference_steps * ms_step * 1e-3 + ms * 1e-3), 4),
+            "note": "SDXL VAE decode to uint8 frames (bf16, frames batched); not part of the denoise metric"}
+
+
 def cpu_baseline(args, cfg):
     """Oracle (fp32 CPU restatement) timed on a bounded sample: one UNet forward (one CFG branch)
     of a `cpu_sample_frames`-frame clip at the bench resolution; extrapolated to frames/s of the
@@ -279,15 +310,28 @@ def bench_train(args, world, rank, local, dev):
     g = torch.Generator().manual_seed(100 + rank)
     h = args.size // 8
     lat = torch.randn(1, 4, args.frames, h, h, generator=g).to(dev)
+    vae = frames = None
+    if not args.no_vae:
+        # train_animatediff.py:219-224 inside every step: the clip's frames (synthetic, in [-1, 1]) -> VAE encode ->
+        # latent_dist.sample() * scaling_factor (fp32 VAE in the reference; the HIP VAE, bf16, frames batched)
+        from video_style_transfer_amd.config import VAEConfig
+        from video_style_transfer_amd.train import encode_frames
+        from video_style_transfer_amd.vae import build_vae
+        vae = build_vae(VAEConfig.sdxl(), seed=args.seed + 1, device=dev)
+        frames = (torch.rand(1, args.frames, 3, args.size, args.size, generator=g) * 2 - 1).to(dev)
+        vgen = torch.Generator(device=dev).manual_seed(200 + rank)
+        lat = encode_frames(vae, frames, vgen)
     enc = torch.randn(1, 77, cfg.cross_attention_dim, generator=g)
     pooled = torch.randn(1, cfg.text_embed_dim, generator=g)
     unc, unp = torch.zeros_like(enc), torch.zeros_like(pooled)
     if graph:
         step.capture(lat, enc, pooled, uncond_prompt=unc, uncond_pooled=unp)
-        run = step.replay
+
+        def run():
+            return step.replay(None if vae is None else encode_frames(vae, frames, vgen))
     else:
         def run():
-            return step(lat, enc, pooled, unc, unp)
+            return step(lat if vae is None else encode_frames(vae, frames, vgen), enc, pooled, unc, unp)
     t_build = time.perf_counter() - t_build
     for _ in range(args.warmup):
         run()
@@ -314,7 +358,7 @@ def bench_train(args, world, rank, local, dev):
     if not args.no_roofline:
         # one instrumented eager step (HIP events around every launch on its stream)
         K.profile_launches(True)
-        step(lat, enc, pooled)
+        step(lat if vae is None else encode_frames(vae, frames, vgen), enc, pooled)
         rl, table = _roofline_from(K.collect_launches())
         K.profile_launches(False)
         fl = rl.pop("step_flops")
@@ -334,7 +378,9 @@ def bench_train(args, world, rank, local, dev):
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
             "config": {"workload": f"BASELINE configs[4]: train_animatediff.py step, {args.frames}x{args.size}x"
                                    f"{args.size} clip/GPU, temporal LoRA r=32, UnZipLoRA r={args.lora_rank} frozen, "
-                                   f"orth loss 1e-4, clip 0.5, AdamW",
+                                   f"orth loss 1e-4, clip 0.5, AdamW" + (
+                                       ", from synthetic latents (no VAE encode)" if vae is None else
+                                       ", VAE encode of the synthetic frames in every step"),
                        "model": "SDXL UNet + AnimateDiff-SDXL motion modules (synthetic weights)",
                        "global_batch": world, "frames": args.frames, "resolution": args.size,
                        "parallelism": f"dp{world}" + (" (RCCL bucketed all-reduce)" if world > 1 else ""),
@@ -442,6 +488,7 @@ def main():
             rl["peak_measured"] = measured_peaks(dev, rl)
             step["frac_of_measured"] = round(step["achieved_tflops"] / rl["peak_measured"]["mfma_bf16_tflops"], 4)
     graphed = den.graph is not None
+    vae_rec = None if args.no_vae else vae_decode_timing(args, den, dev, ms_step)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         del den, unet
@@ -466,7 +513,8 @@ def main():
                                        f"replicas x{world}" if world > 1 else "single") + (
                                        f", {nclips} clips batched per GPU" if shard is None and nclips > 1 else ""),
                        "graph": graphed, "note": graph_note},
-            "roofline": rl, "step_roofline": step, "cpu_baseline": cpu, "kernels": table, "finite": ok,
+            "roofline": rl, "step_roofline": step, "vae_decode": vae_rec, "cpu_baseline": cpu, "kernels": table,
+            "finite": ok,
             "setup_s": round(t_build, 1),
         }
         print(json.dumps(out))

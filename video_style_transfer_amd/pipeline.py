@@ -142,3 +142,9 @@ class AnimateDiffDenoiser:
         else:
             self.set_latents(latents)
         return self.run_steps()
+
+    def decode(self, vae) -> torch.Tensor:
+        """inference_animatediff.py:137-144 for the frames this rank holds: latents / scaling_factor -> VAE decode ->
+        uint8 (clips * F_local, 8h, 8w, 3) on the device.  Frame-sharded runs decode their own frames (no exchange);
+        the frames of a clip are decoded together instead of one vae.decode call per frame."""
+        return torch.cat([vae.decode_to_frames(self.lat[c:c + 1]) for c in range(self.lat.shape[0])])

@@ -272,3 +272,14 @@ class TrainStep:
         if self.lr_scheduler is not None:
             self.lr_scheduler.step()
         return self.s_out
+
+
+def encode_frames(vae, frames: torch.Tensor, generator: Optional[torch.Generator] = None) -> torch.Tensor:
+    """train_animatediff.py:219-224 + :238-246: frames (B, F, 3, H, W) in [-1, 1] -> VAE encode (no grad) ->
+    latent_dist.sample() * scaling_factor -> (B, 4, F, h, w) fp32, the layout TrainStep takes."""
+    B, F = frames.shape[:2]
+    with torch.no_grad():
+        flat = frames.reshape(B * F, *frames.shape[2:]).float()
+        lat = vae.encode(flat).latent_dist.sample(generator, scale=vae.config.scaling_factor)
+    return lat.view(B, F, *lat.shape[1:]).permute(0, 2, 1, 3, 4).contiguous()
+
