@@ -68,6 +68,21 @@ constexpr int SA_KT = 64;                         // keys per tile
 constexpr int SA_TILE = SA_KT * 64 * 2;           // 8 KiB
 constexpr int SA_LDS = 4 * SA_TILE;               // K,V double-buffered
 
+typedef __attribute__((address_space(3))) void sa_lds_void;
+
+// One 1-KiB LDS-DMA piece: 64 lanes x 16 B, lane-linear in LDS at `lds_piece` (wave-uniform).
+__device__ __forceinline__ void sa_dma16(__amdgpu_buffer_rsrc_t r, char* lds_piece, int off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(
+      r, (sa_lds_void*)((__attribute__((address_space(3))) char*)(uintptr_t)lds_piece), 16, off, 0, 0, 0);
+}
+
+// PRE = 0: K/V tiles of 64 keys double-buffered through registers (long key ranges: the 32x32 / 64x64 levels).
+// PRE = n (1..4, Nk <= 64 n): the whole K/V of the (batch, head) is brought into LDS up front by LDS-DMA -- every
+// load of the workgroup in flight at once, no per-tile barrier -- for the 77 text tokens of cross-attention, where
+// the short key loop left one HBM latency exposed per tile (dispatch: up to two tiles, see vst_spatial_attention).  The DMA writes each
+// 8-row piece lane-linearly, so each lane fetches the global chunk that the tile's swizzle (k_off / v_off) puts at
+// its LDS slot.
+template <int PRE>
 __global__ __launch_bounds__(256, 2) void spatial_attn_kernel(
     const bf16_t* __restrict__ Q, int ldq, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V, int ldkv,
     bf16_t* __restrict__ O, int ldo, int nbatch, int heads, int Nq, int Nk, int kv_div, float scale_log2,
@@ -138,13 +153,31 @@ __global__ __launch_bounds__(256, 2) void spatial_attn_kernel(
     const int li = lane & 15, r0 = g * 4 + (li >> 2), col = db * 16 + (li & 3) * 4;
     voff[db] = v_off(r0, col >> 3) + (col & 7) * 2;
   }
-  load_kv(0);
-  store_kv(0);
+  if constexpr (PRE == 0) {
+    load_kv(0);
+    store_kv(0);
+  } else {
+    // pieces: tile t, operand (K, V), 8-row piece p; wave w issues p = w and p = w + 4 of every tile and operand
+    const int prow = lane >> 3, pslot = lane & 7;
+#pragma unroll
+    for (int t = 0; t < PRE; ++t)
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) {
+        const int row = (wid + 4 * pp) * 8 + prow;
+        const int key = t * SA_KT + row;
+        const int ck = pslot ^ ((row >> 1) & 7), cv = pslot ^ (((row >> 1) & 3) << 1);
+        const int base = (bkv * Nk + key) * ldkv + h * 64;
+        char* dst = smem + t * 2 * SA_TILE + (wid + 4 * pp) * 1024;
+        sa_dma16(rk, dst, key < Nk ? (base + ck * 8) * 2 : kOOB);
+        sa_dma16(rv, dst + SA_TILE, key < Nk ? (base + cv * 8) * 2 : kOOB);
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __syncthreads();
 
   for (int t = 0; t < nt; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < nt) load_kv(t + 1);
+    const int cur = PRE ? t : (t & 1);
+    if (PRE == 0 && t + 1 < nt) load_kv(t + 1);
     const char* Ks = smem + cur * 2 * SA_TILE;
     const char* Vs = Ks + SA_TILE;
 
@@ -223,8 +256,10 @@ __global__ __launch_bounds__(256, 2) void spatial_attn_kernel(
           o[db][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[st][qb], o[db][qb], 0, 0, 0);
       }
     }
-    if (t + 1 < nt) store_kv(cur ^ 1);
-    __syncthreads();
+    if constexpr (PRE == 0) {
+      if (t + 1 < nt) store_kv(cur ^ 1);
+      __syncthreads();
+    }
   }
 
   // ---- finalize: O[q][d] = O^T[d][q] / l ----
@@ -950,9 +985,31 @@ extern "C" int vst_spatial_attention(const void* q, int ldq, const void* k, cons
   const uint32_t qb = clampb(((size_t)(nbatch * Nq - 1) * ldq + heads * 64) * 2);
   // K and V may be column views of one fused buffer; each rsrc is sized from its own base
   const uint32_t kvb_v = clampb(((size_t)(nkv * Nk - 1) * ldkv + heads * 64) * 2);
-  hipLaunchKernelGGL(spatial_attn_kernel, dim3(nqb * heads * nbatch), dim3(256), SA_LDS, (hipStream_t)stream,
-                     (const bf16_t*)q, ldq, (const bf16_t*)k, (const bf16_t*)v, ldkv, (bf16_t*)o, ldo, nbatch, heads,
-                     Nq, Nk, kv_div, scale * 1.4426950408889634f, qb, kvb_v, lse);
+  const int nt = (Nk + SA_KT - 1) / SA_KT;
+  static int pre_env = -1;  // VST_SA_PRELOAD=0 disables the whole-K/V preload (A/B diagnostics)
+  if (pre_env < 0) {
+    const char* e = getenv("VST_SA_PRELOAD");
+    pre_env = e ? atoi(e) : 1;
+  }
+  // measured (tools/attn_bench.py, one process, alternating): cross-attention over 77 text keys 33 -> 28.5 us at 32x32
+  // and 18 -> 17.3 us at 16x16; the 16x16 self-attention (4 tiles) 29.2 -> 31.2 us (64 KiB of LDS per workgroup
+  // drops occupancy from 3 to 2 workgroups per CU), so only up to two tiles are preloaded
+  const int pre = pre_env && nt <= 2 ? nt : 0;
+  const dim3 grid(nqb * heads * nbatch);
+  const size_t lds = pre ? (size_t)pre * 2 * SA_TILE : SA_LDS;
+  hipStream_t st = (hipStream_t)stream;
+  const float sl2 = scale * 1.4426950408889634f;
+#define VST_SA_LAUNCH(P)                                                                                         \
+  hipLaunchKernelGGL(spatial_attn_kernel<P>, grid, dim3(256), lds, st, (const bf16_t*)q, ldq, (const bf16_t*)k, \
+                     (const bf16_t*)v, ldkv, (bf16_t*)o, ldo, nbatch, heads, Nq, Nk, kv_div, sl2, qb, kvb_v, lse)
+  switch (pre) {
+    case 1: VST_SA_LAUNCH(1); break;
+    case 2: VST_SA_LAUNCH(2); break;
+    case 3: VST_SA_LAUNCH(3); break;
+    case 4: VST_SA_LAUNCH(4); break;
+    default: VST_SA_LAUNCH(0); break;
+  }
+#undef VST_SA_LAUNCH
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 
