@@ -40,6 +40,19 @@ static_assert(P8Cfg::LDS <= 160 * 1024, "LDS budget");
 
 typedef __attribute__((address_space(3))) void p8_lds_void;
 
+#ifdef VST_P8_TRACE
+// diagnostics build only (tools/p8_trace.py): per-workgroup wall-clock (100 MHz) and shader-clock stamps at
+// kernel entry, first operands landed, k-loop done, epilogue done
+__device__ unsigned long long vst_p8_trace_buf[8192 * 8];
+#define VST_P8_STAMP(I)                                                                    \
+  if (threadIdx.x == 0 && blockIdx.x < 8192) {                                             \
+    vst_p8_trace_buf[blockIdx.x * 8 + 2 * (I)] = __builtin_amdgcn_s_memrealtime();         \
+    vst_p8_trace_buf[blockIdx.x * 8 + 2 * (I) + 1] = __builtin_readcyclecounter();         \
+  }
+#else
+#define VST_P8_STAMP(I)
+#endif
+
 __device__ __forceinline__ void p8_dma16(__amdgpu_buffer_rsrc_t r, char* lds_piece, int off) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(
       r, (p8_lds_void*)((__attribute__((address_space(3))) char*)(uintptr_t)lds_piece), 16, off, 0, 0, 0);
@@ -83,6 +96,12 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   const int nk = (p.K + 63) / 64;
   const bool ktail = (p.K & 63) != 0;
   const bool late = wid >= 4;
+#ifdef VST_P8_TRACE
+  // diagnostics build only (VST_GEMM_ABLATE): 1 no loop DMA, 2 no MFMA, 4 no loop vmcnt waits, 16 no fragment reads
+  const int abl = p.ablate;
+#else
+  constexpr int abl = 0;
+#endif
 
   // ---- per-lane DMA descriptors: slot s in {Amq0, Amq1, Bnq0, Bnq1}, piece pc in {0, 1} = slot rows
   //      8*(wid + 8*pc) + (lane >> 3); this lane moves chunk c = (lane & 7) ^ ((row >> 1) & 7) of that row.
@@ -108,6 +127,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   };
   // slot s of k-tile kt into buffer (kt & 1); kt >= kend: out-of-range offsets (zeros), keeps vmcnt counts uniform
   auto dma_slot = [&](int s, int kt, int kend) {
+    if ((abl & 1) && kt > 1) return;
     char* dst = smem + (kt & 1) * BUF + s * SLOT + wid * 1024;
     const int k0 = kt * 64;
     const bool live = kt < kend;
@@ -133,7 +153,12 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   f32x4 acc[8][4];
   bf16x8 fa[4][2];         // A fragments of the current row quadrant (mq): 4 x 16 rows x 2 k-halves
   bf16x8 fb0[2][2], fb1[2][2];  // W fragments of column quadrants nq0 / nq1
+#ifdef VST_P8_TRACE
+  for (int i = 0; i < 4; ++i) for (int h = 0; h < 2; ++h) fa[i][h] = bf16x8{};
+  for (int j = 0; j < 2; ++j) for (int h = 0; h < 2; ++h) fb0[j][h] = fb1[j][h] = bf16x8{};
+#endif
   auto read_a = [&](int buf, int mq) {
+    if (abl & 16) return;
     const char* S = smem + buf * BUF + mq * SLOT;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -141,6 +166,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       for (int h = 0; h < 2; ++h) fa[i][h] = *reinterpret_cast<const bf16x8*>(S + p8_off(wr * 64 + i * 16 + fr, h * 4 + fq));
   };
   auto read_b = [&](int buf, int nq, bf16x8 (&fb)[2][2]) {
+    if (abl & 16) return;
     const char* S = smem + buf * BUF + (2 + nq) * SLOT;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
@@ -148,7 +174,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       for (int h = 0; h < 2; ++h) fb[j][h] = *reinterpret_cast<const bf16x8*>(S + p8_off(wc * 32 + j * 16 + fr, h * 4 + fq));
   };
 #define VST_P8_QUAD(MQ, NQ, FB)                                                                        \
-  {                                                                                                  \
+  if (!(abl & 2)) {                                                                                  \
     __builtin_amdgcn_s_setprio(1);                                                                   \
     _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j)      \
         _Pragma("unroll") for (int h = 0; h < 2; ++h) acc[(MQ) * 4 + i][(NQ) * 2 + j] =              \
@@ -167,6 +193,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     dma_slot(0, kb + 1, ke); dma_slot(2, kb + 1, ke); dma_slot(3, kb + 1, ke);
     asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // Amq0(kb), Bnq0(kb) landed
     p8_barrier();
+    VST_P8_STAMP(1)
     if (late) p8_barrier();
 
     for (int t = kb; t < ke; ++t) {
@@ -174,14 +201,14 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       // phase 0: Q(0,0)
       read_a(buf, 0);
       read_b(buf, 0, fb0);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Bnq1(t) landed
+      if (!(abl & 4)) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Bnq1(t) landed
       dma_slot(1, t + 1, ke);
       p8_barrier();
       VST_P8_QUAD(0, 0, fb0)
       p8_barrier();
       // phase 1: Q(0,1)
       read_b(buf, 1, fb1);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Amq1(t) landed
+      if (!(abl & 4)) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Amq1(t) landed
       p8_barrier();
       VST_P8_QUAD(0, 1, fb1)
       p8_barrier();
@@ -193,7 +220,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       VST_P8_QUAD(1, 1, fb1)
       p8_barrier();
       // phase 3: Q(1,0)
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Amq0(t+1), Bnq0(t+1) landed
+      if (!(abl & 4)) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Amq0(t+1), Bnq0(t+1) landed
       dma_slot(3, t + 2, ke);
       p8_barrier();
       VST_P8_QUAD(1, 0, fb0)
@@ -207,10 +234,17 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
 
   if constexpr (!SK) {
     int m0, n0;
+    VST_P8_STAMP(0)
     tile_origin(xcd_remap(blockIdx.x, ntiles), m0, n0);
     setup_tile(m0, n0);
     run_segment(0, nk);
+    VST_P8_STAMP(2)
     tile_epilogue<P8Cfg, EPI>(p, smem, m0, n0, acc, wr, wc);
+#ifdef VST_P8_TRACE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#endif
+    VST_P8_STAMP(3)
   } else {
     // Launched only with fewer tiles than workgroups, so a workgroup's share (< nk k-tiles) meets at most two
     // tiles: first the tail of one (contributor, unless the share starts on a tile boundary), then the head of the
@@ -301,3 +335,11 @@ int launch_gemm_p8(const GemmArgs& a, int epi, hipStream_t s) {
 }
 
 }  // namespace vst
+
+#ifdef VST_P8_TRACE
+extern "C" int vst_p8_trace_read(void* host_dst, int n_wg) {
+  if (n_wg > 8192) n_wg = 8192;
+  return hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(vst::vst_p8_trace_buf), (size_t)n_wg * 64, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : 2;
+}
+#endif
