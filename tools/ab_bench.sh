@@ -1,0 +1,18 @@
+#!/bin/bash
+# Same-box A/B of the denoise step over library builds: bash tools/ab_bench.sh new nofast old ...
+# "new" = the in-tree .so, any other name = abx/libvst_<name>.so (tools/ab_lib.sh, tools/ring_variants.sh).
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+for tag in "$@"; do
+  if [ "${tag%%[0-9]*}" = new ]; then unset VST_LIB_AB; else export VST_LIB_AB=abx/libvst_${tag%%[0-9]*}.so; fi
+  VST_BENCH_SHAPES=1 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-peaks \
+    > gpurun_out/ab_$tag.json 2> gpurun_out/ab_$tag.err || { tail -20 gpurun_out/ab_$tag.err; exit 1; }
+  python - "$tag" <<'PY'
+import json, sys
+d = json.load(open(f"gpurun_out/ab_{sys.argv[1]}.json"))
+k = d["kernels"]
+print(sys.argv[1], "ms/step", d["ms_per_step"], "|", "  ".join(f"{n} {v['ms_per_step']:.2f}" for n, v in list(k.items())[:6]))
+print("   fused:", {s: v["ms_per_step"] for s, v in d["roofline"]["fused_lora_gemms"].items()})
+PY
+done

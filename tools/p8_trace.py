@@ -39,6 +39,14 @@ def main():
         b = torch.randn(N, device=dev, generator=g) * 0.1
         r = torch.randn(M, N // 2 if geglu else N, device=dev, generator=g).to(BF) if res else None
         fl = 2.0 * M * N * Kt
+        if not geglu and not abl:  # correctness of this build against fp32 torch on the same bf16 operands
+            xc = torch.cat([x, x2], 1) if K2 else x
+            ref = xc.float() @ w.float().t() + b
+            if res:
+                ref = ref.to(BF).float() + r.float()
+            out = K.linear(x, w, b, x2=x2, residual=r).float()
+            print(f"{name} rel-L2 vs fp32 torch {((out - ref).norm() / ref.norm()).item():.2e}", flush=True)
+            del xc, ref, out
         for _ in range(5):
             K.linear(x, w, b, x2=x2, residual=r, geglu=geglu)
         torch.cuda.synchronize()

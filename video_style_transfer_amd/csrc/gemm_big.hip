@@ -205,10 +205,10 @@ __device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const i
   };
   int offs[Cfg::DPT];
   bool a_second = false;
-  auto prep = [&](int kt) {
+  auto prep = [&](int kt, auto fast_tag) {  // fast: the k-tile lies fully inside K (no per-lane tail check)
     const int k0 = kt * RBK;
     const uint32_t kb = (uint32_t)k0 * 2u;
-    const bool kin = !ktail || (k0 + lchunk * 8 < p.K);
+    const bool kin = decltype(fast_tag)::value || !ktail || (k0 + lchunk * 8 < p.K);
 #pragma unroll
     for (int q = 0; q < Cfg::B_PIECES; ++q) offs[q] = kin ? (int)(bB[q] + kb) : kOOB;
     if constexpr (Cfg::B_EXTRA != 0) offs[Cfg::IDX_BX] = kin ? (int)(bB[Cfg::B_PIECES] + kb) : kOOB;
@@ -245,8 +245,8 @@ __device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const i
       dma16(a_second ? ra2 : ra1, As + (q * Cfg::NWAVES + wid) * 1024, offs[idx]);
     }
   };
-  auto issue = [&](int kt, int stage) {
-    prep(kt);
+  auto issue = [&](int kt, int stage, auto fast_tag) {
+    prep(kt, fast_tag);
 #pragma unroll
     for (int d = 0; d < Cfg::DPT; ++d) dma_piece(stage, d);
   };
@@ -259,7 +259,12 @@ __device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const i
 
   constexpr int S = Cfg::STAGES;
   const int fr = lane & 15, fq = lane >> 4;
-  const bool no_dma = p.ablate & 1, no_mfma = p.ablate & 2, no_lds = p.ablate & 16;
+#ifdef VST_GEMM_DIAG
+  const int abl = p.ablate;  // VST_GEMM_ABLATE (diagnostics build only, tools/p8_variants.sh)
+#else
+  constexpr int abl = 0;
+#endif
+  const bool no_dma = abl & 1, no_mfma = abl & 2, no_lds = abl & 16;
   typedef bf16x8 FragA[Cfg::MI];
   typedef bf16x8 FragB[Cfg::NJ];
   FragA fa0, fa1;
@@ -275,8 +280,8 @@ __device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const i
     for (int i = 0; i < Cfg::MI; ++i)
       fa[i] = *reinterpret_cast<const bf16x8*>(As + rswz(wr * Cfg::WM + i * 16 + fr, fq));
   };
-  auto mfmas = [&](FragA& ca, FragB& cb) {
-    __builtin_amdgcn_s_setprio(1);
+  auto mfmas = [&](FragA& ca, FragB& cb, auto flip_tag) {  // flip: s_setprio 1/0 around the chain
+    if constexpr (decltype(flip_tag)::value) __builtin_amdgcn_s_setprio(1);
     if (!no_mfma) {
 #pragma unroll
       for (int i = 0; i < Cfg::MI; ++i)
@@ -291,7 +296,7 @@ __device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const i
 #pragma unroll
       for (int j = 0; j < Cfg::NJ; ++j) asm volatile("" ::"v"(cb[j]));
     }
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (decltype(flip_tag)::value) __builtin_amdgcn_s_setprio(0);
   };
 
   if constexpr (Cfg::NWAVES == 8) {
@@ -310,14 +315,21 @@ __device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const i
     const bool late = wid >= 4;
 #pragma unroll
     for (int s = 0; s < S - 1; ++s)
-      if (s < nk) issue(kt0 + s, s);
+      if (s < nk) issue(kt0 + s, s, std::false_type{});
     wait_tiles<Cfg>(min(nk, S - 1) - 1, n_extra);  // own DMA of tile 0 landed
     __builtin_amdgcn_s_barrier();
     if (late) __builtin_amdgcn_s_barrier();
+#ifdef VST_RING_LATEPRIO
+    if (late) __builtin_amdgcn_s_setprio(1);  // static priority for the second-dispatched half
+    using flip_t = std::false_type;
+#else
+    using flip_t = std::true_type;
+#endif
     int wrs = S - 1, rd = 0;
-    for (int it = 0; it < nk; ++it) {
-      const bool steady = it + S - 1 < nk;  // tile it+S-1 exists: issue it, keep S-2 tiles in flight
-      if (steady && !no_dma) issue(kt0 + it + S - 1, wrs);
+    auto ktile = [&](int it, auto fast_tag) {
+      constexpr bool FAST = decltype(fast_tag)::value;  // tile it+S-1 exists and is not the last of K
+      const bool steady = FAST || it + S - 1 < nk;  // tile it+S-1 exists: issue it, keep S-2 tiles in flight
+      if (steady && !no_dma) issue(kt0 + it + S - 1, wrs, fast_tag);
       wrs = wrs + 1 == S ? 0 : wrs + 1;
       load_into(fa0, fb0, rd);
       rd = rd + 1 == S ? 0 : rd + 1;
@@ -325,15 +337,22 @@ __device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const i
       else if (it + 1 < nk) wait_tiles<Cfg>(0, n_extra);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      mfmas(fa0, fb0);
+      mfmas(fa0, fb0, flip_t{});
       __builtin_amdgcn_s_barrier();
-    }
+    };
+    int it = 0;
+    // fast iterations: tile it+S-1 < nk - 1 (and, with a K tail, never the last k-tile of K)
+    const int it_fast = ktail && kt1 == (p.K + RBK - 1) / RBK ? nk - S : nk - S + 1;
+#ifndef VST_RING_NOFAST
+    for (; it < it_fast; ++it) ktile(it, std::true_type{});
+#endif
+    for (; it < nk; ++it) ktile(it, std::false_type{});
     if (!late) __builtin_amdgcn_s_barrier();
   } else {
   // ---- prologue: tiles 0..S-2 in flight, retire tile 0 ----
 #pragma unroll
   for (int s = 0; s < S - 1; ++s)
-    if (s < nk) issue(kt0 + s, s);
+    if (s < nk) issue(kt0 + s, s, std::false_type{});
   wait_tiles<Cfg>(min(nk, S - 1) - 1, n_extra);
   __builtin_amdgcn_s_barrier();
 
@@ -352,11 +371,11 @@ __device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const i
       else wait_tiles<Cfg>(0, n_extra);
       __builtin_amdgcn_s_barrier();
     }
-    if (it + S - 1 < nk && !no_dma) issue(kt0 + it + S - 1, wrs);
+    if (it + S - 1 < nk && !no_dma) issue(kt0 + it + S - 1, wrs, std::false_type{});
     wrs = wrs + 1 == S ? 0 : wrs + 1;
     if (it + 1 < nk) load_into(na, nb, nrd);
     nrd = nrd + 1 == S ? 0 : nrd + 1;
-    mfmas(ca, cb);
+    mfmas(ca, cb, std::true_type{});
   };
   if (nk > 0) load_into(fa0, fb0, 0);
   for (int it = 0; it < nk; it += 2) {
@@ -365,7 +384,7 @@ __device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const i
   }
   }
   __builtin_amdgcn_s_barrier();  // all waves done with the ring before the epilogue reuses LDS
-  if (p.ablate & 8) {  // diagnostics: no epilogue (keep the accumulators alive)
+  if (abl & 8) {  // diagnostics: no epilogue (keep the accumulators alive)
 #pragma unroll
     for (int i = 0; i < Cfg::MI; ++i)
 #pragma unroll
@@ -379,7 +398,7 @@ __device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const i
     // agent scope — no L2-wide writeback or invalidate, which would also evict every other
     // workgroup's A/W panels from the shared L2.
     const auto rsk = make_rsrc(p.sk_ws, (uint32_t)((size_t)p.sk_grid * BM * BN * sizeof(float)));
-    if (sk_mode != 0 && (p.ablate & 4)) {  // diagnostics: segmenting cost only (wrong results)
+    if (sk_mode != 0 && (abl & 4)) {  // diagnostics: segmenting cost only (wrong results)
       if (sk_mode == 1) return;
     } else if (sk_mode == 1) {
       const int base = sk_slot * (BM * BN * 4);

@@ -26,6 +26,8 @@
 #include "gemm_common.h"
 #include "gemm_epilogue.h"
 
+#include <type_traits>
+
 namespace vst {
 
 struct P8Cfg {  // the epilogue's view of the tile (same wave tiling as RingCfg<256, 256, 2, 4, S>)
@@ -130,7 +132,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     if ((abl & 1) && kt > 1) return;
     char* dst = smem + (kt & 1) * BUF + s * SLOT + wid * 1024;
     const int k0 = kt * 64;
-    const bool live = kt < kend;
+    const bool live = kt < kend && !((abl & 32) && kt > 1);
     if (s < 2) {
       const bool second = k0 >= p.K1;
       const uint32_t kb = (uint32_t)(second ? k0 - p.K1 : k0) * 2u;
@@ -147,6 +149,23 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
         const bool kin = live && (!ktail || k0 + c8[s][pc] < p.K);
         p8_dma16(rw, dst + pc * 8192, kin ? (int)(base1[s][pc] + kb) : kOOB);
       }
+    }
+  };
+
+  // slot s of a k-tile that is live and fully inside K (every k-tile but the last two of a segment): no checks
+  auto dma_fast = [&](int s, int kt) {
+    if ((abl & 1) && kt > 1) return;
+    char* dst = smem + (kt & 1) * BUF + s * SLOT + wid * 1024;
+    const int k0 = kt * 64;
+    if (s < 2) {
+      const bool second = k0 >= p.K1;
+      const uint32_t kb = (uint32_t)(second ? k0 - p.K1 : k0) * 2u;
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc)
+        p8_dma16(second ? ra2 : ra1, dst + pc * 8192, (int)((second ? base2[s][pc] : base1[s][pc]) + kb));
+    } else {
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc) p8_dma16(rw, dst + pc * 8192, (int)(base1[s][pc] + (uint32_t)k0 * 2u));
     }
   };
 
@@ -175,11 +194,9 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   };
 #define VST_P8_QUAD(MQ, NQ, FB)                                                                        \
   if (!(abl & 2)) {                                                                                  \
-    __builtin_amdgcn_s_setprio(1);                                                                   \
     _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j)      \
         _Pragma("unroll") for (int h = 0; h < 2; ++h) acc[(MQ) * 4 + i][(NQ) * 2 + j] =              \
         __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j][h], fa[i][h], acc[(MQ) * 4 + i][(NQ) * 2 + j], 0, 0, 0); \
-    __builtin_amdgcn_s_setprio(0);                                                                   \
   }
 
   // k-tiles [kb, ke) of the current tile into acc (zeroed here); ends with the LDS drained and free for reuse
@@ -195,14 +212,22 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     p8_barrier();
     VST_P8_STAMP(1)
     if (late) p8_barrier();
+    // static priority for the second-dispatched half (the arbitration loser), no per-cluster flips: measured
+    // 4-7 % faster than s_setprio 1/0 around every MFMA cluster (tools/p8_variants.sh, profiles/r2_p8_variants.txt)
+    if (late) __builtin_amdgcn_s_setprio(1);
 
-    for (int t = kb; t < ke; ++t) {
+    // FAST: every DMA of the iteration targets a live k-tile fully inside K (t + 2 < ke - 1, or < ke without a K tail)
+    auto ktile = [&](int t, auto fast_tag) {
+      constexpr bool FAST = decltype(fast_tag)::value;
+      auto dma = [&](int s_, int kt) {
+        if constexpr (FAST) dma_fast(s_, kt); else dma_slot(s_, kt, ke);
+      };
       const int buf = t & 1;
       // phase 0: Q(0,0)
       read_a(buf, 0);
       read_b(buf, 0, fb0);
       if (!(abl & 4)) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Bnq1(t) landed
-      dma_slot(1, t + 1, ke);
+      dma(1, t + 1);
       p8_barrier();
       VST_P8_QUAD(0, 0, fb0)
       p8_barrier();
@@ -214,18 +239,22 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       p8_barrier();
       // phase 2: Q(1,1)
       read_a(buf, 1);
-      dma_slot(0, t + 2, ke);
-      dma_slot(2, t + 2, ke);
+      dma(0, t + 2);
+      dma(2, t + 2);
       p8_barrier();
       VST_P8_QUAD(1, 1, fb1)
       p8_barrier();
       // phase 3: Q(1,0)
       if (!(abl & 4)) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Amq0(t+1), Bnq0(t+1) landed
-      dma_slot(3, t + 2, ke);
+      dma(3, t + 2);
       p8_barrier();
       VST_P8_QUAD(1, 0, fb0)
       p8_barrier();
-    }
+    };
+    int t = kb;
+    const int ke_fast = ke - 2 - (ktail ? 1 : 0);
+    for (; t < ke_fast; ++t) ktile(t, std::true_type{});
+    for (; t < ke; ++t) ktile(t, std::false_type{});
     if (!late) p8_barrier();
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the trailing zero DMAs land before LDS reuse
     p8_barrier();
