@@ -11,6 +11,8 @@ from video_style_transfer_amd import kernels as K  # noqa: E402
 
 BF = torch.bfloat16
 SHAPES = [  # name, M, N, K1, K2, geglu, residual, bias
+    ("sp1280_qkv_lora", 8192, 3840, 1280, 64, False, False, True),
+    ("sp640_qkv_lora", 32768, 1920, 640, 64, False, False, True),
     ("tr1280_out_lora", 4096, 1280, 1280, 32, False, True, True),
     ("tr1280_ff2", 4096, 1280, 5120, 0, False, True, True),
     ("tr1280_dx", 4096, 1280, 1280, 0, False, False, False),
@@ -25,7 +27,7 @@ SHAPES = [  # name, M, N, K1, K2, geglu, residual, bias
     ("sp640_ff2", 32768, 640, 2560, 0, False, True, True),
     ("mm320_ff2", 131072, 320, 1280, 0, False, True, True),
 ]
-TILES = [(0, 0), (8, 1), (3, 1), (3, 0), (1, 1), (1, 0), (4, 1), (4, 0), (6, 1), (7, 1)]  # (tile, splits), 0 = auto
+TILES = [(0, 0), (8, 1), (3, 1), (6, 1), (7, 1)]  # (tile, splits), 0 = auto
 
 
 def run(x, x2, w, b, r, geglu, tile):

@@ -489,6 +489,20 @@ constexpr int kCUs = 256;
 // tile / split choice.  tile: 0 auto, 1 = 128x128, 2 = 128x64.  splits: 0 auto, >=1 forced.
 // tile codes: 1 = 128x128, 2 = 128x64 (gemm_kernel, 4 waves, up to 2 WG/CU);
 //             3 = 256x256, 4 = 256x128 (gemm_big_kernel, 8 waves, LDS-DMA staging, 1 WG/CU)
+
+// 256x160 ring tiles for Cout = 320 / 640 convs on full grids: Cout splits into 160-column tiles without the
+// 256-wide tiles' padding (Cout = 320: 37.5 % of the MFMA work wasted, 640: 17 %).  Measured in the denoise step
+// (tools/ab_bench.sh, profiles/r2_ab_t160.txt): convs 13.1 -> 12.4 ms per step.  The same tiles for N = 640 / 1280
+// projections win in isolation (tools/tile_ab.py: 32768x640x672 50.1 -> 43.8 us) but lose in the step
+// (74.0 -> 74.7 ms: operands arrive cold), so projections stay on the 8-phase kernel; Cout = 1280 convs gain
+// nothing; GEGLU needs 64-column [h | g] blocks.
+static bool t160_auto(int M, int N, bool geglu, bool conv) {
+  if (geglu || N % 160) return false;
+  const bool n_ok = conv && (N == 320 || N == 640);
+  const int mb = (M + 255) / 256;
+  return n_ok && mb * ((N + 255) / 256) >= kCUs / 2;
+}
+
 static void choose(int M, int N, int K, int geglu, int conv, size_t ws_bytes, int& tile, int& splits) {
   const int mt = (M + BM - 1) / BM;
   const int t128 = mt * ((N + 127) / 128);
@@ -506,6 +520,7 @@ static void choose(int M, int N, int K, int geglu, int conv, size_t ws_bytes, in
   // 128x128 tile's 4x larger grid wins (tools/tile_ab.py: 4096x1280x1312 44.6 -> 30.7 us, x5120 112 -> 82 us).
   if (tile == 0) {
     if (conv && N <= 64) tile = 2;
+    else if (t160_auto(M, N, geglu, conv)) tile = 6;
     else if (t256 >= kCUs / 2) tile = 3;
     else tile = 1;
   }
@@ -544,11 +559,12 @@ static int gemm_p8_env() {
   return v;
 }
 
-// Automatic choice of the 8-phase kernel (tile 0).  Measured in the denoise step (tools/p8_bench.sh, VST_BENCH_SHAPES,
-// one MI355X): it beats the ring on every projection / GEGLU shape with K < 2048 -- the 16x16-level out-projection
-// 8192x1280x1312 9.53 -> 8.55 ms per step, GEGLU 8192x10240x1280 14.29 -> 13.93, the K = 320 shapes of the 64x64
-// level 3-7 % -- and loses 2-6 % at K >= 2048 (ff.net.2), where the ring's 5-stage LDS-DMA lookahead pays.
-// VST_GEMM_P8 = 0 off, 1 every full-grid shape, unset = that rule (plus any K when stream-K applies, below).
+// Automatic choice of the 8-phase kernel (tile 0).  Measured in the denoise step (tools/ab_bench.sh, VST_BENCH_SHAPES,
+// one MI355X): it beats the ring on every projection / GEGLU shape -- first at K < 2048 (the 16x16-level
+// out-projection 8192x1280x1312 9.53 -> 8.55 ms per step, GEGLU 8192x10240x1280 14.29 -> 13.93, the K = 320 shapes of
+// the 64x64 level 3-7 %), and since its loop lost the per-piece K checks also at K >= 2048 (ff.net.2: ring 10.6 ->
+// 9.1 ms per step, profiles/r2_ab_p8_all_k.txt).
+// VST_GEMM_P8 = 0 off, unset / 1 every shape with at least half a wave of 256x256 tiles.
 static int device_cus();
 static bool p8_sk_on();
 static bool p8_sk_shape(int M, int N, int K) {
@@ -561,7 +577,7 @@ static bool p8_auto(int M, int N, int K, bool geglu) {
   const int e = gemm_p8_env();
   if (e == 0) return false;
   const int t256 = ((M + 255) / 256) * ((N + 255) / 256);
-  return t256 >= kCUs / 2 && K >= 128 && (e == 1 || K < 2048 || p8_sk_shape(M, N, K));
+  return t256 >= kCUs / 2 && K >= 128;
 }
 
 // tile code 8: AMODE 0, no split-K, a 64-aligned A source split, 256x256 tiles

@@ -105,16 +105,18 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   constexpr int abl = 0;
 #endif
 
-  // ---- per-lane DMA descriptors: slot s in {Amq0, Amq1, Bnq0, Bnq1}, piece pc in {0, 1} = slot rows
-  //      8*(wid + 8*pc) + (lane >> 3); this lane moves chunk c = (lane & 7) ^ ((row >> 1) & 7) of that row.
-  uint32_t base1[4][2], base2[2][2];
-  int c8[4][2];
+  // ---- per-lane DMA descriptors: slot s in {Amq0, Amq1, Bnq0, Bnq1}; 1-KiB piece q = PB + PS*pc of a slot holds slot
+  //      rows 8q .. 8q+7 (row 8q + (lane >> 3)); this lane moves chunk c = (lane & 7) ^ ((row >> 1) & 7) of that row.
+  constexpr int NPC = 2, PS = 8;
+  const int PB = wid;
+  uint32_t base1[4][NPC], base2[2][NPC];
+  int c8[4][NPC];
   auto setup_tile = [&](int m0, int n0) {
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
-      for (int pc = 0; pc < 2; ++pc) {
-        const int r = 8 * (wid + 8 * pc) + (lane >> 3);
+      for (int pc = 0; pc < NPC; ++pc) {
+        const int r = 8 * (PB + PS * pc) + (lane >> 3);
         const int c = (lane & 7) ^ ((r >> 1) & 7);
         c8[s][pc] = c * 8;
         if (s < 2) {
@@ -130,24 +132,24 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   // slot s of k-tile kt into buffer (kt & 1); kt >= kend: out-of-range offsets (zeros), keeps vmcnt counts uniform
   auto dma_slot = [&](int s, int kt, int kend) {
     if ((abl & 1) && kt > 1) return;
-    char* dst = smem + (kt & 1) * BUF + s * SLOT + wid * 1024;
+    char* dst = smem + (kt & 1) * BUF + s * SLOT + PB * 1024;
     const int k0 = kt * 64;
     const bool live = kt < kend && !((abl & 32) && kt > 1);
     if (s < 2) {
       const bool second = k0 >= p.K1;
       const uint32_t kb = (uint32_t)(second ? k0 - p.K1 : k0) * 2u;
 #pragma unroll
-      for (int pc = 0; pc < 2; ++pc) {
+      for (int pc = 0; pc < NPC; ++pc) {
         const bool kin = live && (!ktail || k0 + c8[s][pc] < p.K);
         const int off = kin ? (int)((second ? base2[s][pc] : base1[s][pc]) + kb) : kOOB;
-        p8_dma16(second ? ra2 : ra1, dst + pc * 8192, off);
+        p8_dma16(second ? ra2 : ra1, dst + pc * PS * 1024, off);
       }
     } else {
       const uint32_t kb = (uint32_t)k0 * 2u;
 #pragma unroll
-      for (int pc = 0; pc < 2; ++pc) {
+      for (int pc = 0; pc < NPC; ++pc) {
         const bool kin = live && (!ktail || k0 + c8[s][pc] < p.K);
-        p8_dma16(rw, dst + pc * 8192, kin ? (int)(base1[s][pc] + kb) : kOOB);
+        p8_dma16(rw, dst + pc * PS * 1024, kin ? (int)(base1[s][pc] + kb) : kOOB);
       }
     }
   };
@@ -155,17 +157,17 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   // slot s of a k-tile that is live and fully inside K (every k-tile but the last two of a segment): no checks
   auto dma_fast = [&](int s, int kt) {
     if ((abl & 1) && kt > 1) return;
-    char* dst = smem + (kt & 1) * BUF + s * SLOT + wid * 1024;
+    char* dst = smem + (kt & 1) * BUF + s * SLOT + PB * 1024;
     const int k0 = kt * 64;
     if (s < 2) {
       const bool second = k0 >= p.K1;
       const uint32_t kb = (uint32_t)(second ? k0 - p.K1 : k0) * 2u;
 #pragma unroll
-      for (int pc = 0; pc < 2; ++pc)
-        p8_dma16(second ? ra2 : ra1, dst + pc * 8192, (int)((second ? base2[s][pc] : base1[s][pc]) + kb));
+      for (int pc = 0; pc < NPC; ++pc)
+        p8_dma16(second ? ra2 : ra1, dst + pc * PS * 1024, (int)((second ? base2[s][pc] : base1[s][pc]) + kb));
     } else {
 #pragma unroll
-      for (int pc = 0; pc < 2; ++pc) p8_dma16(rw, dst + pc * 8192, (int)(base1[s][pc] + (uint32_t)k0 * 2u));
+      for (int pc = 0; pc < NPC; ++pc) p8_dma16(rw, dst + pc * PS * 1024, (int)(base1[s][pc] + (uint32_t)k0 * 2u));
     }
   };
 
