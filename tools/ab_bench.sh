@@ -7,7 +7,9 @@ mkdir -p gpurun_out
 for tag in "$@"; do
   base=$(echo $tag | sed 's/[0-9]*$//')  # trailing digits: repeats of the same build
   unset VST_GEMM_P8
-  if [ "$base" = newall ]; then export VST_GEMM_P8=1; base=new; fi  # the 8-phase kernel for every K too
+  unset VST_LN_GENERIC
+  if [ "$base" = lngen ]; then export VST_LN_GENERIC=1; base=new; fi  # the generic LayerNorm kernel only
+  if [ "$base" = newall ]; then export VST_GEMM_P8=1; base=new; fi  # the 8-phase kernel for every shape
   if [ "$base" = new ]; then unset VST_LIB_AB; else export VST_LIB_AB=abx/libvst_$base.so; fi
   VST_BENCH_SHAPES=1 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-peaks \
     > gpurun_out/ab_$tag.json 2> gpurun_out/ab_$tag.err || { tail -20 gpurun_out/ab_$tag.err; exit 1; }

@@ -447,6 +447,75 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const bf16_t* __restrict
   }
 }
 
+// LayerNorm for C = 40 * LPR (320 / 640 / 1280): LPR lanes per row, each holding CPL = 5 interleaved 16-B chunks
+// (lane l of a row reads chunks l, l + LPR, ...: every load instruction covers whole 128-B+ row segments), so all 64
+// lanes work for every C (the generic kernel above idles 37 % of its lanes at C = 320) and a wave normalises
+// 64 / LPR rows per pass; RIT passes' loads are all issued before the first reduction.  Row statistics are two-pass
+// (mean, then squared deviations), reduced over the row's LPR lanes by xor shuffles.
+template <int LPR, int RIT>
+__global__ __launch_bounds__(256) void layernorm_g_kernel(const bf16_t* __restrict__ x, int ldx, int C, int rows,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float eps,
+                                                          const float* __restrict__ pe, int pe_div, int pe_mod,
+                                                          bf16_t* __restrict__ y, int ldy) {
+  constexpr int CPL = 5, RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, l = lane % LPR, rsub = lane / LPR;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW * RIT;
+  if (row0 >= rows) return;
+  float v[RIT][CPL][8];
+#pragma unroll
+  for (int it = 0; it < RIT; ++it) {
+    const int row = row0 + it * RPW + rsub;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      u32x4 raw = u32x4{0u, 0u, 0u, 0u};
+      if (row < rows) raw = *reinterpret_cast<const u32x4*>(x + (size_t)row * ldx + (l + LPR * i) * 8);
+      unpack8(raw, v[it][i]);
+    }
+  }
+  const float invc = 1.0f / (float)C;
+#pragma unroll
+  for (int it = 0; it < RIT; ++it) {
+    const int row = row0 + it * RPW + rsub;
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sum += v[it][i][e];
+#pragma unroll
+    for (int o = LPR / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    const float mean = sum * invc;
+    float sq = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { const float d = v[it][i][e] - mean; sq += d * d; }
+#pragma unroll
+    for (int o = LPR / 2; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
+    const float rstd = rsqrtf(sq * invc + eps);
+    if (row >= rows) continue;
+    const float* pr = pe ? pe + (size_t)((row / pe_div) % pe_mod) * C : nullptr;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const int c0 = (l + LPR * i) * 8;
+      const f32x4 g0 = *reinterpret_cast<const f32x4*>(gamma + c0), g1 = *reinterpret_cast<const f32x4*>(gamma + c0 + 4);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(beta + c0), b1 = *reinterpret_cast<const f32x4*>(beta + c0 + 4);
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[e] = (v[it][i][e] - mean) * (rstd * g0[e]) + b0[e];
+        o[e + 4] = (v[it][i][e + 4] - mean) * (rstd * g1[e]) + b1[e];
+      }
+      if (pr) {
+        const f32x4 p0 = *reinterpret_cast<const f32x4*>(pr + c0), p1 = *reinterpret_cast<const f32x4*>(pr + c0 + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { o[e] += p0[e]; o[e + 4] += p1[e]; }
+      }
+      *reinterpret_cast<u32x4*>(y + (size_t)row * ldy + c0) = pack8(o);
+    }
+  }
+}
+
 // LayerNorm fused with the UnZipLoRA down-projection of the projections that consume its output
 // (BasicTransformerBlock norm1 -> attn1 q/k/v, norm2 -> attn2 q): y = LN(x) (bf16, as the reference's
 // LayerNorm output) and u = y . Acat^T (Acat: [R, C] bf16, R <= 64 a multiple of 16), reading x once.
@@ -817,6 +886,24 @@ extern "C" int vst_layernorm(const void* x, int ldx, int C, int rows, const floa
   hipStream_t s = (hipStream_t)stream;
   const int CH = C / 8;
   const dim3 blk(256);
+#define VST_LNG(LPR, RIT)                                                                                      \
+  hipLaunchKernelGGL((layernorm_g_kernel<LPR, RIT>), dim3((rows + 4 * (64 / LPR) * RIT - 1) / (4 * (64 / LPR) * RIT)), \
+                     blk, 0, s, (const bf16_t*)x, ldx, C, rows, gamma, beta, eps, pe, pe_div, pe_mod, (bf16_t*)y, ldy)
+  static const bool generic_only = getenv("VST_LN_GENERIC") != nullptr;  // A/B switch (tools/ab_bench.sh)
+  const bool g16 = !generic_only && ((uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)pe) % 16 == 0;
+  if (g16 && C == 320) {
+    VST_LNG(8, 2);
+    return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+  }
+  if (g16 && C == 640) {
+    VST_LNG(16, 2);
+    return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+  }
+  if (g16 && C == 1280) {
+    VST_LNG(32, 2);
+    return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+  }
+#undef VST_LNG
 #define VST_LN(MC, R)                                                                                          \
   hipLaunchKernelGGL((layernorm_kernel<MC, R>), dim3((rows + 4 * R - 1) / (4 * R)), blk, 0, s, (const bf16_t*)x, ldx, \
                      C, rows, gamma, beta, eps, pe, pe_div, pe_mod, (bf16_t*)y, ldy)
