@@ -29,6 +29,11 @@ cat gpurun_out/bench_$TAG.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- \
   python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-peaks > gpurun_out/bench_prof_$TAG.json 2> gpurun_out/prof_$TAG.err \
   || { echo "rocprof failed"; tail -20 gpurun_out/prof_$TAG.err; exit 1; }
+if [ -n "$TRAIN" ]; then
+  timeout -k 10 400 python -u bench.py --train --steps 5 --warmup 2 > gpurun_out/bench_train_$TAG.json 2> gpurun_out/bench_train_$TAG.err \
+    || { echo "train bench failed"; tail -20 gpurun_out/bench_train_$TAG.err; exit 1; }
+  cat gpurun_out/bench_train_$TAG.json
+fi
 # keep only the stats summary (the raw traces overflow gpurun_out's copy-back limit)
 STATS=$(find gpurun_out/prof_$TAG -name '*kernel_stats.csv' | head -1)
 if [ -n "$STATS" ]; then python tools/prof_summary.py "$STATS" > gpurun_out/kernel_stats_$TAG.csv; fi
