@@ -90,21 +90,24 @@ def src_hash():
 
 
 def pmc_traffic(symbol):
-    """HBM bytes per launch of `symbol` from the newest profiles/pmc_traffic_*.json (tools/pmc_traffic.py:
-    rocprofv3 FETCH_SIZE / WRITE_SIZE passes with the gfx950 corrections), only if it was measured on
-    this exact libvst_hip.so (same md5, or same source hash).  (bytes, source) or (None, reason)."""
+    """HBM bytes per launch of `symbol` from the profiles/pmc_traffic_*.json (tools/pmc_traffic.py: rocprofv3
+    FETCH_SIZE / WRITE_SIZE passes with the gfx950 corrections) that was measured on this exact libvst_hip.so
+    (same md5, or same source hash); the newest such file wins.  (bytes, source) or (None, reason)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic_*.json")), key=os.path.getmtime)
     if not files:
         return None, "no PMC profile"
-    with open(files[-1]) as f:
-        d = json.load(f)
-    if d.get("lib_md5") != _lib_md5() and d.get("src_hash") != src_hash():
-        return None, f"{os.path.basename(files[-1])} was measured on another build of libvst_hip.so"
-    k = d.get("kernels", {}).get(symbol)
-    if k is None:
-        return None, f"{symbol} not in {os.path.basename(files[-1])}"
-    return k["traffic_bytes"], os.path.basename(files[-1])
+    md5, sh = _lib_md5(), src_hash()
+    for fn in reversed(files):
+        with open(fn) as f:
+            d = json.load(f)
+        if d.get("lib_md5") != md5 and d.get("src_hash") != sh:
+            continue
+        k = d.get("kernels", {}).get(symbol)
+        if k is None:
+            return None, f"{symbol} not in {os.path.basename(fn)}"
+        return k["traffic_bytes"], os.path.basename(fn)
+    return None, "no PMC profile of this build of libvst_hip.so"
 
 
 def roofline(den):

@@ -325,8 +325,11 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
 // bytes read per x byte are N/32 (the L2 traffic that bounded the 16-row version).  The 8 partial
 // accumulators are summed through LDS (64 KiB at N = 64).  ceil(M/32) workgroups (256 at M = 8192), 2 per CU.
 template <int NJ>
+#ifndef VST_SKINNY_MI
+#define VST_SKINNY_MI 2
+#endif
 __global__ __launch_bounds__(512, 2) void gemm_skinny_kernel(GemmArgs p) {
-  constexpr int MI = 2, NW = 8;
+  constexpr int MI = VST_SKINNY_MI, NW = 8;
   constexpr int SK = NJ <= 2 ? 6 : 3;  // k32-steps per wave per load group (all in flight at once)
   __shared__ f32x4 red[NW][MI][NJ][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -407,7 +410,7 @@ __global__ __launch_bounds__(512, 2) void gemm_skinny_kernel(GemmArgs p) {
 }
 
 static int launch_skinny(const GemmArgs& a, hipStream_t s) {
-  const dim3 grid((a.M + 31) / 32);
+  const dim3 grid((a.M + 16 * VST_SKINNY_MI - 1) / (16 * VST_SKINNY_MI));
   switch ((a.N + 15) / 16) {
     case 1: hipLaunchKernelGGL(gemm_skinny_kernel<1>, grid, dim3(512), 0, s, a); break;
     case 2: hipLaunchKernelGGL(gemm_skinny_kernel<2>, grid, dim3(512), 0, s, a); break;

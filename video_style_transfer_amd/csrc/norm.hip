@@ -531,7 +531,10 @@ __global__ __launch_bounds__(512, 2) void layernorm_lora_kernel(const bf16_t* __
                                                                 const bf16_t* __restrict__ A, int R,
                                                                 bf16_t* __restrict__ y, int ldy, bf16_t* __restrict__ u,
                                                                 int ldu) {
-  constexpr int MI = 2, NW = 8;  // MAXT = ceil(C / 256) k32-chunks per wave (C <= 256 * MAXT)
+#ifndef VST_LNL_MI
+#define VST_LNL_MI 2
+#endif
+  constexpr int MI = VST_LNL_MI, NW = 8;  // MAXT = ceil(C / 256) k32-chunks per wave (C <= 256 * MAXT)
   __shared__ f32x4 red[NW][MI][NJ][64];
   __shared__ float st[NW][MI][16];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -923,7 +926,7 @@ extern "C" int vst_layernorm_lora(const void* x, int ldx, int C, int rows, const
                                   float eps, const void* A, int R, void* y, int ldy, void* u, int ldu, void* stream) {
   if (!x || !y || !u || !A || !gamma || !beta || rows <= 0 || C <= 0 || (C & 31) || C > 1280) return VST_ERR_ARG;
   if (R <= 0 || R > 64 || (R & 15) || (ldx & 7) || (ldy & 7) || (ldu & 3) || ldu < R) return VST_ERR_ARG;
-  const dim3 grid((rows + 31) / 32), blk(512);
+  const dim3 grid((rows + 16 * VST_LNL_MI - 1) / (16 * VST_LNL_MI)), blk(512);
   hipStream_t s = (hipStream_t)stream;
 #define VST_LNL(NJ, MT)                                                                                         \
   hipLaunchKernelGGL((layernorm_lora_kernel<NJ, MT>), grid, blk, 0, s, (const bf16_t*)x, ldx, C, rows, gamma, beta, \
