@@ -30,6 +30,10 @@ def run(path):
     out["add"] = K.add(r(1 << 20), r(1 << 20, a=1e-3))
     xt = r(2 * 16 * 1024, 3 * 640)
     out["temporal"] = K.temporal_attention(xt[:, :640], xt[:, 640:1280], xt[:, 1280:], 2, 16, 1024, 8, 80)
+    out["geglu_p8"] = K.linear(r(8192, 1280), r(10240, 1280, a=0.03), torch.randn(10240, device=dev, generator=g),
+                               geglu=True)
+    out["geglu_ring"] = K.linear(r(1024, 640), r(2560, 640, a=0.04), torch.randn(2560, device=dev, generator=g),
+                                 geglu=True)
     out["conv"] = K.conv3x3(r(8 * 32 * 32, 320), 8, 32, 32, r(640, 9 * 320, a=0.02), None)
     torch.cuda.synchronize()
     torch.save({k: (v[0] if isinstance(v, tuple) else v).cpu() for k, v in out.items()}, path)

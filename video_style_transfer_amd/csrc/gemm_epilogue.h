@@ -48,6 +48,46 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, char* smem, con
       for (int i = 0; i < Cfg::MI; ++i) acc[i][j] += b4;
     }
   }
+  if constexpr (EPI == 1 && Cfg::WN == 64 && Cfg::NJ == 4) {
+    // GEGLU from the registers: a wave's 64 weight rows are one [32 hidden | 32 gate] block, so lane-wise
+    // acc[i][j] (j = 0, 1) is the hidden half and acc[i][j + 2] the gate of the same output column.  Both are
+    // rounded to bf16 first (the reference's projection output), then h * gelu(g) is rounded once, as the LDS path
+    // below does; only the 32-column outputs are staged (half the tile) for full-row stores.
+    constexpr int OC = BN / 2;            // output columns of the tile
+    constexpr int OROW = OC * 2 + 16;     // staged bf16 output row
+    static_assert(BM * OROW <= Cfg::LDS, "GEGLU staging must fit in the ring's LDS");
+#pragma unroll
+    for (int i = 0; i < Cfg::MI; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float h = bf2f(f2bf(acc[i][j][e])), g = bf2f(f2bf(acc[i][j + 2][e]));
+          o[e] = h * gelu_erf(g);
+        }
+        u32x2 v;
+        v[0] = pack2bf(o[0], o[1]);
+        v[1] = pack2bf(o[2], o[3]);
+        *reinterpret_cast<u32x2*>(smem + (lrow0 + i * 16) * OROW + (wc * 32 + j * 16 + 4 * fq) * 2) = v;
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    constexpr int OCPR = OC / 8;
+    constexpr int OTOT = BM * OCPR;
+    constexpr int OITEMS = (OTOT + Cfg::THREADS - 1) / Cfg::THREADS;
+    const int nout = p.N / 2, c0 = n0 / 2;
+#pragma unroll
+    for (int k = 0; k < OITEMS; ++k) {
+      const int idx = tid + k * Cfg::THREADS;
+      const int row = idx / OCPR, cc = idx - row * OCPR;
+      const int m = m0 + row, n = c0 + cc * 8;
+      if (idx >= OTOT || m >= p.M || n >= nout) continue;
+      *reinterpret_cast<u32x4*>(p.C + (size_t)m * p.ldc + n) =
+          *reinterpret_cast<const u32x4*>(smem + row * OROW + cc * 16);
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < Cfg::MI; ++i)
 #pragma unroll
