@@ -13,16 +13,15 @@
 // ds_read_b128 fragment reads), filled by `buffer_load ... lds` (16 B per lane, lane-linear 1-KiB pieces, the
 // inverse permutation applied to the source address).
 //
-// 8 waves = 2 (M) x 4 (N), wave tile 128 x 64 = 8 x 4 accumulators (16x16).  A k-tile is four phases; phase p
-// multiplies one quadrant of the wave tile (16 MFMAs of 16x16x32):
-//   p0: read A(mq0) + B(nq0), Q(0,0)      p1: read B(nq1), Q(0,1)      p2: read A(mq1), Q(1,1)      p3: Q(1,0)
-// Each phase = {fragment reads, counted vmcnt wait, LDS-DMA issue} barrier {16 MFMAs} barrier; waves 4-7 run one
+// 8 waves = 2 (M) x 4 (N), wave tile 128 x 64 = 8 x 4 accumulators (16x16).  A k-tile is three barrier intervals
+// over the quadrants Q(mq, nq) of the wave tile (16 MFMAs of 16x16x32 per quadrant):
+//   I0: read A(mq0) + B(nq0), Q(0,0) + Q(0,1)      I1: read A(mq1), Q(1,1)      I2: read B(nq1) of t+1, Q(1,0)
+// Each interval = {fragment reads, counted vmcnt wait, LDS-DMA issue} barrier {MFMAs} barrier; waves 4-7 run one
 // barrier behind waves 0-3, so on every SIMD one wave's MFMAs overlap its partner's reads and DMA issue.
-// DMA of tile t+2 into the buffer of tile t: Amq0 + Bnq0 in p2 of tile t, Bnq1 in p3 of tile t, Amq1 in p0 of
-// tile t+1 -- each slot right after the barrier that retires its last reads (WAR), and each is waited for
-// (s_waitcnt vmcnt(8): exactly 4 younger slots of 2 DMAs each are in flight) one phase before its first read
-// (RAW).  Past the last k-tile the same DMAs are issued with out-of-range offsets (zeros), so the count is the same
-// at every phase; they are drained before the epilogue reuses the LDS.
+// A slot is refilled two intervals after the one that reads it (every wave's reads retired: WAR) and waited for
+// (counted s_waitcnt vmcnt, 2 DMAs per slot per wave) in the interval before its first read (RAW).  Past the last
+// k-tile the same DMAs are issued with out-of-range offsets (zeros), so the counts are the same in every interval;
+// they are drained before the epilogue reuses the LDS.
 #include "gemm_common.h"
 #include "gemm_epilogue.h"
 
@@ -207,48 +206,47 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // ---- prologue: k-tile kb complete, k-tile kb+1 except Amq1 (issued in phase 0 of tile kb) ----
-    dma_slot(0, kb, ke); dma_slot(2, kb, ke); dma_slot(3, kb, ke); dma_slot(1, kb, ke);
-    dma_slot(0, kb + 1, ke); dma_slot(2, kb + 1, ke); dma_slot(3, kb + 1, ke);
-    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // Amq0(kb), Bnq0(kb) landed
+    // Three barrier intervals per k-tile: I0 = {read Amq0, Bnq0} | Q(0,0) + Q(0,1) (32 MFMAs, fb1 = Bnq1(t) read in
+    // I2 of t-1); I1 = {read Amq1} | Q(1,1); I2 = {read Bnq1(t+1)} | Q(1,0).  (Four phases of 16 MFMAs, one per
+    // quadrant, measured 0.3 ms per step slower: 8 barriers per k-tile instead of 6, profiles/r2_ab_p8_3ph.txt.)  A slot read in interval I is refilled
+    // in interval I+2 (both halves' reads retired), and waited for in the interval before its first read:
+    //   I0(t): wait Amq1(t), issue Amq1(t+1);  I1(t): wait Bnq1(t+1), issue Bnq1(t+2);
+    //   I2(t): wait Amq0/Bnq0(t+1), issue Amq0/Bnq0(t+2).   (2 DMAs per slot per wave)
+    dma_slot(0, kb, ke); dma_slot(2, kb, ke); dma_slot(3, kb, ke);
+    dma_slot(1, kb, ke); dma_slot(3, kb + 1, ke); dma_slot(0, kb + 1, ke); dma_slot(2, kb + 1, ke);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Amq0, Bnq0, Bnq1 of kb landed
     p8_barrier();
     VST_P8_STAMP(1)
+    read_b(kb & 1, 1, fb1);
     if (late) p8_barrier();
-    // static priority for the second-dispatched half (the arbitration loser), no per-cluster flips: measured
-    // 4-7 % faster than s_setprio 1/0 around every MFMA cluster (tools/p8_variants.sh, profiles/r2_p8_variants.txt)
     if (late) __builtin_amdgcn_s_setprio(1);
-
-    // FAST: every DMA of the iteration targets a live k-tile fully inside K (t + 2 < ke - 1, or < ke without a K tail)
     auto ktile = [&](int t, auto fast_tag) {
       constexpr bool FAST = decltype(fast_tag)::value;
       auto dma = [&](int s_, int kt) {
         if constexpr (FAST) dma_fast(s_, kt); else dma_slot(s_, kt, ke);
       };
       const int buf = t & 1;
-      // phase 0: Q(0,0)
+      // I0
       read_a(buf, 0);
       read_b(buf, 0, fb0);
-      if (!(abl & 4)) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Bnq1(t) landed
+      if (!(abl & 4)) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // Amq1(t) landed
       dma(1, t + 1);
       p8_barrier();
       VST_P8_QUAD(0, 0, fb0)
-      p8_barrier();
-      // phase 1: Q(0,1)
-      read_b(buf, 1, fb1);
-      if (!(abl & 4)) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Amq1(t) landed
-      p8_barrier();
       VST_P8_QUAD(0, 1, fb1)
       p8_barrier();
-      // phase 2: Q(1,1)
+      // I1
       read_a(buf, 1);
-      dma(0, t + 2);
-      dma(2, t + 2);
+      if (!(abl & 4)) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // Bnq1(t+1) landed
+      dma(3, t + 2);
       p8_barrier();
       VST_P8_QUAD(1, 1, fb1)
       p8_barrier();
-      // phase 3: Q(1,0)
-      if (!(abl & 4)) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Amq0(t+1), Bnq0(t+1) landed
-      dma(3, t + 2);
+      // I2
+      read_b(buf ^ 1, 1, fb1);
+      if (!(abl & 4)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // Amq0(t+1), Bnq0(t+1) landed
+      dma(0, t + 2);
+      dma(2, t + 2);
       p8_barrier();
       VST_P8_QUAD(1, 0, fb0)
       p8_barrier();
