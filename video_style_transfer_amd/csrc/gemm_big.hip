@@ -364,23 +364,31 @@ __device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const i
   // the spare register set, and only then runs tile it's MFMA chain — the LDS read latency of
   // the next tile hides under the current MFMAs instead of opening a bubble after every barrier.
   int wrs = S - 1, nrd = 1 % S;  // next stage to fill / stage holding tile it+1
-  auto step = [&](int it, FragA& ca, FragB& cb, FragA& na, FragB& nb) {
-    if (it + 1 < nk) {
+  // FAST: tile it+S-1 exists and is not the last k-tile of K (no per-lane tail checks, no end-of-range tests)
+  auto step = [&](int it, FragA& ca, FragB& cb, FragA& na, FragB& nb, auto fast_tag) {
+    constexpr bool FAST = decltype(fast_tag)::value;
+    if (FAST || it + 1 < nk) {
       // tile it+1 must have landed: steady state leaves S-3 younger tiles in flight, the tail drains
-      if (it + S - 2 < nk && !no_dma) wait_tiles<Cfg>(S - 3, n_extra);
+      if (FAST || (it + S - 2 < nk && !no_dma)) wait_tiles<Cfg>(S - 3, n_extra);
       else wait_tiles<Cfg>(0, n_extra);
       __builtin_amdgcn_s_barrier();
     }
-    if (it + S - 1 < nk && !no_dma) issue(kt0 + it + S - 1, wrs, std::false_type{});
+    if (FAST || (it + S - 1 < nk && !no_dma)) issue(kt0 + it + S - 1, wrs, fast_tag);
     wrs = wrs + 1 == S ? 0 : wrs + 1;
-    if (it + 1 < nk) load_into(na, nb, nrd);
+    if (FAST || it + 1 < nk) load_into(na, nb, nrd);
     nrd = nrd + 1 == S ? 0 : nrd + 1;
     mfmas(ca, cb, std::true_type{});
   };
   if (nk > 0) load_into(fa0, fb0, 0);
-  for (int it = 0; it < nk; it += 2) {
-    step(it, fa0, fb0, fa1, fb1);
-    if (it + 1 < nk) step(it + 1, fa1, fb1, fa0, fb0);
+  const int it_fast = no_dma ? 0 : (ktail && kt1 == (p.K + RBK - 1) / RBK ? nk - S : nk - S + 1);
+  int it = 0;
+  for (; it + 1 < it_fast; it += 2) {
+    step(it, fa0, fb0, fa1, fb1, std::true_type{});
+    step(it + 1, fa1, fb1, fa0, fb0, std::true_type{});
+  }
+  for (; it < nk; it += 2) {
+    step(it, fa0, fb0, fa1, fb1, std::false_type{});
+    if (it + 1 < nk) step(it + 1, fa1, fb1, fa0, fb0, std::false_type{});
   }
   }
   __builtin_amdgcn_s_barrier();  // all waves done with the ring before the epilogue reuses LDS
