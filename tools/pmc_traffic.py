@@ -36,6 +36,7 @@ def bench_symbol(name: str) -> str:
     if "layernorm_lora_kernel" in name:
         return "layernorm_lora"
     for k, v in (("gemm_skinny", "gemm_skinny"), ("spatial_attn_kernel", "spatial_attn_kernel"),
+                 ("layernorm_g_kernel", "layernorm_kernel"),
                  ("temporal_attn_kernel", "temporal_attn_kernel"), ("layernorm_kernel", "layernorm_kernel"),
                  ("gn_", "gn_stats/gn_finalize/gn_apply"), ("gemm_kernel<2", "gemm_kernel<conv_in>")):
         if k in name:
