@@ -63,8 +63,8 @@ def test_gemm_skinny_lora_down(cuda, K, M, N, Kd, tile):
 
 @pytest.mark.parametrize("M,N,Kd,K2", [(4096, 1280, 1280, 32), (4000, 1200, 640, 0), (8192, 1280, 2048, 64)])
 def test_gemm_underfilled_grids(cuda, K, M, N, Kd, K2):
-    """Tile counts that leave CUs idle under 256x256 (160 tiles on 256 CUs: the policy keeps 256x256, stream-K
-    when VST_STREAMK=1; 80 tiles: 128x128), and the same GEMMs forced onto the 192x256 tile."""
+    """Tile counts that leave CUs idle under 256x256 (160 tiles on 256 CUs: the policy takes the 8-phase kernel's
+    256x192 tiles, 224 of them; 80 tiles: 128x128), and the same GEMMs forced onto the ring's 192x256 tile."""
     g = torch.Generator().manual_seed(M + N + Kd)
     x, x2 = rnd(M, Kd, gen=g), (rnd(M, K2, gen=g) if K2 else None)
     w = rnd(N, Kd + K2, scale=(Kd + K2) ** -0.5, gen=g)
@@ -73,7 +73,7 @@ def test_gemm_underfilled_grids(cuda, K, M, N, Kd, K2):
     r = rnd(M, N, gen=g)
     name = K.gemm_kernel_name(M, N, Kd + K2, 0)
     t256 = ((M + 255) // 256) * ((N + 255) // 256)
-    assert ("256x256" if t256 >= 128 else "128x128") in name, name
+    assert ("256x192" if t256 >= 128 else "128x128") in name, name
     for tile in (0, 7, 0):  # policy tile, forced 192x256, policy again (stream-K: flags reset by the first)
         K.GEMM_POLICY.update(tile=tile, splits=0)
         try:
@@ -97,13 +97,41 @@ def test_gemm_8phase_bitwise_equals_ring(cuda, K, M, N, K1, K2, geglu):
     b = torch.randn(N, generator=g).to(cuda)
     r = None if geglu else rnd(M, N, gen=g).to(cuda)
     outs = []
-    for tile in (3, 8):
+    for tile in ((3, 8) if geglu else (3, 8, 9)):  # tile 9: the 8-phase kernel at 256x192 (no GEGLU)
         K.GEMM_POLICY.update(tile=tile, splits=1)
         try:
             outs.append(K.linear(x, w, b, x2=x2, residual=r, geglu=geglu))
         finally:
             K.GEMM_POLICY.update(tile=0, splits=0)
-    assert torch.equal(outs[0], outs[1])
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o)
+
+
+@pytest.mark.parametrize("M,N,K1,K2,act", [(8192, 1280, 1280, 32, None), (32768, 640, 640, 32, None),
+                                           (131072, 320, 320, 0, None), (1000, 200, 192, 0, "gelu"),
+                                           (4096, 576, 1344, 0, None)])
+def test_gemm_8phase_256x192_vs_torch(cuda, K, M, N, K1, K2, act):
+    """The 256x192 tiles of the 8-phase kernel, chosen automatically for N = 320 / 640 / 1280 on full grids
+    (gemm.hip p8_bn192): against fp32 torch, with M / N tails (N = 200: a 192 + 8 split) and the GELU epilogue."""
+    g = torch.Generator().manual_seed(M + N)
+    x, x2 = rnd(M, K1, gen=g).to(cuda), (rnd(M, K2, gen=g).to(cuda) if K2 else None)
+    w = rnd(N, K1 + K2, scale=(K1 + K2) ** -0.5, gen=g).to(cuda)
+    b = torch.randn(N, generator=g).to(cuda)
+    r = None if act else rnd(M, N, gen=g).to(cuda)
+    K.GEMM_POLICY.update(tile=9, splits=1)
+    try:
+        out = K.linear(x, w, b, x2=x2, residual=r, act=act)
+    finally:
+        K.GEMM_POLICY.update(tile=0, splits=0)
+    xc = torch.cat([x, x2], 1) if K2 else x
+    ref = xc.float() @ w.float().t() + b
+    if act:
+        ref = torch.nn.functional.gelu(ref)
+    if r is not None:
+        ref = ref.to(torch.bfloat16).float() + r.float()
+    check(out, ref, name=f"gemm_p8<256x192> {M}x{N}x{K1 + K2}")
+    if not act and M >= 8192:
+        assert "256x192" in K.gemm_kernel_name(M, N, K1 + K2, 0), K.gemm_kernel_name(M, N, K1 + K2, 0)
 
 
 @pytest.mark.parametrize("M,N,K1,K2,geglu", [(8192, 1280, 1280, 32, False), (8192, 1280, 5120, 0, False),

@@ -550,7 +550,7 @@ static void choose(int M, int N, int K, int geglu, int conv, size_t ws_bytes, in
 }
 
 int launch_gemm_ring(const GemmArgs& a, int amode, int epi, int tile, int splits, hipStream_t s);
-int launch_gemm_p8(const GemmArgs& a, int epi, hipStream_t s);
+int launch_gemm_p8(const GemmArgs& a, int epi, int bn, hipStream_t s);
 
 // 8-phase 256x256x64 kernel (gemm_p8.hip) for plain / LoRA-augmented projections and GEGLU (see p8_auto).
 static int gemm_p8_env() {
@@ -581,6 +581,22 @@ static bool p8_auto(int M, int N, int K, bool geglu) {
   if (e == 0) return false;
   const int t256 = ((M + 255) / 256) * ((N + 255) / 256);
   return t256 >= kCUs / 2 && K >= 128;
+}
+
+// 256x192 tiles for the 8-phase kernel (tile code 9, and tile 0 wherever it wins the round count): N = 1280 gives
+// 7 column tiles (224 workgroups at M = 8192) instead of 5 (160 of 256 CUs), N = 640 two full rounds instead of
+// 1.5, N = 320 a 192 + 128 split instead of 256 + 64.  A 256x192 tile costs ~0.8 of a 256x256 one (its fill and
+// epilogue do not shrink with it), so it is taken when ceil(tiles192 / CUs) * 0.8 beats ceil(tiles256 / CUs).
+// VST_P8_BN=256 keeps every shape on 256x256 (A/B).
+static bool p8_bn192(int M, int N, bool geglu) {
+  static const int env = [] {
+    const char* e = getenv("VST_P8_BN");
+    return e ? atoi(e) : 0;
+  }();
+  if (geglu || env == 256 || p8_sk_on()) return false;
+  const int mb = (M + 255) / 256, cus = device_cus();
+  const int r256 = (mb * ((N + 255) / 256) + cus - 1) / cus, r192 = (mb * ((N + 191) / 192) + cus - 1) / cus;
+  return env == 192 || 0.8 * r192 < 0.97 * r256;
 }
 
 // tile code 8: AMODE 0, no split-K, a 64-aligned A source split, 256x256 tiles
@@ -699,7 +715,7 @@ static int run_gemm(GemmArgs& a, int amode, int geglu, int tile, int splits, hip
   if (tile == 8) {
     if (amode != 0 || splits > 1) return VST_ERR_ARG;
     a.splits = 1;
-    return launch_gemm_p8(a, geglu ? 1 : (a.act ? 3 : 0), s);
+    return launch_gemm_p8(a, geglu ? 1 : (a.act ? 3 : 0), a.p8_bn == 192 ? 192 : 256, s);
   }
   if (amode == 2) {  // scalar-gather conv (conv_in): register-staged kernel, no split
     a.splits = 1;
@@ -745,9 +761,13 @@ extern "C" const char* vst_gemm_kernel_name(int M, int N, int K, int kind, int t
                                        "gemm_ring<256x160,splitk>", "gemm_ring<192x256,splitk>"};
   if (kind == 3) return "gemm_kernel<conv_in>";
   if (kind == 0 && (tile == 5 || (tile == 0 && N <= 64 && M >= 1024))) return "gemm_skinny";  // no-epilogue calls
-  if (kind < 0 || kind > 3 || tile < 0 || tile > 8 || tile == 5 || splits < 0) return "";
+  if (kind < 0 || kind > 3 || tile < 0 || tile > 9 || tile == 5 || splits < 0) return "";
+  if (tile == 9) return kind == 0 ? "gemm_p8<256x192>" : "";
   const int splits_in = splits;
-  if (tile == 0 && kind <= 1 && p8_auto(M, N, K, kind == 1)) tile = 8;
+  if (tile == 0 && kind <= 1 && p8_auto(M, N, K, kind == 1)) {
+    if (splits_in == 0 && kind == 0 && p8_bn192(M, N, false)) return "gemm_p8<256x192>";
+    tile = 8;
+  }
   choose(M, N, K, kind == 1, kind == 2, ws_bytes > kFlagBytes ? ws_bytes - kFlagBytes : 0, tile, splits);
   if (tile == 8) {
     const bool sk = splits_in != 1 && p8_sk_shape(M, N, K) &&
@@ -778,8 +798,9 @@ extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int
   if (epilogue == 2 && (R || row_bias)) return VST_ERR_ARG;  // GELU: bias only
   if (R && (ldr & 7)) return VST_ERR_ARG;
   if (row_bias && row_bias_div <= 0) return VST_ERR_ARG;
-  if (tile < 0 || tile > 8 || splits < 0) return VST_ERR_ARG;
-  if (tile == 8 && !p8_applies(M, N, K1, A2 != nullptr)) return VST_ERR_ARG;
+  if (tile < 0 || tile > 9 || splits < 0) return VST_ERR_ARG;
+  if ((tile == 8 || tile == 9) && !p8_applies(M, N, K1, A2 != nullptr)) return VST_ERR_ARG;
+  if (tile == 9 && epilogue == 1) return VST_ERR_ARG;  // GEGLU needs the 256-wide tiles
   const bool skinny_ok = N <= 64 && !A2 && !bias && !row_bias && !R && epilogue == 0;
   if (tile == 5 && !skinny_ok) return VST_ERR_ARG;
   GemmArgs a{};
@@ -799,7 +820,12 @@ extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int
   if (tile == 5) return run_gemm(a, 0, 0, 5, 1, (hipStream_t)stream);
   const size_t slab_bytes = (workspace && ws_bytes > kFlagBytes) ? ws_bytes - kFlagBytes : 0;
   const int splits_in = splits;  // tile 8: splits 1 = plain tiling, 0 = stream-K where it applies
-  if (tile == 0 && splits == 0 && p8_auto(M, N, K, epilogue == 1) && p8_applies(M, N, K1, A2 != nullptr)) tile = 8;
+  if (tile == 0 && splits == 0 && p8_auto(M, N, K, epilogue == 1) && p8_applies(M, N, K1, A2 != nullptr))
+    tile = p8_bn192(M, N, epilogue == 1) ? 9 : 8;
+  if (tile == 9) {  // the 8-phase kernel at 256x192 (no stream-K)
+    a.p8_bn = 192;
+    return run_gemm(a, 0, 0, 8, 1, (hipStream_t)stream);
+  }
   choose(M, N, K, epilogue == 1, 0, slab_bytes, tile, splits);
   if (slab_bytes) apply_stream_k(a, tile, splits, epilogue == 1 ? 1 : 0, workspace, ws_bytes);
   if (tile == 8 && splits_in != 1) apply_p8_sk(a, workspace, ws_bytes);

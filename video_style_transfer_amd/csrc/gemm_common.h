@@ -21,6 +21,7 @@ struct GemmArgs {
   int act;     // EPI 0 only: 1 = GELU(erf) after the bias (TemporalTransformerBlock ffn, no residual / row bias)
   int persist;  // > 0: persistent launch over `persist` CUs (VST_GEMM_PERSIST; 0 = one workgroup per tile)
   int group_m;  // grouped tile order: row panels per group (0 = default 8; VST_GEMM_GROUP_M for tuning)
+  int p8_bn;   // 8-phase kernel tile width: 0 / 256 or 192 (gemm_p8.hip)
   int ablate;  // diagnostics only (VST_GEMM_ABLATE): bit0 skip loop DMA, bit1 skip MFMA
   // stream-K (ring GEMM, 256x256): k-steps per workgroup (0 = data-parallel), grid, partial slots
   // [sk_grid][BM*BN] fp32 and their flags (zero between launches; consumers reset them)

@@ -29,15 +29,26 @@
 
 namespace vst {
 
-struct P8Cfg {  // the epilogue's view of the tile (same wave tiling as RingCfg<256, 256, 2, 4, S>)
-  static constexpr int BM = 256, BN = 256, WAVES_M = 2, WAVES_N = 4, NWAVES = 8, THREADS = 512;
-  static constexpr int WM = 128, WN = 64, MI = 8, NJ = 4;
-  static constexpr int SLOT = 128 * 64 * 2;  // 16 KiB
-  static constexpr int BUF = 4 * SLOT;
+// BN = 256 (wave tile 128 x 64) or 192 (128 x 48: the N = 1280 / 640 / 320 grids in fewer-padded, fuller rounds).
+// Slot Bnq0 holds the first 32 columns of every wave column, Bnq1 the remaining WN - 32 (32 or 16).
+template <int BN_>
+struct P8Cfg {  // the epilogue's view of the tile (same wave tiling as RingCfg<256, BN, 2, 4, S>)
+  static constexpr int BM = 256, BN = BN_, WAVES_M = 2, WAVES_N = 4, NWAVES = 8, THREADS = 512;
+  static constexpr int WM = 128, WN = BN / 4, MI = 8, NJ = WN / 16;
+  static constexpr int RB1 = WN - 32;               // Bnq1 rows per wave column
+  static constexpr int NJ1 = RB1 / 16;              // Bnq1 fragments per wave
+  static constexpr int NPB1 = 4 * RB1 / 64;         // Bnq1 1-KiB pieces per wave (2 or 1)
+  static constexpr int SLOT = 128 * 64 * 2;         // 16 KiB: Amq0, Amq1, Bnq0
+  static constexpr int SLOT_B1 = 4 * RB1 * 128;     // Bnq1
+  static constexpr int BUF = 3 * SLOT + SLOT_B1;
   static constexpr int EPI_BYTES = BM * (BN * 2 + 16);
   static constexpr int LDS = 2 * BUF > EPI_BYTES ? 2 * BUF : EPI_BYTES;
+  static_assert(BN == 256 || BN == 192, "tile width");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
 };
-static_assert(P8Cfg::LDS <= 160 * 1024, "LDS budget");
+
+template <int N>
+__device__ __forceinline__ void p8_vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
 typedef __attribute__((address_space(3))) void p8_lds_void;
 
@@ -74,22 +85,25 @@ __device__ __forceinline__ void p8_barrier() {
 // their partial slot, then raise their flag (agent-scope release).  The owner adds the partials in workgroup order
 // (deterministic), clears the flags for the next launch, and runs the epilogue.  Only owners wait, and only on
 // higher-numbered workgroups that wait on nobody, and the grid is at most one workgroup per CU: no cycle.
-template <int EPI, bool SK>
+template <int EPI, bool SK, int BN>
 __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int SLOT = P8Cfg::SLOT, BUF = P8Cfg::BUF;
+  using Cfg = P8Cfg<BN>;
+  static_assert(!SK || BN == 256, "stream-K partial slots are 256 x 256");
+  static_assert(EPI != 1 || BN == 256, "GEGLU needs 64-column [hidden | gate] blocks");
+  constexpr int SLOT = Cfg::SLOT, BUF = Cfg::BUF, RB1 = Cfg::RB1, NJ1 = Cfg::NJ1, NPB1 = Cfg::NPB1;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid >> 2, wc = wid & 3;
   const int fr = lane & 15, fq = lane >> 4;
-  const int nbm = (p.M + 255) / 256, nbn = (p.N + 255) / 256;
+  const int nbm = (p.M + 255) / 256, nbn = (p.N + BN - 1) / BN;
   const int ntiles = nbm * nbn;
   auto tile_origin = [&](int t, int& m0, int& n0) {
     const int GROUP_M = 8, in_group = GROUP_M * nbn;
     const int gid = t / in_group, first_m = gid * GROUP_M;
     const int gsize = min(nbm - first_m, GROUP_M);
     m0 = (first_m + (t - gid * in_group) % gsize) * 256;
-    n0 = ((t - gid * in_group) / gsize) * 256;
+    n0 = ((t - gid * in_group) / gsize) * BN;
   };
   const auto ra1 = make_rsrc(p.A1, p.a1_bytes);
   const auto ra2 = make_rsrc(p.A2 ? p.A2 : p.A1, p.A2 ? p.a2_bytes : 0u);
@@ -123,8 +137,9 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
           base1[s][pc] = m < p.M ? (uint32_t)(m * p.lda1 + c * 8) * 2u : (uint32_t)kOOB;
           base2[s][pc] = m < p.M ? (uint32_t)(m * p.lda2 + c * 8) * 2u : (uint32_t)kOOB;
         } else {
-          const int n = n0 + (r >> 5) * 64 + (s - 2) * 32 + (r & 31);
-          base1[s][pc] = n < p.N ? (uint32_t)(n * p.ldw + c * 8) * 2u : (uint32_t)kOOB;
+          const int rb = s == 2 ? 32 : RB1;
+          const int n = n0 + (r / rb) * Cfg::WN + (s - 2) * 32 + (r % rb);
+          base1[s][pc] = (n < p.N && (s == 2 || pc < NPB1)) ? (uint32_t)(n * p.ldw + c * 8) * 2u : (uint32_t)kOOB;
         }
       }
   };
@@ -146,7 +161,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     } else {
       const uint32_t kb = (uint32_t)k0 * 2u;
 #pragma unroll
-      for (int pc = 0; pc < NPC; ++pc) {
+      for (int pc = 0; pc < (s == 3 ? NPB1 : NPC); ++pc) {
         const bool kin = live && (!ktail || k0 + c8[s][pc] < p.K);
         p8_dma16(rw, dst + pc * PS * 1024, kin ? (int)(base1[s][pc] + kb) : kOOB);
       }
@@ -166,11 +181,12 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
         p8_dma16(second ? ra2 : ra1, dst + pc * PS * 1024, (int)((second ? base2[s][pc] : base1[s][pc]) + kb));
     } else {
 #pragma unroll
-      for (int pc = 0; pc < NPC; ++pc) p8_dma16(rw, dst + pc * PS * 1024, (int)(base1[s][pc] + (uint32_t)k0 * 2u));
+      for (int pc = 0; pc < (s == 3 ? NPB1 : NPC); ++pc)
+        p8_dma16(rw, dst + pc * PS * 1024, (int)(base1[s][pc] + (uint32_t)k0 * 2u));
     }
   };
 
-  f32x4 acc[8][4];
+  f32x4 acc[8][Cfg::NJ];
   bf16x8 fa[4][2];         // A fragments of the current row quadrant (mq): 4 x 16 rows x 2 k-halves
   bf16x8 fb0[2][2], fb1[2][2];  // W fragments of column quadrants nq0 / nq1
 #ifdef VST_P8_TRACE
@@ -188,14 +204,15 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   auto read_b = [&](int buf, int nq, bf16x8 (&fb)[2][2]) {
     if (abl & 16) return;
     const char* S = smem + buf * BUF + (2 + nq) * SLOT;
+    const int rb = nq == 0 ? 32 : RB1;
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < (nq == 0 ? 2 : NJ1); ++j)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) fb[j][h] = *reinterpret_cast<const bf16x8*>(S + p8_off(wc * 32 + j * 16 + fr, h * 4 + fq));
+      for (int h = 0; h < 2; ++h) fb[j][h] = *reinterpret_cast<const bf16x8*>(S + p8_off(wc * rb + j * 16 + fr, h * 4 + fq));
   };
 #define VST_P8_QUAD(MQ, NQ, FB)                                                                        \
   if (!(abl & 2)) {                                                                                  \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j)      \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < ((NQ) == 0 ? 2 : NJ1); ++j) \
         _Pragma("unroll") for (int h = 0; h < 2; ++h) acc[(MQ) * 4 + i][(NQ) * 2 + j] =              \
         __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j][h], fa[i][h], acc[(MQ) * 4 + i][(NQ) * 2 + j], 0, 0, 0); \
   }
@@ -205,7 +222,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < Cfg::NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     // Three barrier intervals per k-tile: I0 = {read Amq0, Bnq0} | Q(0,0) + Q(0,1) (32 MFMAs, fb1 = Bnq1(t) read in
     // I2 of t-1); I1 = {read Amq1} | Q(1,1); I2 = {read Bnq1(t+1)} | Q(1,0).  (Four phases of 16 MFMAs, one per
     // quadrant, measured 0.3 ms per step slower: 8 barriers per k-tile instead of 6, profiles/r2_ab_p8_3ph.txt.)  A slot read in interval I is refilled
@@ -214,7 +231,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     //   I2(t): wait Amq0/Bnq0(t+1), issue Amq0/Bnq0(t+2).   (2 DMAs per slot per wave)
     dma_slot(0, kb, ke); dma_slot(2, kb, ke); dma_slot(3, kb, ke);
     dma_slot(1, kb, ke); dma_slot(3, kb + 1, ke); dma_slot(0, kb + 1, ke); dma_slot(2, kb + 1, ke);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Amq0, Bnq0, Bnq1 of kb landed
+    p8_vmwait<6 + NPB1>();  // Amq0, Bnq0, Bnq1 of kb landed
     p8_barrier();
     VST_P8_STAMP(1)
     read_b(kb & 1, 1, fb1);
@@ -229,7 +246,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       // I0
       read_a(buf, 0);
       read_b(buf, 0, fb0);
-      if (!(abl & 4)) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // Amq1(t) landed
+      if (!(abl & 4)) p8_vmwait<4 + NPB1>();  // Amq1(t) landed
       dma(1, t + 1);
       p8_barrier();
       VST_P8_QUAD(0, 0, fb0)
@@ -237,14 +254,14 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       p8_barrier();
       // I1
       read_a(buf, 1);
-      if (!(abl & 4)) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // Bnq1(t+1) landed
+      if (!(abl & 4)) p8_vmwait<6>();  // Bnq1(t+1) landed
       dma(3, t + 2);
       p8_barrier();
       VST_P8_QUAD(1, 1, fb1)
       p8_barrier();
       // I2
       read_b(buf ^ 1, 1, fb1);
-      if (!(abl & 4)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // Amq0(t+1), Bnq0(t+1) landed
+      if (!(abl & 4)) p8_vmwait<2 + NPB1>();  // Amq0(t+1), Bnq0(t+1) landed
       dma(0, t + 2);
       dma(2, t + 2);
       p8_barrier();
@@ -268,7 +285,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     setup_tile(m0, n0);
     run_segment(0, nk);
     VST_P8_STAMP(2)
-    tile_epilogue<P8Cfg, EPI>(p, smem, m0, n0, acc, wr, wc);
+    tile_epilogue<Cfg, EPI>(p, smem, m0, n0, acc, wr, wc);
 #ifdef VST_P8_TRACE
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -333,32 +350,41 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
         }
         if (tl == 0) __hip_atomic_store(p.sk_flags + c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      tile_epilogue<P8Cfg, EPI>(p, smem, m0, n0, acc, wr, wc, tl);
+      tile_epilogue<Cfg, EPI>(p, smem, m0, n0, acc, wr, wc, tl);
     }
   }
 }
 
-template <int EPI, bool SK>
+template <int EPI, bool SK, int BN>
 static int launch_p8_epi(const GemmArgs& a, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_p8_kernel<EPI, SK>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              P8Cfg::LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_p8_kernel<EPI, SK, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              P8Cfg<BN>::LDS);
     attr = true;
   }
-  const int nwg = SK ? a.sk_grid : ((a.M + 255) / 256) * ((a.N + 255) / 256);
-  hipLaunchKernelGGL((gemm_p8_kernel<EPI, SK>), dim3(nwg), dim3(512), P8Cfg::LDS, s, a);
+  const int nwg = SK ? a.sk_grid : ((a.M + 255) / 256) * ((a.N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_p8_kernel<EPI, SK, BN>), dim3(nwg), dim3(512), P8Cfg<BN>::LDS, s, a);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 
-// epi: 0 bias / row bias / residual, 1 GEGLU, 3 bias + GELU
-int launch_gemm_p8(const GemmArgs& a, int epi, hipStream_t s) {
+// epi: 0 bias / row bias / residual, 1 GEGLU, 3 bias + GELU; bn: 256 or 192 (not with GEGLU or stream-K)
+int launch_gemm_p8(const GemmArgs& a, int epi, int bn, hipStream_t s) {
   if (a.A2 && (a.K1 & 63)) return VST_ERR_ARG;  // a 64-deep k-tile must not straddle the two A sources
   const bool sk = a.sk_grid > 0 && a.sk_ws && a.sk_flags;
+  if (bn == 192) {
+    if (sk) return VST_ERR_ARG;
+    switch (epi) {
+      case 0: return launch_p8_epi<0, false, 192>(a, s);
+      case 3: return launch_p8_epi<3, false, 192>(a, s);
+      default: return VST_ERR_ARG;
+    }
+  }
+  if (bn != 256) return VST_ERR_ARG;
   switch (epi) {
-    case 0: return sk ? launch_p8_epi<0, true>(a, s) : launch_p8_epi<0, false>(a, s);
-    case 1: return sk ? launch_p8_epi<1, true>(a, s) : launch_p8_epi<1, false>(a, s);
-    case 3: return sk ? launch_p8_epi<3, true>(a, s) : launch_p8_epi<3, false>(a, s);
+    case 0: return sk ? launch_p8_epi<0, true, 256>(a, s) : launch_p8_epi<0, false, 256>(a, s);
+    case 1: return sk ? launch_p8_epi<1, true, 256>(a, s) : launch_p8_epi<1, false, 256>(a, s);
+    case 3: return sk ? launch_p8_epi<3, true, 256>(a, s) : launch_p8_epi<3, false, 256>(a, s);
     default: return VST_ERR_ARG;
   }
 }
