@@ -219,7 +219,21 @@ def test_configs0_sdxl_image_unet_f1(cuda):
     log("[bf16-parity] configs[0]: emulation, probe and fp32 oracle on the CPU ...")
     with torch.no_grad():
         ref_bf, floor = _floor(lambda: E.unet_forward(P, cfg.to_dict(), lat, t, enc, pooled, tids), out)
+        t0 = time.perf_counter()
         ref32 = O.unet_forward(P, cfg.to_dict(), lat, t, enc, pooled, tids)
+        cpu_s = time.perf_counter() - t0
+    cpu_model = next((ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name")),
+                     "unknown CPU")
+    # BASELINE configs[0] is the reference's PyTorch CPU-eager plumbing run: the fp32 oracle's eager forward of the
+    # same CFG pair, timed here on the box's host cores (one HIP forward of it is timed beside it)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    unet(lat.to(cuda), t.to(cuda), enc.to(cuda), added_cond_kwargs={"text_embeds": pooled.to(cuda),
+                                                                    "time_ids": tids.to(cuda)})
+    torch.cuda.synchronize()
+    gpu_s = time.perf_counter() - t0
+    log(f"[bf16-parity] configs[0] CPU eager fp32 forward (CFG pair): {cpu_s:.2f} s on {torch.get_num_threads()} "
+        f"threads of {cpu_model}; HIP eager forward {gpu_s * 1e3:.1f} ms")
     e2, em = _report("configs[0] SDXL image UNet F=1 32x32", out, ref_bf, ref32)
     log(f"[bf16-parity] configs[0] reassociation floor {floor:.2e}")
     assert e2 <= max(5e-3, 3 * floor) and em <= 5e-2
