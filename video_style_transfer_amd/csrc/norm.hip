@@ -55,7 +55,10 @@ __global__ __launch_bounds__(512) void gn_stats_kernel(const bf16_t* __restrict_
 #pragma unroll
   for (int e = 0; e < 8; ++e) { a[e] = 0.f; q[e] = 0.f; }
   // GN_UNROLL independent 16-B loads in flight per thread
-  constexpr int GN_UNROLL = 8;
+#ifndef VST_GN_STATS_U
+#define VST_GN_STATS_U 8
+#endif
+  constexpr int GN_UNROLL = VST_GN_STATS_U;
   for (int r = r_beg + rph; r < r_end; r += GN_UNROLL * rps) {
     u32x4 v[GN_UNROLL];
 #pragma unroll
@@ -300,7 +303,10 @@ __global__ __launch_bounds__(512) void gn_apply_kernel(const bf16_t* __restrict_
   const f32x4* sc = reinterpret_cast<const f32x4*>(scale + (size_t)s * C + c);
   const f32x4* sh = reinterpret_cast<const f32x4*>(shift + (size_t)s * C + c);
   const f32x4 a0 = sc[0], a1 = sc[1], b0 = sh[0], b1 = sh[1];
-  constexpr int U = 4;  // loads in flight per thread
+#ifndef VST_GN_APPLY_U
+#define VST_GN_APPLY_U 4
+#endif
+  constexpr int U = VST_GN_APPLY_U;  // loads in flight per thread
   for (int r = r_beg + rph; r < r_end; r += U * rps) {
     u32x4 v[U];
 #pragma unroll
