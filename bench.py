@@ -62,9 +62,12 @@ def parse():
                     "encode of the training frames (--train: the step then starts from synthetic latents)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--train", action="store_true",
-                    help="BASELINE configs[4]: one train_animatediff.py optimizer step per rank (fwd+bwd on a 16-frame "
-                         "clip, orth loss, clip_grad_norm_, AdamW; RCCL gradient all-reduce for N>1) instead of the "
-                         "denoise loop")
+                    help="BASELINE configs[4]: one train_animatediff.py optimizer step per rank (fwd+bwd on "
+                         "--grad-accum 16-frame clips, orth loss, clip_grad_norm_, AdamW, cosine lr; RCCL gradient "
+                         "all-reduce for N>1) instead of the denoise loop")
+    ap.add_argument("--grad-accum", type=int, default=4,
+                    help="--train: gradient_accumulation_steps (train_animatediff.py:395, default 4): clips per rank "
+                         "per optimizer step")
     return ap.parse_args()
 
 
@@ -286,14 +289,17 @@ def _cpu_model():
 def bench_train(args, world, rank, local, dev):
     """BASELINE configs[4] (train_animatediff.py:212-319): SDXL UNet + AnimateDiff-SDXL motion modules (synthetic
     weights), UnZipLoRA r=8 frozen on all spatial projections, temporal LoRA r=32 injected, freeze_spatial_layers,
-    one 16x512x512 clip (synthetic VAE latents) per rank per step: Euler add_noise, UNet fwd, MSE + orth loss
-    (lambda 1e-4), backward, gradient all-reduce (RCCL, N>1), clip_grad_norm_(0.5), AdamW(2e-5).  N=1: the whole
-    step is one captured HIP graph; N>1: eager steps with the bucketed all-reduce overlapping the backward."""
+    --grad-accum 16x512x512 clips (VAE-encoded synthetic frames) per rank per optimizer step (accelerator.accumulate,
+    default 4): Euler add_noise, UNet fwd, MSE + orth loss (lambda 1e-4), backward; on the window's last clip gradient
+    all-reduce (RCCL, N>1), clip_grad_norm_(0.5), AdamW(2e-5, cosine schedule with 100 warm-up steps).  N=1: every
+    clip replays one of two captured HIP graphs (accumulate / sync); N>1: eager calls with the bucketed all-reduce
+    overlapping the last clip's backward."""
     from video_style_transfer_amd import kernels as K
     from video_style_transfer_amd.config import UNetMotionConfig
     from video_style_transfer_amd.scheduler import EulerDiscreteScheduler
     from video_style_transfer_amd.temporal_lora import build_spatial_lora_index, inject_temporal_lora
-    from video_style_transfer_amd.train import GradBucketAllReducer, TrainStep, broadcast_parameters
+    from video_style_transfer_amd.train import GradBucketAllReducer, TrainStep, broadcast_parameters, get_scheduler, \
+        make_adamw
     from video_style_transfer_amd.utils import build_unet, freeze_spatial_layers
     cfg = UNetMotionConfig.sdxl()
     t_build = time.perf_counter()
@@ -305,11 +311,14 @@ def bench_train(args, world, rank, local, dev):
         broadcast_parameters(unet)
     params = [p for p in unet.parameters() if p.requires_grad]
     graph = world == 1 and not args.no_graph
-    opt = torch.optim.AdamW(params, lr=2e-5, betas=(0.9, 0.999), weight_decay=1e-2, eps=1e-8, capturable=graph)
+    # train_animatediff.py:163-169, :180-184 defaults: AdamW(2e-5, wd 1e-2), cosine schedule, 100 warm-up steps of
+    # --max_train_steps 1000; the lr lives in a device tensor so the schedule reaches the captured step
+    opt = make_adamw(params, lr=2e-5, betas=(0.9, 0.999), weight_decay=1e-2, eps=1e-8, capturable=graph, device=dev)
+    lr_sched = get_scheduler("cosine", opt, num_warmup_steps=100, num_training_steps=1000)
     reducer = GradBucketAllReducer(params) if world > 1 else None
     step = TrainStep(unet, opt, EulerDiscreteScheduler(), reducer=reducer, lambda_orth=1e-4,
                      spatial_index=build_spatial_lora_index(unet), max_grad_norm=0.5, resolution=args.size,
-                     seed=args.seed)
+                     seed=args.seed, lr_scheduler=lr_sched, gradient_accumulation_steps=args.grad_accum)
     g = torch.Generator().manual_seed(100 + rank)
     h = args.size // 8
     lat = torch.randn(1, 4, args.frames, h, h, generator=g).to(dev)
@@ -330,11 +339,17 @@ def bench_train(args, world, rank, local, dev):
     if graph:
         step.capture(lat, enc, pooled, uncond_prompt=unc, uncond_pooled=unp)
 
-        def run():
+        def micro():
             return step.replay(None if vae is None else encode_frames(vae, frames, vgen))
     else:
-        def run():
+        def micro():
             return step(lat if vae is None else encode_frames(vae, frames, vgen), enc, pooled, unc, unp)
+
+    def run():  # one optimizer step = one accumulation window of --grad-accum clips per rank
+        for _ in range(args.grad_accum):
+            out = micro()
+        assert out["sync"]
+        return out
     t_build = time.perf_counter() - t_build
     for _ in range(args.warmup):
         run()
@@ -355,13 +370,15 @@ def bench_train(args, world, rank, local, dev):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     ms_step = dt / args.steps * 1e3
-    value = args.frames * world / (ms_step * 1e-3)
+    value = args.frames * args.grad_accum * world / (ms_step * 1e-3)
     ok = bool(torch.isfinite(out["loss"]).item())
+    lr_now = float(opt.param_groups[0]["lr"])
     rl = table = step_rl = None
     if not args.no_roofline:
         # one instrumented eager step (HIP events around every launch on its stream)
         K.profile_launches(True)
-        step(lat if vae is None else encode_frames(vae, frames, vgen), enc, pooled)
+        for _ in range(args.grad_accum):  # one whole window, so the optimizer / clip launches are counted once
+            step(lat if vae is None else encode_frames(vae, frames, vgen), enc, pooled)
         rl, table = _roofline_from(K.collect_launches())
         K.profile_launches(False)
         fl = rl.pop("step_flops")
@@ -374,21 +391,24 @@ def bench_train(args, world, rank, local, dev):
         cpu = train_cpu_baseline(args, cfg)
     if rank == 0:
         print(json.dumps({
-            "metric": f"train frames/sec (fwd+bwd+AdamW step), {args.frames}x{args.size}x{args.size} clip per GPU, "
-                      f"AnimateDiff-XL temporal LoRA",
+            "metric": f"train frames/sec (fwd+bwd, AdamW step per {args.grad_accum} clips), {args.frames}x{args.size}x"
+                      f"{args.size} clips per GPU, AnimateDiff-XL temporal LoRA",
             "value": round(value, 3), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
             "config": {"workload": f"BASELINE configs[4]: train_animatediff.py step, {args.frames}x{args.size}x"
                                    f"{args.size} clip/GPU, temporal LoRA r=32, UnZipLoRA r={args.lora_rank} frozen, "
-                                   f"orth loss 1e-4, clip 0.5, AdamW" + (
+                                   f"orth loss 1e-4, clip 0.5, AdamW, cosine lr (100 warm-up), gradient accumulation "
+                                   f"{args.grad_accum} (one step = {args.grad_accum} clips per GPU)" + (
                                        ", from synthetic latents (no VAE encode)" if vae is None else
                                        ", VAE encode of the synthetic frames in every step"),
                        "model": "SDXL UNet + AnimateDiff-SDXL motion modules (synthetic weights)",
-                       "global_batch": world, "frames": args.frames, "resolution": args.size,
+                       "global_batch": world * args.grad_accum, "frames": args.frames, "resolution": args.size,
+                       "gradient_accumulation_steps": args.grad_accum,
                        "parallelism": f"dp{world}" + (" (RCCL bucketed all-reduce)" if world > 1 else ""),
                        "graph": graph, "trainable_params": sum(p.numel() for p in params)},
-            "loss": round(float(out["loss"]), 5), "finite": ok,
+            "loss": round(float(out["loss"]), 5), "finite": ok, "lr": lr_now,
+            "ms_per_clip": round(ms_step / args.grad_accum, 3),
             "roofline": rl, "step_roofline": step_rl, "cpu_baseline": cpu, "kernels": table,
             "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1), "setup_s": round(t_build, 1)}))
 

@@ -131,15 +131,15 @@ def test_grad_bucket_all_reducer_cpu_world2():
 
 
 # ------------------------------------------------------------------------------------- GPU
-def _train_setup(dev):
+def _train_setup(dev, config="tiny"):
     from video_style_transfer_amd.config import UNetMotionConfig
     from video_style_transfer_amd.temporal_lora import TemporalLoRALinear, build_spatial_lora_index, \
         inject_temporal_lora
     from video_style_transfer_amd.utils import build_unet, freeze_spatial_layers
-    cfg = UNetMotionConfig.tiny()
+    cfg = UNetMotionConfig.tiny() if config == "tiny" else UNetMotionConfig.sdxl()
     unet = build_unet(cfg, seed=3, lora_rank=8, device=dev)
     torch.manual_seed(4)
-    inject_temporal_lora(unet, rank=4, alpha=1.0)
+    inject_temporal_lora(unet, rank=4 if config == "tiny" else 32, alpha=1.0)
     with torch.no_grad():
         for m in unet.modules():
             if isinstance(m, TemporalLoRALinear):
@@ -149,6 +149,8 @@ def _train_setup(dev):
 
 
 def _clip_inputs(cfg, nclip=2, F=4, h=8):
+    if cfg.block_out_channels[0] == 320:  # SDXL: BASELINE configs[4]'s clip, 16 frames at 512^2
+        F, h = 16, 64
     g = torch.Generator().manual_seed(5)
     lat = torch.randn(nclip, 4, F, h, h, generator=g)
     noise = torch.randn(nclip, 4, F, h, h, generator=g)
@@ -158,38 +160,43 @@ def _clip_inputs(cfg, nclip=2, F=4, h=8):
     return lat, noise, t, enc, pooled
 
 
-def _run_step(unet, index, lat, noise, t, enc, pooled, reducer=None):
+def _run_step(unet, index, lat, noise, t, enc, pooled, reducer=None, sdxl=False):
     from video_style_transfer_amd.scheduler import EulerDiscreteScheduler
     from video_style_transfer_amd.train import TrainStep
     params = [p for p in unet.parameters() if p.requires_grad]
     opt = torch.optim.SGD(params, lr=0.0)  # lr 0: the weights stay comparable; the gradients are the check
-    step = TrainStep(unet, opt, EulerDiscreteScheduler(), reducer=reducer, lambda_orth=0.5, spatial_index=index,
-                     max_grad_norm=0.05, resolution=64)
+    # SDXL: the reference's orth weight and clip (train_animatediff.py:414, :394); tiny: large enough to matter
+    step = TrainStep(unet, opt, EulerDiscreteScheduler(), reducer=reducer, lambda_orth=1e-4 if sdxl else 0.5,
+                     spatial_index=index, max_grad_norm=0.5 if sdxl else 0.05, resolution=512 if sdxl else 64)
     dev = next(unet.parameters()).device
     out = step(lat.to(dev), enc, pooled, noise=noise, timesteps=t, use_uncond=False)
     grads = {n: p.grad.detach().float().cpu() for n, p in unet.named_parameters() if p.requires_grad}
     return out, grads
 
 
-def _dp_gpu_worker(rank, world, port, q):
+def _dp_gpu_worker(rank, world, port, q, config="tiny"):
     try:
         sys.path.insert(0, ROOT)
         _init(rank, world, port)
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
         from video_style_transfer_amd.train import GradBucketAllReducer
-        cfg, unet, index = _train_setup(dev)
+        sdxl = config == "sdxl"
+        cfg, unet, index = _train_setup(dev, config)
         assert index, "orth-loss pairing found no spatial partner"
         lat, noise, t, enc, pooled = _clip_inputs(cfg)
         sl = slice(rank, rank + 1)
-        red = GradBucketAllReducer([p for p in unet.parameters() if p.requires_grad], bucket_mb=1.0)
-        out, grads = _run_step(unet, index, lat[sl], noise[sl], t[sl], enc, pooled, red)
+        red = GradBucketAllReducer([p for p in unet.parameters() if p.requires_grad],
+                                   bucket_mb=64.0 if sdxl else 1.0)
+        out, grads = _run_step(unet, index, lat[sl], noise[sl], t[sl], enc, pooled, red, sdxl)
         red.remove()
+        del unet, red
+        torch.cuda.empty_cache()
         loss = torch.tensor([float(out["loss_mse"])])
         dist.all_reduce(loss)
         if rank == 0:
-            cfg, unet1, index1 = _train_setup(dev)
-            out1, grads1 = _run_step(unet1, index1, lat, noise, t, enc, pooled)
+            cfg, unet1, index1 = _train_setup(dev, config)
+            out1, grads1 = _run_step(unet1, index1, lat, noise, t, enc, pooled, sdxl=sdxl)
             errs = {n: ((grads[n] - grads1[n]).norm() / grads1[n].norm().clamp_min(1e-20)).item() for n in grads1}
             worst = max(errs, key=errs.get)
             lm, l1 = float(loss) / world, float(out1["loss_mse"])
@@ -211,10 +218,13 @@ def _dp_gpu_worker(rank, world, port, q):
 
 
 @pytest.mark.gpu
-def test_train_step_data_parallel_two_ranks_one_gpu():
+@pytest.mark.parametrize("config", ["tiny", "sdxl"])
+def test_train_step_data_parallel_two_ranks_one_gpu(config):
+    """sdxl: BASELINE configs[4]'s workload (SDXL + motion modules, UnZipLoRA r=8 frozen, temporal LoRA r=32, one
+    16x512^2 clip per rank, 64 MB buckets) -- the two ranks' bucketed average equals the 2-clip batch."""
     if torch.cuda.device_count() == 0:
         pytest.skip("no HIP device")
-    res = _spawn(_dp_gpu_worker, 2)
+    res = _spawn(_dp_gpu_worker, 2, config)
     for rank, status, info in res:
         print(f"[dp] rank {rank}: {status} {info}")
         assert status == "ok", f"rank {rank}: {info}"

@@ -1,0 +1,168 @@
+"""The configs[4] training step on the HIP path (train_animatediff.py:212-319): the captured HIP-graph step against
+the eager step, gradient accumulation and the lr schedule through the graphs, and the production-size step.
+
+  * tiny config, gradient_accumulation_steps 2, the reference's cosine-with-warm-up schedule: an eager TrainStep with
+    a plain (non-capturable) AdamW and a float lr -- the reference's optimizer -- against TrainStep.capture + replays
+    with a device-tensor lr on an identical model, for 8 calls (4 optimizer steps): loss and grad norm per call, and
+    every trainable parameter after every call.  Also: capture refuses a float lr with a scheduler, and capturing
+    changes no training state.
+  * SDXL architecture at BASELINE configs[4]'s size (16 x 512^2 clip, UnZipLoRA r=8 frozen, temporal LoRA r=32,
+    orth loss 1e-4, clip 0.5, AdamW 2e-5): the captured step equals the eager step on the same draws.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+BF = torch.bfloat16
+
+
+@pytest.fixture(scope="module")
+def cuda():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda")
+
+
+def rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _model(cfg, dev, lora_rank, t_rank, seed=3):
+    from video_style_transfer_amd.temporal_lora import TemporalLoRALinear, build_spatial_lora_index, \
+        inject_temporal_lora
+    from video_style_transfer_amd.utils import build_unet, freeze_spatial_layers
+    unet = build_unet(cfg, seed=seed, lora_rank=lora_rank, device=dev)
+    torch.manual_seed(seed + 1)
+    inject_temporal_lora(unet, rank=t_rank, alpha=1.0)
+    with torch.no_grad():
+        for m in unet.modules():
+            if isinstance(m, TemporalLoRALinear):
+                m.lora_B.normal_(0, 0.02)  # B = 0 at init would make the orth loss and its gradient vanish
+    freeze_spatial_layers(unet)
+    return unet, build_spatial_lora_index(unet)
+
+
+def _text(cfg, seed=5):
+    g = torch.Generator().manual_seed(seed)
+    enc = torch.randn(1, 77, cfg.cross_attention_dim, generator=g)
+    pooled = torch.randn(1, cfg.text_embed_dim, generator=g)
+    return enc, pooled, torch.zeros_like(enc), torch.zeros_like(pooled)
+
+
+def test_train_step_graph_equals_eager_accumulation_and_schedule(cuda):
+    from video_style_transfer_amd.config import UNetMotionConfig
+    from video_style_transfer_amd.scheduler import EulerDiscreteScheduler
+    from video_style_transfer_amd.train import TrainStep, get_scheduler, make_adamw
+    cfg = UNetMotionConfig.tiny()
+    accum, calls, lr = 2, 8, 1e-3
+    ue, index_e = _model(cfg, cuda, 8, 4)
+    ug, index_g = _model(cfg, cuda, 8, 4)
+    pe = [p for p in ue.parameters() if p.requires_grad]
+    pg = [p for p in ug.parameters() if p.requires_grad]
+    for a, b in zip(pe, pg):
+        assert torch.equal(a, b)
+    enc, pooled, unc, unp = _text(cfg)
+    lat = [torch.randn(1, 4, 4, 8, 8, generator=torch.Generator().manual_seed(10 + i)).to(cuda) for i in range(calls)]
+    kw = dict(lambda_orth=1e-2, max_grad_norm=0.5, resolution=64, seed=9, gradient_accumulation_steps=accum)
+
+    # eager = the reference's optimizer: AdamW(float lr), non-capturable; cosine, warm-up 2 of 6 optimizer steps
+    opt_e = torch.optim.AdamW(pe, lr=lr, betas=(0.9, 0.999), weight_decay=1e-2, eps=1e-8)
+    step_e = TrainStep(ue, opt_e, EulerDiscreteScheduler(), spatial_index=index_e,
+                       lr_scheduler=get_scheduler("cosine", opt_e, 2, 6), **kw)
+
+    # graph: a float lr with a scheduler must be refused (it would be baked into the captured AdamW)
+    bad = torch.optim.AdamW(pg, lr=lr, capturable=True)
+    with pytest.raises(ValueError):
+        TrainStep(ug, bad, EulerDiscreteScheduler(), spatial_index=index_g, lr_scheduler=get_scheduler("cosine", bad, 2, 6),
+                  **kw).capture(lat[0], enc, pooled)
+    for p in pg:
+        p.grad = None
+    opt_g = make_adamw(pg, lr=lr, betas=(0.9, 0.999), weight_decay=1e-2, eps=1e-8, capturable=True)
+    step_g = TrainStep(ug, opt_g, EulerDiscreteScheduler(), spatial_index=index_g,
+                       lr_scheduler=get_scheduler("cosine", opt_g, 2, 6), **kw)
+    snap = [p.detach().clone() for p in pg]
+    step_g.capture(lat[0], enc, pooled, uncond_prompt=unc, uncond_pooled=unp)
+    # capturing (two eager warm-up windows with optimizer steps) left the weights and the draws untouched
+    for a, b in zip(pg, snap):
+        assert torch.equal(a, b)
+    assert step_g.graph_micro is not None and step_g.micro == 0
+
+    prev_e = [p.detach().clone() for p in pe]
+    prev_g = [p.detach().clone() for p in pg]
+    for i in range(calls):
+        oe = step_e(lat[i], enc, pooled, unc, unp)
+        og = step_g.replay(lat[i])
+        torch.cuda.synchronize()
+        assert oe["sync"] == og["sync"] == (i % accum == accum - 1)
+        assert oe["uncond"] == og["uncond"] and torch.equal(oe["timesteps"], og["timesteps"])
+        le, lg = float(oe["loss"]), float(og["loss"])
+        assert abs(le - lg) <= 1e-3 * abs(le), (i, le, lg)
+        lr_e, lr_g = opt_e.param_groups[0]["lr"], float(opt_g.param_groups[0]["lr"])
+        assert lr_g == pytest.approx(lr_e, rel=1e-6, abs=1e-12), (i, lr_e, lr_g)
+        if og["sync"]:
+            ge, gg = float(oe["grad_norm"]), float(og["grad_norm"])
+            assert abs(ge - gg) <= 1e-2 * ge, (i, ge, gg)
+            de = torch.cat([(p.detach() - q).float().flatten() for p, q in zip(pe, prev_e)])
+            dg = torch.cat([(p.detach() - q).float().flatten() for p, q in zip(pg, prev_g)])
+            if i == accum - 1:  # the first optimizer step runs at warm-up lr 0: no parameter moves on either path
+                assert de.abs().max() == 0 and dg.abs().max() == 0
+            else:
+                e = rel(dg, de)
+                print(f"[train-graph] call {i}: lr {lr_e:.3e} loss {le:.5f}/{lg:.5f} gnorm {ge:.4e}/{gg:.4e} "
+                      f"|update| {de.norm():.3e}/{dg.norm():.3e} rel {e:.2e}")
+                assert de.norm() > 0 and e < 5e-2, (i, e)
+            prev_e = [p.detach().clone() for p in pe]
+            prev_g = [p.detach().clone() for p in pg]
+        else:
+            assert torch.isnan(og["grad_norm"])
+            for p, q in zip(pg, prev_g):  # an accumulation call never touches the weights
+                assert torch.equal(p, q)
+    for p, q in zip(pe, pg):
+        assert rel(q, p) < 1e-2
+
+
+def test_train_step_sdxl_16x512_graph_equals_eager(cuda):
+    """BASELINE configs[4] at its own size: SDXL UNet + 15 motion modules, UnZipLoRA r=8 frozen on all 560 spatial
+    projections, temporal LoRA r=32 on the 120 motion projections, one 16-frame 512^2 clip, orth loss 1e-4,
+    clip_grad_norm_(0.5), AdamW(2e-5) -- eager vs captured on the same draws and the same starting weights."""
+    from video_style_transfer_amd.config import UNetMotionConfig
+    from video_style_transfer_amd.scheduler import EulerDiscreteScheduler
+    from video_style_transfer_amd.train import TrainStep, make_adamw
+    cfg = UNetMotionConfig.sdxl()
+    unet, index = _model(cfg, cuda, 8, 32, seed=21)
+    params = [p for p in unet.parameters() if p.requires_grad]
+    assert 150e6 < sum(p.numel() for p in params) < 160e6
+    enc, pooled, unc, unp = _text(cfg, 6)
+    lat = torch.randn(1, 4, 16, 64, 64, generator=torch.Generator().manual_seed(7)).to(cuda)
+    kw = dict(lambda_orth=1e-4, spatial_index=index, max_grad_norm=0.5, resolution=512, seed=11)
+    snap = [p.detach().clone() for p in params]
+
+    opt_e = torch.optim.AdamW(params, lr=2e-5, betas=(0.9, 0.999), weight_decay=1e-2, eps=1e-8)
+    oe = TrainStep(unet, opt_e, EulerDiscreteScheduler(), **kw)(lat, enc, pooled, unc, unp)
+    torch.cuda.synchronize()
+    de = [(p.detach() - q).float() for p, q in zip(params, snap)]
+    le, ge, lo = float(oe["loss"]), float(oe["grad_norm"]), float(oe["loss_orth"])
+    del opt_e
+    with torch.no_grad():
+        for p, q in zip(params, snap):
+            p.copy_(q)
+            p.grad = None
+    torch.cuda.empty_cache()
+
+    opt_g = make_adamw(params, lr=2e-5, capturable=True)
+    step = TrainStep(unet, opt_g, EulerDiscreteScheduler(), **kw)
+    step.capture(lat, enc, pooled, uncond_prompt=unc, uncond_pooled=unp)
+    og = step.replay()
+    torch.cuda.synchronize()
+    lg, gg = float(og["loss"]), float(og["grad_norm"])
+    dg = [(p.detach() - q).float() for p, q in zip(params, snap)]
+    e_upd = rel(torch.cat([d.flatten() for d in dg]), torch.cat([d.flatten() for d in de]))
+    worst = max(range(len(params)), key=lambda i: rel(dg[i], de[i]) if de[i].norm() > 0 else 0.0)
+    print(f"[train-sdxl] loss eager {le:.6f} graph {lg:.6f} (orth {lo:.3e}); grad_norm {ge:.5e} / {gg:.5e}; "
+          f"update rel_l2 {e_upd:.2e}, worst tensor {rel(dg[worst], de[worst]):.2e}; "
+          f"peak {torch.cuda.max_memory_allocated() / 2 ** 30:.1f} GiB")
+    assert torch.isfinite(og["loss"]) and torch.isfinite(og["grad_norm"]) and lo > 0
+    assert oe["timesteps"].tolist() == og["timesteps"].tolist() and oe["uncond"] == og["uncond"]
+    assert abs(le - lg) <= 1e-4 * abs(le) and abs(ge - gg) <= 1e-3 * ge
+    assert e_upd < 1e-2

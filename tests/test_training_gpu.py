@@ -418,38 +418,42 @@ def test_transformer2d_backward_vs_oracle(cuda, unfreeze_mergers):
             assert e < 5e-2, (n, e)
 
 
-def test_unet_training_step_grads_vs_oracle(cuda):
-    """train_animatediff.py's fwd+bwd on the whole (tiny-config) AnimateDiff UNet: frozen
-    spatial path with UnZipLoRA r=4, motion modules with temporal LoRA r=4 injected and trainable per
-    freeze_spatial_layers (animatediff/utils.py:66-95).  The loss gradient w.r.t. the trainable parameters, computed
-    entirely by HIP kernels (unet_train_tokens + autograd Functions), vs torch.autograd through the fp32 oracle UNet.
-    Setup as test_unet_forward_tiny_vs_oracle (F=8, 16x16 latent, UnZipLoRA r=8): the inference path itself is 1e-2
-    from the oracle there (bf16 arithmetic); with F=2 and r=4 factors both paths drift ~0.3 (bf16 differences
-    amplified through the random-weight network), so that setup says nothing about the backward."""
+@pytest.mark.parametrize("config", ["tiny", "sdxl"])
+def test_unet_training_step_grads_vs_oracle(cuda, config):
+    """train_animatediff.py's fwd+bwd on the whole AnimateDiff UNet: frozen spatial path with
+    UnZipLoRA r=8, motion modules with temporal LoRA injected and trainable per freeze_spatial_layers
+    (animatediff/utils.py:66-95).  The loss gradient w.r.t. EVERY trainable parameter, computed entirely by HIP
+    kernels (unet_train_tokens + autograd Functions), vs torch.autograd through the fp32 oracle UNet.
+      tiny: F=8, 16x16 latent, temporal LoRA r=4;
+      sdxl: the production architecture (SDXL UNet + 15 motion modules, 156 M trainable parameters, temporal LoRA
+            r=32 as train_animatediff.py:436) at F=2 and a 64x64 latent (512^2 px), the largest size the fp32 CPU
+            oracle back-propagates in seconds.
+    Weights: the conditioned synthetic init (weights.INIT_SCALES), on which the network does not amplify single bf16
+    rounding flips, so the comparison measures the kernels (the legacy init drifted ~0.3 at F=2)."""
     from oracle.unet import LoRAState, unet_forward
     from video_style_transfer_amd import kernels as K
     from video_style_transfer_amd.autograd import unet_train_tokens
     from video_style_transfer_amd.config import UNetMotionConfig
     from video_style_transfer_amd.temporal_lora import TemporalLoRALinear, inject_temporal_lora
     from video_style_transfer_amd.utils import build_unet, freeze_spatial_layers
-    from video_style_transfer_amd.weights import synthetic_state_dict
-    cfg = UNetMotionConfig.tiny()
-    sd = synthetic_state_dict(cfg, 0, 8)
-    sd = {k: (v if "lora_layer" in k else v.to(BF).float()) for k, v in sd.items()}
-    unet = build_unet(cfg, state_dict=sd, lora_rank=8, device=cuda)
+    if config == "tiny":
+        cfg, B, Fr, h, rank = UNetMotionConfig.tiny(), 1, 8, 16, 4
+    else:
+        cfg, B, Fr, h, rank = UNetMotionConfig.sdxl(), 1, 2, 64, 32
+    torch.set_num_threads(16)
+    unet = build_unet(cfg, seed=0, lora_rank=8, device=cuda)
     torch.manual_seed(1)
-    assert inject_temporal_lora(unet, rank=4, alpha=1.0) > 0
+    assert inject_temporal_lora(unet, rank=rank, alpha=1.0) > 0
     with torch.no_grad():
         for m in unet.modules():
             if isinstance(m, TemporalLoRALinear):
-                m.lora_B.normal_(0, 0.02)
+                m.lora_B.normal_(0, 0.02)  # B = 0 at init would zero every lora_A gradient
     freeze_spatial_layers(unet)
-    B, Fr, h = 1, 8, 16
     g = torch.Generator().manual_seed(2)
     sample = torch.randn(B, 4, Fr, h, h, generator=g).to(BF).float()
     enc = torch.randn(B, 77, cfg.cross_attention_dim, generator=g).to(BF).float()
     pooled = torch.randn(B, cfg.text_embed_dim, generator=g).to(BF).float()
-    tids = torch.tensor([[128, 128, 0, 0, 128, 128]], dtype=torch.float32)
+    tids = torch.tensor([[8 * h, 8 * h, 0, 0, 8 * h, 8 * h]], dtype=torch.float32)
     t = torch.tensor([761.0])
     G = torch.randn(B * Fr * h * h, 4, generator=g).to(BF).float()
 
@@ -469,6 +473,7 @@ def test_unet_training_step_grads_vs_oracle(cuda):
     ref = unet_forward(P, cfg.to_dict(), sample, t, enc, pooled, tids, LoRAState())
     ref_tok = ref.permute(0, 2, 3, 4, 1).reshape(-1, 4)
     (ref_tok * G).sum().backward()
+    del P, ref
 
     emb = unet.embed(t.to(cuda).expand(B).contiguous(), pooled.to(cuda, BF), tids.to(cuda), B)
     x = torch.empty(B * Fr * h * h, 4, dtype=BF, device=cuda)
@@ -478,19 +483,29 @@ def test_unet_training_step_grads_vs_oracle(cuda):
 
     with torch.no_grad():
         y_inf = unet.forward_tokens(x, B, Fr, h, h, emb, enc.to(cuda, BF))
-    print(f"[train] unet inference path vs oracle: rel_l2={rel(y_inf, ref_tok.detach()):.2e}; "
+    print(f"[train] {config} unet inference path vs oracle: rel_l2={rel(y_inf, ref_tok.detach()):.2e}; "
           f"training vs inference: {rel(y, y_inf):.2e}")
     e = rel(y, ref_tok.detach())
-    print(f"[train] unet y: rel_l2={e:.2e}")
+    print(f"[train] {config} unet y: rel_l2={e:.2e}")
     assert e < 3e-2
     named = dict(unet.named_parameters())
     trainable = [n for n, p in named.items() if p.requires_grad]
     assert trainable and all("motion_modules" in n for n in trainable)
-    picks = [n for n in trainable if n.endswith("lora_A")][:2] + [n for n in trainable if n.endswith("lora_B")][-2:] + \
-        [n for n in trainable if "ff.net.0.proj.weight" in n][:2] + [n for n in trainable if "proj_out.weight" in n][-1:]
-    for n in picks:
+    errs = {}
+    for n in trainable:
         got, want = named[n].grad, leaves[n].grad
-        assert got is not None, n
-        e = rel(got, want)
-        print(f"[train] unet grad {n}: rel_l2={e:.2e}")
-        assert e < 5e-2, (n, e)
+        assert got is not None and want is not None, n
+        errs[n] = rel(got, want)
+    order = sorted(errs, key=errs.get)
+    kinds = {}
+    for n in trainable:
+        k = n.split(".transformer_blocks.0.")[-1] if ".transformer_blocks.0." in n else n.rsplit(".", 2)[-2] + "." + \
+            n.rsplit(".", 1)[-1]
+        kinds[k] = max(kinds.get(k, 0.0), errs[n])
+    print(f"[train] {config}: {len(errs)} trainable tensors ({sum(named[n].numel() for n in trainable) / 1e6:.1f} M "
+          f"params); grad rel_l2 median {errs[order[len(order) // 2]]:.2e}, 95th pct "
+          f"{errs[order[int(0.95 * (len(order) - 1))]]:.2e}, worst {order[-1]} {errs[order[-1]]:.2e}")
+    for k, v in sorted(kinds.items(), key=lambda kv: -kv[1]):
+        print(f"[train] {config}   worst per kind {k:40s} {v:.2e}")
+    bad = {n: e for n, e in errs.items() if e >= 5e-2}
+    assert not bad, bad

@@ -16,6 +16,8 @@ with data-parallel gradient averaging over RCCL.
 """
 from __future__ import annotations
 
+import functools
+import math
 from typing import Dict, Iterable, List, Optional
 
 import torch
@@ -61,11 +63,16 @@ class GradBucketAllReducer:
         self._ready = [set() for _ in self.buckets]
         self._works: List[Optional[object]] = [None] * len(self.buckets)
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+        # False inside an accumulation window (DDP's no_sync): gradients only accumulate locally; the sync call's
+        # hooks then see the accumulated p.grad and reduce it
+        self.sync = True
 
     def bucket_sizes_mb(self) -> List[float]:
         return [t.numel() * t.element_size() / 2 ** 20 for t in self.flat]
 
     def _on_grad(self, p: torch.nn.Parameter) -> None:
+        if not self.sync:
+            return
         b, off = self.where[id(p)]
         self.flat[b][off:off + p.numel()].copy_(p.grad.reshape(-1))
         self._ready[b].add(id(p))
@@ -84,6 +91,8 @@ class GradBucketAllReducer:
     def finish(self) -> None:
         """Launch the buckets that still wait for unused parameters (their segments are zero-filled), wait for every
         all-reduce, divide by the world size and write the averages back into p.grad."""
+        if not self.sync:
+            raise RuntimeError("GradBucketAllReducer.finish() inside an accumulation window (sync=False)")
         for b, plist in enumerate(self.buckets):
             if self._works[b] is None:
                 for p in plist:
@@ -123,17 +132,79 @@ def broadcast_parameters(module: torch.nn.Module, src: int = 0, group=None) -> N
             dist.broadcast(t.data, src, group=group)
 
 
+def _cosine_with_warmup(step: int, warmup: int, total: int, num_cycles: float = 0.5) -> float:
+    if step < warmup:
+        return float(step) / float(max(1, warmup))
+    progress = float(step - warmup) / float(max(1, total - warmup))
+    return max(0.0, 0.5 * (1.0 + math.cos(math.pi * float(num_cycles) * 2.0 * progress)))
+
+
+def _linear_with_warmup(step: int, warmup: int, total: int) -> float:
+    if step < warmup:
+        return float(step) / float(max(1, warmup))
+    return max(0.0, float(total - step) / float(max(1, total - warmup)))
+
+
+def get_scheduler(name: str, optimizer, num_warmup_steps: int = 0, num_training_steps: int = 0):
+    """diffusers.optimization.get_scheduler (train_animatediff.py:180-184; `--lr_scheduler` default "cosine", 100
+    warmup steps, :403-404): a LambdaLR over the optimizer's lr.  "cosine" is half a cosine cycle after a linear
+    warmup, "linear" a linear decay after it, "constant_with_warmup" / "constant" what they say.  With a device-tensor
+    lr (make_adamw(..., capturable=True)) every step() writes the new value into that tensor in place, so a captured
+    AdamW reads it on the next replay."""
+    w, n = num_warmup_steps, num_training_steps
+    if name == "cosine":
+        fn = functools.partial(_cosine_with_warmup, warmup=w, total=n)
+    elif name == "linear":
+        fn = functools.partial(_linear_with_warmup, warmup=w, total=n)
+    elif name == "constant_with_warmup":
+        def fn(step):
+            return float(step) / float(max(1, w)) if step < w else 1.0
+    elif name == "constant":
+        def fn(step):
+            return 1.0
+    else:
+        raise ValueError(f"get_scheduler: unsupported schedule {name!r} (cosine, linear, constant_with_warmup, "
+                         "constant)")
+    return torch.optim.lr_scheduler.LambdaLR(optimizer, fn)
+
+
+def make_adamw(params, lr: float = 2e-5, betas=(0.9, 0.999), weight_decay: float = 1e-2, eps: float = 1e-8, *,
+               capturable: bool = False, device=None):
+    """The reference's optimizer (train_animatediff.py:163-169: AdamW, --learning_rate 2e-5, betas 0.9/0.999, weight
+    decay 1e-2, eps 1e-8).  capturable=True (for TrainStep.capture) keeps lr as a one-element fp32 tensor on the
+    parameters' device: a Python-float lr would be baked into the captured update kernels (both the step size and the
+    decoupled decay 1 - lr*wd), and the lr schedule would never reach the replayed graph."""
+    params = list(params)
+    if capturable:
+        dev = device if device is not None else params[0].device
+        lr = torch.tensor(float(lr), dtype=torch.float32, device=dev)
+    return torch.optim.AdamW(params, lr=lr, betas=betas, weight_decay=weight_decay, eps=eps, capturable=capturable)
+
+
 class TrainStep:
     """One train_animatediff.py iteration (:214-319) for a UNetMotionModel with temporal LoRA injected and the spatial
     path frozen (`utils.freeze_spatial_layers`).  Inputs are VAE latents already scaled by vae.scaling_factor
-    (B, 4, F, h, w) fp32 on the device; prompt embeddings are (1, 77, D) / (1, Dp) as encode_prompt returns them."""
+    (B, 4, F, h, w) fp32 on the device; prompt embeddings are (1, 77, D) / (1, Dp) as encode_prompt returns them.
+
+    Gradient accumulation follows `accelerator.accumulate(unet)` with `Accelerator(gradient_accumulation_steps=N)`
+    (:51-54, :214; accelerate 1.x semantics, pinned against accelerate itself by tests/test_train_host.py): every call
+    is one micro-batch; the loss is divided by N before the backward (`accelerator.backward`); the gradients of N
+    consecutive calls accumulate; only the N-th call (`sync_gradients`) all-reduces them over the data-parallel ranks
+    (DDP's no_sync on the others), clips (:315-316), steps the optimizer and zeroes the gradients (:317-319).  The lr
+    scheduler, wrapped by accelerate, advances only on sync calls and then once per process
+    (AcceleratedScheduler.step with split_batches=False), so on P ranks the schedule runs P times as fast per
+    optimizer step, as in the reference."""
 
     def __init__(self, unet, optimizer, scheduler, *, reducer: Optional[GradBucketAllReducer] = None,
                  lambda_orth: float = 0.0, spatial_index: Optional[Dict] = None, max_grad_norm: float = 1.0,
-                 p_uncond: float = 0.1, resolution: int = 512, seed: int = 0, lr_scheduler=None):
+                 p_uncond: float = 0.1, resolution: int = 512, seed: int = 0, lr_scheduler=None,
+                 gradient_accumulation_steps: int = 1, num_processes: Optional[int] = None):
         """`seed` is offset by the process rank: every data-parallel rank draws its own noise, timesteps and
         unconditional-prompt coin (the reference's per-process RNG streams).  `lr_scheduler` (optional) steps after
-        the optimizer (train_animatediff.py:318)."""
+        the optimizer (train_animatediff.py:318), `num_processes` times per optimizer step (default: the world
+        size)."""
+        if gradient_accumulation_steps < 1:
+            raise ValueError("gradient_accumulation_steps must be >= 1")
         self.unet = unet
         self.opt = optimizer
         self.sched = scheduler
@@ -144,9 +215,19 @@ class TrainStep:
         self.max_grad_norm = max_grad_norm
         self.p_uncond = p_uncond
         self.resolution = resolution
+        self.accum = int(gradient_accumulation_steps)
+        self.micro = 0  # calls since the last sync (accelerator.step)
+        self.graph = self.graph_micro = None
         self.params = [p for p in unet.parameters() if p.requires_grad]
-        rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+        dist_on = dist.is_available() and dist.is_initialized()
+        rank = dist.get_rank() if dist_on else 0
+        self.num_processes = num_processes or (dist.get_world_size() if dist_on else 1)
         self.gen = torch.Generator(device="cpu").manual_seed(seed + 1000003 * rank)
+
+    @property
+    def sync_gradients(self) -> bool:
+        """Whether the next call ends an accumulation window (accelerate's GradientState.sync_gradients)."""
+        return (self.micro + 1) % self.accum == 0
 
     def _draw(self, latents, noise=None, timesteps=None, use_uncond=None, has_uncond=False):
         """The step's random draws (train_animatediff.py:228-254) from this rank's generator; overrides win."""
@@ -165,10 +246,31 @@ class TrainStep:
         pool = pool.expand(B, -1).contiguous()
         return enc, pool
 
-    def _body(self, latents, noise, t, enc, pool) -> Dict:
-        """Forward, losses, backward, gradient averaging, clipping and the optimizer step on device tensors only (no
-        host synchronisation: the body is what TrainStep.capture records into a HIP graph).  Gradients must be
-        None or zero on entry."""
+    def _body(self, latents, noise, t, enc, pool, sync: bool = True, zero_in_place: bool = False) -> Dict:
+        """Forward, losses, backward (gradients accumulate into p.grad); on a sync call also gradient averaging,
+        clipping and the optimizer step.  Device tensors only (no host synchronisation: the body is what
+        TrainStep.capture records into a HIP graph).  zero_in_place: the sync body ends by zeroing the gradient
+        tensors in place (the captured graphs keep static .grad tensors), instead of the eager zero_grad(None)."""
+        dev = latents.device
+        loss, loss_mse, loss_orth = self._loss(latents, noise, t, enc, pool)
+        if self.reducer is not None:
+            self.reducer.sync = sync                                                       # DDP no_sync otherwise
+        (loss / self.accum if self.accum > 1 else loss).backward()                         # :314 accelerator.backward
+        if sync:
+            if self.reducer is not None:
+                self.reducer.finish()
+            gnorm = torch.nn.utils.clip_grad_norm_(self.params, self.max_grad_norm)       # :315-316
+            self.opt.step()                                                                # :317
+            if zero_in_place:
+                torch._foreach_zero_([p.grad for p in self.params])                        # :319
+        else:
+            gnorm = torch.full((), float("nan"), device=dev)                               # no clip on this call
+        return {"loss": loss.detach(), "loss_mse": loss_mse.detach(), "loss_orth": loss_orth.detach(),
+                "grad_norm": gnorm.detach()}
+
+    def _loss(self, latents, noise, t, enc, pool):
+        """The micro-batch loss (train_animatediff.py:228-312): Euler add_noise, the HIP UNet forward, epsilon MSE in
+        fp32 and the orthogonality loss."""
         from . import kernels as K
         from .autograd import unet_train_tokens
         from .temporal_lora import compute_orth_loss
@@ -190,14 +292,7 @@ class TrainStep:
             loss_orth = compute_orth_loss(unet, self.spatial_index, self.lambda_orth).to(dev)
         else:
             loss_orth = torch.zeros((), device=dev)
-        loss = loss_mse + loss_orth
-        loss.backward()                                                                    # :314
-        if self.reducer is not None:
-            self.reducer.finish()
-        gnorm = torch.nn.utils.clip_grad_norm_(self.params, self.max_grad_norm)           # :316
-        self.opt.step()                                                                    # :317
-        return {"loss": loss.detach(), "loss_mse": loss_mse.detach(), "loss_orth": loss_orth.detach(),
-                "grad_norm": gnorm.detach()}
+        return loss_mse + loss_orth, loss_mse, loss_orth
 
     def _tids(self, B, dev):
         key = (B, dev)
@@ -207,33 +302,61 @@ class TrainStep:
             c[key] = torch.tensor([[r, r, 0.0, 0.0, r, r]], device=dev).expand(B, -1).contiguous()
         return c[key]
 
+    def _advance(self, sync: bool) -> None:
+        """accelerate's bookkeeping after a call: the step counter, and AcceleratedScheduler.step (:318)."""
+        self.micro = 0 if sync else self.micro + 1
+        if self.lr_scheduler is None:
+            return
+        if not sync:
+            self.lr_scheduler._step_count += 1  # GradientAccumulationPlugin.adjust_scheduler: counted, lr unchanged
+            return
+        for _ in range(self.num_processes):
+            self.lr_scheduler.step()
+
     def __call__(self, latents: torch.Tensor, prompt, pooled, uncond_prompt=None, uncond_pooled=None, *,
                  noise: Optional[torch.Tensor] = None, timesteps: Optional[torch.Tensor] = None,
                  use_uncond: Optional[bool] = None) -> Dict:
-        """noise / timesteps / use_uncond override the step's random draws (tests compare a data-parallel step
-        with a single-process step on the concatenated batch)."""
+        """One eager micro-batch.  noise / timesteps / use_uncond override the step's random draws (tests compare a
+        data-parallel step with a single-process step on the concatenated batch).  The returned "loss" is the
+        undivided micro-batch loss (what the reference logs); "grad_norm" is NaN on calls that do not sync."""
         dev = latents.device
         B = latents.shape[0]
         noise, t, use_uncond = self._draw(latents, noise, timesteps, use_uncond, uncond_prompt is not None)
         enc, pool = self._text(uncond_prompt if use_uncond else prompt, uncond_pooled if use_uncond else pooled, B,
                                dev)
-        self.opt.zero_grad(set_to_none=True)
-        out = self._body(latents, noise.to(dev, torch.float32), t.to(dev), enc, pool)
-        if self.lr_scheduler is not None:
-            self.lr_scheduler.step()                                                       # :318
-        out.update(uncond=use_uncond, timesteps=t)
+        sync = self.sync_gradients
+        if self.micro == 0:  # the previous window's :319 (accelerate zeroes only on sync calls)
+            if self.graph is not None:
+                torch._foreach_zero_([p.grad for p in self.params if p.grad is not None])  # keep the static grads
+            else:
+                self.opt.zero_grad(set_to_none=True)
+        out = self._body(latents, noise.to(dev, torch.float32), t.to(dev), enc, pool, sync=sync)
+        self._advance(sync)
+        out.update(uncond=use_uncond, timesteps=t, sync=sync)
         return out
 
     # ---- HIP-graph capture of the whole step (single process) ------------------------------------------------
     def capture(self, latents: torch.Tensor, prompt, pooled, warmup: int = 2, uncond_prompt=None, uncond_pooled=None):
-        """Record one whole training step (forward, backward, clipping, AdamW) into a HIP graph on static buffers,
-        after `warmup` eager steps on a side stream (they fill every frozen-operand cache).  The optimizer must be
-        built with capturable=True; per-step host work left outside the graph: the random draws (copied into the
-        static noise / timestep buffers) and the lr schedule.  Single-process only (the reducer's collectives stay
-        eager)."""
+        """Record the step into HIP graphs on static buffers: one graph for the sync call (forward, backward,
+        clipping, AdamW, zeroing) and, with gradient accumulation, one for the other calls (forward + backward
+        accumulating into the static .grad tensors).  `warmup` eager windows run first on a side stream (they fill
+        every frozen-operand cache and create the optimizer state); the trainable parameters, the optimizer state,
+        the gradients and this rank's random generator are then restored, so capturing changes no training state.
+        The optimizer must be capturable; with an lr scheduler its lr must be a device tensor (make_adamw) so the
+        schedule reaches the replays.  Per-call host work left outside the graphs: the random draws (copied into
+        the static noise / timestep / text buffers) and the scheduler step.  Single process only (the reducer's
+        collectives stay eager)."""
         if self.reducer is not None and self.reducer.world > 1:
             raise NotImplementedError("TrainStep.capture: data-parallel steps run eagerly")
         dev = latents.device
+        for g in self.opt.param_groups:
+            if not g.get("capturable", False):
+                raise ValueError("TrainStep.capture: the optimizer must be built with capturable=True")
+            if self.lr_scheduler is not None and not (isinstance(g["lr"], torch.Tensor) and g["lr"].device == dev):
+                raise ValueError("TrainStep.capture: with an lr scheduler the optimizer's lr must be a device tensor "
+                                 "(train.make_adamw(..., capturable=True)); a float lr is baked into the graph")
+        if self.micro != 0:
+            raise RuntimeError("TrainStep.capture: call at the start of an accumulation window")
         B = latents.shape[0]
         self.s_lat = latents.detach().clone()
         self.s_noise = torch.zeros_like(self.s_lat)
@@ -242,24 +365,59 @@ class TrainStep:
         # the two text conditions a step can draw (:248-254), copied into the static buffers before each replay
         self.text_cond = (self.s_enc.clone(), self.s_pool.clone())
         self.text_uncond = None if uncond_prompt is None else self._text(uncond_prompt, uncond_pooled, B, dev)
+
+        # training state the warm-up must not change
+        gen_state = self.gen.get_state()
+        with torch.no_grad():
+            p_snap = [p.detach().clone() for p in self.params]
+        st_snap = {id(p): {k: (v.detach().clone() if isinstance(v, torch.Tensor) else v)
+                           for k, v in self.opt.state[p].items()} for p in self.params if p in self.opt.state}
+        for p in self.params:  # static gradient tensors, shared by both graphs (accumulation across replays)
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            else:
+                p.grad.zero_()
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
             for _ in range(warmup):
-                noise, t, _ = self._draw(self.s_lat)
-                self.s_noise.copy_(noise)
-                self.s_t.copy_(t)
-                self.opt.zero_grad(set_to_none=True)
-                self._body(self.s_lat, self.s_noise, self.s_t, self.s_enc, self.s_pool)
+                for k in range(self.accum):
+                    noise, t, _ = self._draw(self.s_lat)
+                    self.s_noise.copy_(noise)
+                    self.s_t.copy_(t)
+                    self._body(self.s_lat, self.s_noise, self.s_t, self.s_enc, self.s_pool,
+                               sync=k == self.accum - 1, zero_in_place=True)
+            with torch.no_grad():
+                for p, v in zip(self.params, p_snap):
+                    p.copy_(v)
+                for p in self.params:
+                    st = self.opt.state.get(p)
+                    if not st:
+                        continue
+                    old = st_snap.get(id(p))
+                    for k, v in st.items():
+                        if isinstance(v, torch.Tensor):
+                            if old is not None and isinstance(old.get(k), torch.Tensor):
+                                v.copy_(old[k])
+                            else:
+                                v.zero_()           # state created by the warm-up: back to its initial zeros
+                torch._foreach_zero_([p.grad for p in self.params])
         torch.cuda.current_stream(dev).wait_stream(s)
-        self.opt.zero_grad(set_to_none=True)
+        self.gen.set_state(gen_state)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            self.s_out = self._body(self.s_lat, self.s_noise, self.s_t, self.s_enc, self.s_pool)
+            self.s_out = self._body(self.s_lat, self.s_noise, self.s_t, self.s_enc, self.s_pool, sync=True,
+                                    zero_in_place=True)
+        if self.accum > 1:
+            self.graph_micro = torch.cuda.CUDAGraph()  # own memory pool: its temporaries never alias s_out
+            with torch.cuda.graph(self.graph_micro):
+                self.s_out_micro = self._body(self.s_lat, self.s_noise, self.s_t, self.s_enc, self.s_pool,
+                                              sync=False)
         return self.graph
 
     def replay(self, latents: Optional[torch.Tensor] = None) -> Dict:
-        """One captured step on new latents (or the static ones) with fresh noise / timestep draws."""
+        """One captured micro-batch on new latents (or the static ones) with fresh noise / timestep draws.  The
+        returned tensors are the graph's static outputs: read them before the next replay of the same graph."""
         if latents is not None:
             self.s_lat.copy_(latents)
         noise, t, use_uncond = self._draw(self.s_lat, has_uncond=self.text_uncond is not None)
@@ -268,10 +426,10 @@ class TrainStep:
         enc, pool = self.text_uncond if use_uncond else self.text_cond
         self.s_enc.copy_(enc)
         self.s_pool.copy_(pool)
-        self.graph.replay()
-        if self.lr_scheduler is not None:
-            self.lr_scheduler.step()
-        return self.s_out
+        sync = self.sync_gradients
+        (self.graph if sync else self.graph_micro).replay()
+        self._advance(sync)
+        return dict(self.s_out if sync else self.s_out_micro, uncond=use_uncond, timesteps=t, sync=sync)
 
 
 def encode_frames(vae, frames: torch.Tensor, generator: Optional[torch.Generator] = None) -> torch.Tensor:

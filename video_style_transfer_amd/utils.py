@@ -138,8 +138,9 @@ def attach_unziplora_layers(unet, rank: int):
 
 
 def build_unet(cfg: Optional[UNetMotionConfig] = None, *, state_dict=None, seed: int = 0, lora_rank: Optional[int] = 8,
-               device="cuda", dtype=torch.bfloat16, strict: bool = True) -> UNetMotionModel:
-    """UNetMotionModel with UnZipLoRA layers, weights from `state_dict` or seeded synthetic ones."""
+               device="cuda", dtype=torch.bfloat16, strict: bool = True, init: Optional[str] = None) -> UNetMotionModel:
+    """UNetMotionModel with UnZipLoRA layers, weights from `state_dict` or seeded synthetic ones (`init`: the
+    synthetic-init family, weights.INIT_SCALES; default weights.DEFAULT_INIT)."""
     cfg = cfg or UNetMotionConfig.sdxl()
     with torch.device("meta"):
         unet = UNetMotionModel(cfg)
@@ -151,7 +152,7 @@ def build_unet(cfg: Optional[UNetMotionConfig] = None, *, state_dict=None, seed:
         for name, p in unet.named_parameters():
             if "lora_layer" not in name:
                 p.data = p.data.to(dtype)
-        init_synthetic_(unet, cfg, seed, lora_rank)
+        init_synthetic_(unet, cfg, seed, lora_rank, **({} if init is None else {"init": init}))
         return unet.requires_grad_(False)
     unet = unet.to_empty(device="cpu")
     if lora_rank:

@@ -151,10 +151,25 @@ def param_shapes(cfg: UNetMotionConfig, lora_rank: int | None = 8) -> "OrderedDi
     return S
 
 
-def _init_value(name, shape, kind, g, device):
+# Synthetic-init families.  "legacy" (rounds 1-2): unit-gain projections, residual-branch outputs at 0.5/sqrt(fan_in).
+# With q and k at unit gain the attention logits have std ~1 before any LoRA delta, and the 70 spatial blocks of the
+# SDXL UNet amplify a 1e-3 input perturbation ~47x (F=2, 16x16 latent, fp32 oracle): every end-to-end parity gate
+# then measures that chaos instead of the kernels.  "conditioned" (default) keeps the same random streams but sets
+# q/k at 0.4/sqrt(fan_in) (softer attention, as trained SDXL heads mostly are) and residual-branch outputs at
+# 0.25/sqrt(fan_in): the same perturbation then grows 1.3-1.4x at 16x16 and 32x32 latents, and bf16 autocast lands
+# 1.8e-2 / 2.3e-2 from fp32 instead of 4.8e-1 (tools/init_conditioning.py).
+INIT_SCALES = {"legacy": {"wo": 0.5, "qk": 1.0}, "conditioned": {"wo": 0.25, "qk": 0.4}}
+DEFAULT_INIT = "conditioned"
+
+
+def _init_value(name, shape, kind, g, device, init=DEFAULT_INIT):
     if kind in ("w", "wo"):
+        sc = INIT_SCALES[init]
         fan_in = int(math.prod(shape[1:]))
-        return torch.randn(shape, generator=g, device=device) * ((0.5 if kind == "wo" else 1.0) / math.sqrt(fan_in))
+        gain = sc["wo"] if kind == "wo" else 1.0
+        if name.endswith((".to_q.weight", ".to_k.weight")):
+            gain *= sc["qk"]
+        return torch.randn(shape, generator=g, device=device) * (gain / math.sqrt(fan_in))
     if kind == "b":
         return torch.randn(shape, generator=g, device=device) * 0.02
     if kind == "g":
@@ -170,7 +185,7 @@ def _init_value(name, shape, kind, g, device):
 
 
 @torch.no_grad()
-def init_synthetic_(module, cfg: UNetMotionConfig, seed: int = 0, lora_rank: int | None = 8):
+def init_synthetic_(module, cfg: UNetMotionConfig, seed: int = 0, lora_rank: int | None = 8, init: str = DEFAULT_INIT):
     """Fill an existing (e.g. to_empty'd) module in place, on its own device, with the same
     distributions as synthetic_state_dict (device RNG: values differ from the CPU stream)."""
     sd = module.state_dict()
@@ -178,21 +193,21 @@ def init_synthetic_(module, cfg: UNetMotionConfig, seed: int = 0, lora_rank: int
     g = torch.Generator(device=dev).manual_seed(seed)
     for name, (shape, kind) in param_shapes(cfg, lora_rank).items():
         t = sd[name]
-        t.copy_(_init_value(name, shape, kind, g, dev).to(t.dtype))
+        t.copy_(_init_value(name, shape, kind, g, dev, init).to(t.dtype))
     return module
 
 
 def synthetic_state_dict(cfg: UNetMotionConfig, seed: int = 0, lora_rank: int | None = 8,
-                         dtype: torch.dtype = torch.float32) -> "OrderedDict[str, torch.Tensor]":
-    """Seeded synthetic weights: linear/conv ~ N(0,1)/sqrt(fan_in) (0.5x on the
-    residual-branch outputs), biases N(0, 0.02), norm gamma 1+N(0,0.05) / beta N(0,0.02),
+                         dtype: torch.dtype = torch.float32, init: str = DEFAULT_INIT) -> "OrderedDict[str, torch.Tensor]":
+    """Seeded synthetic weights: linear/conv ~ N(0,1)/sqrt(fan_in) (q/k and the
+    residual-branch outputs scaled per INIT_SCALES[init]), biases N(0, 0.02), norm gamma 1+N(0,0.05) / beta N(0,0.02),
     UnZipLoRA A,B ~ N(0, 1/r) (unziplora_linear_layer.py:281-282), mergers ~ U(0,1).
     Values are generated in fp32 on CPU, then rounded to `dtype` (bf16 for the device path; the
     oracle consumes the same bf16-rounded values in fp32)."""
     g = torch.Generator().manual_seed(seed)
     out = OrderedDict()
     for name, (shape, kind) in param_shapes(cfg, lora_rank).items():
-        out[name] = _init_value(name, shape, kind, g, "cpu").to(dtype)
+        out[name] = _init_value(name, shape, kind, g, "cpu", init).to(dtype)
     return out
 
 
@@ -250,5 +265,5 @@ def vae_param_shapes(cfg) -> "OrderedDict[str, tuple]":
 def vae_synthetic_state_dict(cfg, seed: int = 0, dtype: torch.dtype = torch.float32) -> "OrderedDict[str, torch.Tensor]":
     """Seeded synthetic AutoencoderKL weights (same distributions as synthetic_state_dict; no checkpoint offline)."""
     g = torch.Generator().manual_seed(seed)
-    return OrderedDict((name, _init_value(name, shape, kind, g, "cpu").to(dtype))
+    return OrderedDict((name, _init_value(name, shape, kind, g, "cpu", "legacy").to(dtype))
                        for name, (shape, kind) in vae_param_shapes(cfg).items())
