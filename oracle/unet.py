@@ -28,7 +28,7 @@ def _p(P, k):
 def timestep_embedding(t, dim, flip_sin_to_cos=True, shift=0.0):
     """diffusers get_timestep_embedding (max_period 10000, scale 1)."""
     half = dim // 2
-    exponent = -math.log(10000) * torch.arange(half, dtype=torch.float32) / (half - shift)
+    exponent = -math.log(10000) * torch.arange(half, dtype=torch.float32, device=t.device) / (half - shift)
     emb = t.float()[:, None] * torch.exp(exponent)[None, :]
     emb = torch.cat([torch.sin(emb), torch.cos(emb)], dim=-1)
     if flip_sin_to_cos:
@@ -150,9 +150,12 @@ def unet_forward(P, cfg, sample, timestep, encoder_hidden_states, text_embeds, t
     """
     lora = lora if lora is not None else LoRAState()
     sample = sample.float()
+    dev = sample.device  # the restatement runs wherever its inputs live (CPU; torch fp32 on a GPU for big loops)
+    encoder_hidden_states, text_embeds, time_ids = (encoder_hidden_states.to(dev), text_embeds.to(dev),
+                                                    time_ids.to(dev))
     B, Cin, Fr, h, w = sample.shape
     ch = list(cfg["block_out_channels"])
-    t = timestep.float().reshape(-1)
+    t = timestep.float().reshape(-1).to(dev)
     if t.numel() == 1:
         t = t.expand(B)
     t_emb = timestep_embedding(t, ch[0])

@@ -127,7 +127,7 @@ def proj(P, names, x, lora: Optional[LoRAState] = None, residual=None, u=None, g
     for n in names:
         W = _w(P, n + ".weight")
         Ws.append(W)
-        bs.append(P[n + ".bias"].float() if n + ".bias" in P else torch.zeros(W.shape[0]))
+        bs.append(P[n + ".bias"].float() if n + ".bias" in P else torch.zeros(W.shape[0], device=W.device))
         lr = _lowrank(P, n, lora)
         As.append(None if lr is None else lr[0])
         Vs.append(None if lr is None else lr[1])
@@ -137,7 +137,7 @@ def proj(P, names, x, lora: Optional[LoRAState] = None, residual=None, u=None, g
         if u is None:
             u = q(mm(x, A.t()))
         R = A.shape[0]
-        V = torch.zeros(y.shape[1], R)
+        V = torch.zeros(y.shape[1], R, device=y.device)
         o_n = o_r = 0
         for W, v in zip(Ws, Vs):
             if v is not None:
@@ -192,9 +192,9 @@ def attention_core(qm, km, vm, heads, nbatch, Nq, Nk, kv_div=1, scale=None, tile
         p = torch.exp((s - s.amax(-1, keepdim=True)) * scale)
         o = mm(q(p), vh) / p.sum(-1, keepdim=True)
     else:
-        m = torch.full(s.shape[:-1] + (1,), -float("inf"))
+        m = torch.full(s.shape[:-1] + (1,), -float("inf"), device=s.device)
         l = torch.zeros_like(m)
-        o = torch.zeros(s.shape[:-1] + (hd,))
+        o = torch.zeros(s.shape[:-1] + (hd,), device=s.device)
         for k0 in range(0, Nk, tile):
             st = s[..., k0:k0 + tile]
             m_new = torch.maximum(m, st.amax(-1, keepdim=True))
@@ -381,10 +381,12 @@ def pack(sample, scale=1.0):
 def unet_forward(P, cfg, sample, timestep, encoder_hidden_states, text_embeds, time_ids, lora: LoRAState = None):
     """UNetMotionModel.forward (inference_animatediff.py:110-121) in bf16 emulation; 5-D in, 5-D fp32 out."""
     B, Cin, Fr, h, w = sample.shape
-    t = timestep.float().reshape(-1)
+    dev = sample.device
+    t = timestep.float().reshape(-1).to(dev)
     if t.numel() == 1:
         t = t.expand(B)
-    emb = embed(P, cfg, t, text_embeds, time_ids)
+    emb = embed(P, cfg, t, text_embeds.to(dev), time_ids.to(dev))
+    encoder_hidden_states = encoder_hidden_states.to(dev)
     enc = q(encoder_hidden_states.float()).reshape(-1, encoder_hidden_states.shape[-1])
     y = unet_forward_tokens(P, cfg, pack(sample), B, Fr, h, w, emb, enc, lora)
     return y.view(B, Fr, h, w, -1).permute(0, 4, 1, 2, 3)
@@ -395,15 +397,16 @@ def denoise(P, cfg, latents, cond, uncond, time_ids, num_steps, guidance, lora=N
     emulation: CFG batched as [uncond, cond], fp32 latents, Euler update from the bf16 noise."""
     ts, sigmas, _ = euler_schedule(num_steps)
     lat = latents.float().clone()
+    dev = lat.device
     B, Cl, Fr, h, w = lat.shape
-    enc = q(torch.cat([uncond[0], cond[0]], 0).float())
-    pooled = torch.cat([uncond[1], cond[1]], 0)
-    tids = time_ids.float().reshape(1, -1).repeat(2 * B, 1)
+    enc = q(torch.cat([uncond[0], cond[0]], 0).float().to(dev))
+    pooled = torch.cat([uncond[1], cond[1]], 0).to(dev)
+    tids = time_ids.float().reshape(1, -1).repeat(2 * B, 1).to(dev)
     n = num_steps if steps is None else steps
     for i in range(n):
         x = pack(lat, 1.0 / math.sqrt(float(sigmas[i]) ** 2 + 1.0))
         x = torch.cat([x, x], 0)
-        emb = embed(P, cfg, ts[i:i + 1].float().expand(2 * B), pooled, tids)
+        emb = embed(P, cfg, ts[i:i + 1].float().to(dev).expand(2 * B), pooled, tids)
         noise = unet_forward_tokens(P, cfg, x, 2 * B, Fr, h, w, emb, enc.reshape(-1, enc.shape[-1]), lora)
         rows = B * Fr * h * w
         u, c = noise[:rows], noise[rows:]

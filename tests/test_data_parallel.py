@@ -203,7 +203,10 @@ def _dp_gpu_worker(rank, world, port, q, config="tiny"):
             info = (f"loss_mse dp {lm:.6f} single {l1:.6f}; orth {float(out['loss_orth']):.4e} vs "
                     f"{float(out1['loss_orth']):.4e}; grad_norm {float(out['grad_norm']):.4e} vs "
                     f"{float(out1['grad_norm']):.4e}; worst grad {worst} rel {errs[worst]:.2e} over {len(errs)}")
-            ok = (abs(lm - l1) <= 1e-3 * abs(l1) and errs[worst] < 2e-2 and float(out1["loss_orth"]) > 0
+            # SDXL: the two ranks' B=1 backward and the B=2 backward round differently in bf16 through the 70-block
+            # spatial stack (each is ~4e-2 from fp32, test_training_gpu.py), so 5e-2; tiny: 2e-2
+            ok = (abs(lm - l1) <= 1e-3 * abs(l1) and errs[worst] < (5e-2 if sdxl else 2e-2)
+                  and float(out1["loss_orth"]) > 0
                   and abs(float(out["loss_orth"]) - float(out1["loss_orth"])) <= 1e-5 * float(out1["loss_orth"]))
             q.put((rank, "ok" if ok else "fail", info))
         else:

@@ -73,7 +73,7 @@ class _Recorder:
     def __enter__(self):
         U = self.U
         rec, names = self.rec, self.names
-        for cls in (U.ResnetBlock2D, U.Transformer2DModel, U.MotionModule):
+        for cls in (U.ResnetBlock2D, U.Transformer2DModel, U.MotionModule, U.BasicTransformerBlock):
             self.saved[cls] = cls.run
 
         def res_run(mod, x1, nimg, H, W, ctx, x2=None, _orig=self.saved[U.ResnetBlock2D]):
@@ -94,7 +94,14 @@ class _Recorder:
             rec.append(("motion", names[id(mod)], dict(x=x.float().cpu(), nclip=nimg // ctx.F, F=ctx.F, HW=H * W),
                         y.float().cpu()))
             return y
+        def blk_run(mod, x, nimg, N, ctx, _orig=self.saved[U.BasicTransformerBlock]):
+            y = _orig(mod, x, nimg, N, ctx)
+            if not mod.temporal:  # the motion module's block is covered by the motion-module replay
+                rec.append(("block", names[id(mod)], dict(x=x.float().cpu(), nimg=nimg, N=N, F=ctx.F,
+                            enc=ctx.enc.float().cpu(), heads=mod.attn1.heads), y.float().cpu()))
+            return y
         U.ResnetBlock2D.run, U.Transformer2DModel.run, U.MotionModule.run = res_run, t2d_run, mm_run
+        U.BasicTransformerBlock.run = blk_run
         return self
 
     def __exit__(self, *a):
@@ -117,7 +124,7 @@ def _floor(fn, out=None):
 
 
 def log(msg):
-    print(msg, flush=True)
+    print(f"{time.strftime('%H:%M:%S')} {msg}", flush=True)
 
 
 def _replay(P, kind, name, a, lora):
@@ -127,7 +134,26 @@ def _replay(P, kind, name, a, lora):
     if kind == "transformer2d":
         enc = a["enc"].reshape(-1, a["enc"].shape[-1])
         return E.transformer2d(P, name, a["x"], a["nimg"], a["HW"], enc, a["F"], a["heads"], a["layers"], lora)
+    if kind == "block":
+        enc = a["enc"].reshape(-1, a["enc"].shape[-1])
+        return E.basic_block_spatial(P, name, a["x"], a["nimg"], a["N"], enc, a["F"], a["heads"], lora)
     return E.motion_module(P, name, a["x"], a["nclip"], a["F"], a["HW"])
+
+
+def _on(dev, tree):
+    """Move a param dict / record dict to `dev` (the emulation then runs as torch fp32 ops on that device)."""
+    return {k: (v.to(dev) if isinstance(v, torch.Tensor) else v) for k, v in tree.items()}
+
+
+@pytest.fixture(scope="module")
+def exact_fp32():
+    """The emulation and the fp32 oracle run as torch ops on the GPU for the SDXL-size comparisons (the same
+    restatement, minutes faster than the host CPU): keep torch's fp32 matmuls / convolutions at full fp32."""
+    saved = torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+    yield
+    torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32 = saved
 
 
 @pytest.fixture(scope="module")
@@ -139,67 +165,122 @@ def sdxl_r8(cuda):
     return cfg, unet, _params(unet)
 
 
-def test_configs2_sdxl_f16_per_layer(cuda, sdxl_r8):
+def test_configs2_sdxl_f16_per_layer(cuda, sdxl_r8, exact_fp32):
     """configs[2]: 16 frames, 64x64 latent, UnZipLoRA r=8 (one CFG branch, B=1).  Every ResnetBlock2D /
-    Transformer2DModel / motion module (43 layers) of the HIP forward replayed through the emulation on its own bf16
-    input.  (The chained end-to-end comparison at F=16 is test_configs1; the fp32 oracle at SDXL scale is
-    test_parity_gpu.py::test_unet_forward_sdxl_architecture_vs_oracle.)"""
+    Transformer2DModel / motion module (43 layers) AND every spatial BasicTransformerBlock (70 blocks, so a 10-block
+    Transformer2DModel is not gated at a 10-block stack's floor) of the HIP forward, replayed through the emulation
+    on its own bf16 input.  A layer passes when rel_l2 <= max(1e-3, 3 x the reassociation floor of the first layer of
+    its kind and width that exceeds 1e-3).  (The chained comparisons are test_configs2_sdxl_f16_lora_chained and
+    test_configs1; the fp32 oracle at SDXL scale is test_parity_gpu.py::test_unet_forward_sdxl_architecture_vs_oracle.)"""
     from oracle import unet as O
     cfg, unet, P = sdxl_r8
-    torch.set_num_threads(THREADS)
     lat, enc, pooled, tids = _inputs(cfg, 1, 16, 64, 31)
     t = torch.tensor([601.0])
     kw = dict(added_cond_kwargs={"text_embeds": pooled.to(cuda), "time_ids": tids.to(cuda)})
     with _Recorder(unet) as R:
         out = unet(lat.to(cuda), t.to(cuda), enc.to(cuda), **kw).sample.float().cpu()
-    kinds = {"resnet": 17, "transformer2d": 11, "motion": 15}
+    kinds = {"resnet": 17, "transformer2d": 11, "motion": 15, "block": 70}
     assert {k: sum(1 for r in R.rec if r[0] == k) for k in kinds} == kinds
+    Pd = _on(cuda, P)
     worst = {}
     fails = []
     floors = {}  # (kind, C): reassociation floor of the first layer of that kind and width above 1e-3
     t0 = time.time()
     with torch.no_grad():
         for kind, name, a, y in R.rec:
-            ref = _replay(P, kind, name, a, O.LoRAState())
+            ad = _on(cuda, a)
+            ref = _replay(Pd, kind, name, ad, O.LoRAState())
             e2, em = rel(y, ref)
             key = (kind, y.shape[1])
             if e2 > 1e-3 and key not in floors:
-                floors[key] = _floor(lambda: _replay(P, kind, name, a, O.LoRAState()), y)[1]
+                floors[key] = _floor(lambda: _replay(Pd, kind, name, ad, O.LoRAState()), y)[1]
             floor = floors.get(key) if e2 > 1e-3 else None
-            log(f"[bf16-parity] layer {name:42s} rel_l2={e2:.2e} rel_max={em:.2e}"
+            log(f"[bf16-parity] {kind:13s} {name:58s} rel_l2={e2:.2e} rel_max={em:.2e}"
                 + ("" if floor is None else f" floor({kind}, C={key[1]})={floor:.2e}"))
             w = worst.setdefault(kind, [0.0, 0.0])
             w[0], w[1] = max(w[0], e2), max(w[1], em)
             if e2 > max(1e-3, 3 * (floor or 0.0)) or em > 1.6e-2:
                 fails.append((name, e2, em, floor))
-    log(f"[bf16-parity] configs[2] per-layer worst {worst} (replay {time.time() - t0:.0f}s)")
+    log(f"[bf16-parity] configs[2] per-layer worst {worst}; floors {floors} (replay {time.time() - t0:.0f}s)")
     assert not fails, fails
 
 
-def test_configs1_sdxl_f16_no_lora_chained(cuda):
-    """configs[1]: the same clip without UnZipLoRA (plain SDXL + motion modules)."""
+def test_configs2_sdxl_f16_lora_chained(cuda, sdxl_r8, exact_fp32):
+    """configs[2] end to end: the whole F=16, 64x64 forward with UnZipLoRA r=8 on all 560 spatial projections, HIP
+    vs the bf16 emulation of the same forward, and vs the fp32 oracle (both run as torch ops on the GPU), on the
+    conditioned synthetic init.  Each of the 113 layers sits at its own reassociation floor (~2-4e-3 per block,
+    test_configs2_sdxl_f16_per_layer); chained, those one-ulp flips accumulate to the emulation's own reassociation
+    floor (measured here: the emulation re-run with another fp32 summation order, ~1.7e-2 on this init).  Gate:
+    within 1.5x that floor, and 3e-2 absolute."""
+    from oracle import unet as O
+    from oracle import unet_bf16 as E
+    cfg, unet, P = sdxl_r8
+    lat, enc, pooled, tids = _inputs(cfg, 1, 16, 64, 34)
+    t = torch.tensor([401.0])
+    out = unet(lat.to(cuda), t.to(cuda), enc.to(cuda), added_cond_kwargs={"text_embeds": pooled.to(cuda),
+                                                                         "time_ids": tids.to(cuda)}).sample
+    Pd = _on(cuda, P)
+    args = (lat.to(cuda), t, enc.to(cuda), pooled.to(cuda), tids.to(cuda))
+    with torch.no_grad():
+        ref_bf, floor = _floor(lambda: E.unet_forward(Pd, cfg.to_dict(), *args), out)
+        ref32 = O.unet_forward(Pd, cfg.to_dict(), *args)
+    e2, em = _report("configs[2] SDXL F=16 64x64 UnZipLoRA r=8 chained", out, ref_bf, ref32)
+    log(f"[bf16-parity] configs[2] chained reassociation floor {floor:.2e}")
+    assert e2 <= min(3e-2, max(3e-3, 1.5 * floor)) and em <= 4e-2
+
+
+def test_denoise_50_steps_sdxl_f16_64(cuda, sdxl_r8, exact_fp32):
+    """north_star's "max rel-err vs reference latents" on the production loop: the 50-step CFG (7.5) Euler loop of a
+    16-frame 512^2 clip (64x64 latent) with UnZipLoRA r=8, through the captured HIP graph, against the fp32 oracle's
+    loop (torch fp32 ops on the GPU; 100 UNet forwards), conditioned synthetic init.  Reports rel-L2 and max rel-err
+    (max |d| / max |ref|) of the final latents.  (The bf16-emulation loop with its floor probe is the tiny-config
+    test below; at this size it would take ~10 minutes.)"""
+    from oracle import unet as O
+    from video_style_transfer_amd.pipeline import AnimateDiffDenoiser
+    cfg, unet, P = sdxl_r8
+    _, enc, pooled, tids = _inputs(cfg, 2, 1, 64, 35)
+    den = AnimateDiffDenoiser(unet, 16, 512, 512, num_inference_steps=50, guidance_scale=7.5, device=cuda)
+    den.set_prompt_embeds(enc[1:2], pooled[1:2], enc[0:1], pooled[0:1])
+    lat0 = torch.randn(1, 4, 16, 64, 64, generator=torch.Generator().manual_seed(42)) * den.scheduler.init_noise_sigma
+    den.set_latents(lat0)
+    out = den.run_steps(50).float().cpu()
+    del den
+    torch.cuda.empty_cache()
+    Pd = _on(cuda, P)
+    cond, unc = (enc[1:2].to(cuda), pooled[1:2].to(cuda)), (enc[0:1].to(cuda), pooled[0:1].to(cuda))
+    t0 = time.time()
+    with torch.no_grad():
+        ref32 = O.denoise(Pd, cfg.to_dict(), lat0.to(cuda), cond, unc, tids[:1].to(cuda), 50, 7.5).cpu()
+    f2, fm = rel(out, ref32)
+    log(f"[bf16-parity] denoise 50 steps SDXL F=16 64x64 UnZipLoRA r=8 (graph) vs fp32 oracle loop: rel_l2={f2:.2e} "
+        f"max rel-err={fm:.2e} (oracle loop {time.time() - t0:.0f}s)")
+    assert f2 <= 3e-2 and fm <= 5e-2
+
+
+def test_configs1_sdxl_f16_no_lora_chained(cuda, exact_fp32):
+    """configs[1]: the same clip without UnZipLoRA (plain SDXL + motion modules); emulation on the GPU's torch."""
     from oracle import unet as O
     from oracle import unet_bf16 as E
     from video_style_transfer_amd.config import UNetMotionConfig
     from video_style_transfer_amd.utils import build_unet
     cfg = UNetMotionConfig.sdxl()
     unet = build_unet(cfg, seed=22, lora_rank=None, device=cuda)
-    P = _params(unet)
+    P = _on(cuda, _params(unet))
     assert not any("lora" in k for k in P)
-    torch.set_num_threads(THREADS)
     lat, enc, pooled, tids = _inputs(cfg, 1, 16, 64, 32)
     t = torch.tensor([301.0])
     out = unet(lat.to(cuda), t.to(cuda), enc.to(cuda), added_cond_kwargs={"text_embeds": pooled.to(cuda),
                                                                          "time_ids": tids.to(cuda)}).sample
-    log("[bf16-parity] configs[1]: emulating the whole forward (+ reassociation probe) on the CPU ...")
+    args = (lat.to(cuda), t, enc.to(cuda), pooled.to(cuda), tids.to(cuda))
     with torch.no_grad():
-        ref_bf, floor = _floor(lambda: E.unet_forward(P, cfg.to_dict(), lat, t, enc, pooled, tids), out)
-    e2, em = _report("configs[1] SDXL F=16 64x64 no LoRA chained", out, ref_bf)
+        ref_bf, floor = _floor(lambda: E.unet_forward(P, cfg.to_dict(), *args), out)
+        ref32 = O.unet_forward(P, cfg.to_dict(), *args)
+    e2, em = _report("configs[1] SDXL F=16 64x64 no LoRA chained", out, ref_bf, ref32)
     log(f"[bf16-parity] configs[1] chained reassociation floor {floor:.2e}")
-    assert e2 <= max(5e-3, 3 * floor) and em <= 5e-2
+    assert e2 <= min(3e-2, max(3e-3, 1.5 * floor)) and em <= 4e-2
 
 
-def test_configs0_sdxl_image_unet_f1(cuda):
+def test_configs0_sdxl_image_unet_f1(cuda, exact_fp32):
     """configs[0]: the SDXL UNet2DConditionModel (animatediff/utils.py:20) -- no motion modules, no LoRA -- on one
     frame per sample; "256x256" read as 256x256 pixels = a 32x32 latent (SDXL's VAE factor 8).
     CFG batch 2."""
@@ -216,9 +297,12 @@ def test_configs0_sdxl_image_unet_f1(cuda):
     t = torch.tensor([901.0, 901.0])
     out = unet(lat.to(cuda), t.to(cuda), enc.to(cuda), added_cond_kwargs={"text_embeds": pooled.to(cuda),
                                                                          "time_ids": tids.to(cuda)}).sample
-    log("[bf16-parity] configs[0]: emulation, probe and fp32 oracle on the CPU ...")
+    log("[bf16-parity] configs[0]: emulation and probe (GPU torch), fp32 oracle CPU eager ...")
+    Pd = _on(cuda, P)
     with torch.no_grad():
-        ref_bf, floor = _floor(lambda: E.unet_forward(P, cfg.to_dict(), lat, t, enc, pooled, tids), out)
+        ref_bf, floor = _floor(lambda: E.unet_forward(Pd, cfg.to_dict(), lat.to(cuda), t, enc.to(cuda),
+                                                      pooled.to(cuda), tids.to(cuda)), out)
+        del Pd
         t0 = time.perf_counter()
         ref32 = O.unet_forward(P, cfg.to_dict(), lat, t, enc, pooled, tids)
         cpu_s = time.perf_counter() - t0
@@ -236,7 +320,40 @@ def test_configs0_sdxl_image_unet_f1(cuda):
         f"threads of {cpu_model}; HIP eager forward {gpu_s * 1e3:.1f} ms")
     e2, em = _report("configs[0] SDXL image UNet F=1 32x32", out, ref_bf, ref32)
     log(f"[bf16-parity] configs[0] reassociation floor {floor:.2e}")
-    assert e2 <= max(5e-3, 3 * floor) and em <= 5e-2
+    assert e2 <= max(3e-3, 3 * floor) and em <= 2e-2
+
+
+def test_configs0_sdxl_image_unet_256_latent(cuda, exact_fp32):
+    """configs[0] read literally: "Single 256x256 latent" = a 256x256 LATENT (2048^2 px; 35.9 TF per forward), one
+    sample, the SDXL UNet2DConditionModel (no motion modules, no LoRA).  The level-1 self-attention runs over 16384
+    tokens.  HIP vs the bf16 emulation and the fp32 oracle (torch on the GPU; the emulation's 16384-key online
+    softmax is the kernel's tile order).  The CPU-eager fp32 timing of this forward is tools/config0_cpu_eager.py
+    (profiles/r3_config0_256_cpu_eager.log): about a minute of host time, kept out of the test suite."""
+    from oracle import unet as O
+    from oracle import unet_bf16 as E
+    from video_style_transfer_amd.config import UNetMotionConfig
+    from video_style_transfer_amd.utils import build_unet
+    cfg = UNetMotionConfig.sdxl_image()
+    unet = build_unet(cfg, seed=24, lora_rank=None, device=cuda)
+    lat, enc, pooled, tids = _inputs(cfg, 1, 1, 256, 36)
+    t = torch.tensor([901.0])
+    kw = dict(added_cond_kwargs={"text_embeds": pooled.to(cuda), "time_ids": tids.to(cuda)})
+    out = unet(lat.to(cuda), t.to(cuda), enc.to(cuda), **kw).sample
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    unet(lat.to(cuda), t.to(cuda), enc.to(cuda), **kw)
+    torch.cuda.synchronize()
+    gpu_ms = (time.perf_counter() - t0) * 1e3
+    P = _on(cuda, _params(unet))
+    del unet
+    torch.cuda.empty_cache()
+    args = (lat.to(cuda), t, enc.to(cuda), pooled.to(cuda), tids.to(cuda))
+    with torch.no_grad():
+        ref_bf = E.unet_forward(P, cfg.to_dict(), *args)
+        ref32 = O.unet_forward(P, cfg.to_dict(), *args)
+    log(f"[bf16-parity] configs[0] 256x256 latent: HIP eager forward {gpu_ms:.1f} ms")
+    e2, em = _report("configs[0] SDXL image UNet F=1 256x256 latent", out, ref_bf, ref32)
+    assert e2 <= 5e-3 and em <= 2e-2
 
 
 def test_denoise_50_steps_vs_bf16_emulation(cuda):

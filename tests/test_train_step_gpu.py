@@ -1,13 +1,11 @@
 """The configs[4] training step on the HIP path (train_animatediff.py:212-319): the captured HIP-graph step against
 the eager step, gradient accumulation and the lr schedule through the graphs, and the production-size step.
 
-  * tiny config, gradient_accumulation_steps 2, the reference's cosine-with-warm-up schedule: an eager TrainStep with
-    a plain (non-capturable) AdamW and a float lr -- the reference's optimizer -- against TrainStep.capture + replays
-    with a device-tensor lr on an identical model, for 8 calls (4 optimizer steps): loss and grad norm per call, and
-    every trainable parameter after every call.  Also: capture refuses a float lr with a scheduler, and capturing
-    changes no training state.
+  * tiny config, gradient_accumulation_steps 2, the reference's cosine-with-warm-up schedule: TrainStep.capture +
+    replays against the eager TrainStep (bit for bit, every call) and against the reference's float-lr AdamW (update
+    sizes, fp32 weights).  Also: capture refuses a float lr with a scheduler, and capturing changes no training state.
   * SDXL architecture at BASELINE configs[4]'s size (16 x 512^2 clip, UnZipLoRA r=8 frozen, temporal LoRA r=32,
-    orth loss 1e-4, clip 0.5, AdamW 2e-5): the captured step equals the eager step on the same draws.
+    orth loss 1e-4, clip 0.5, AdamW 2e-5): the captured step equals the eager step on the same draws, bit for bit.
 """
 import pytest
 import torch
@@ -51,75 +49,88 @@ def _text(cfg, seed=5):
 
 
 def test_train_step_graph_equals_eager_accumulation_and_schedule(cuda):
+    """Three identical tiny models, 8 calls (4 optimizer steps), gradient_accumulation_steps 2, the reference's
+    cosine schedule (warm-up 2 of 6 optimizer steps, so the lr changes at every step, from 0):
+      E  eager TrainStep, AdamW with the device-tensor lr (make_adamw(capturable=True));
+      G  the same, captured (TrainStep.capture) and replayed -- must equal E bit for bit after every call: loss, grad
+         norm, every trainable weight (so accumulation, the sync / no_sync graphs, zeroing and the lr tensor written by
+         the scheduler all behave as the eager code);
+      R  eager with the reference's optimizer (torch.optim.AdamW, float lr, foreach): its updates have the same size
+         at every step (the schedule reached the graph), its fp32 weights (temporal LoRA) agree to 1e-5; its bf16
+         weights differ where torch's two AdamW formulations round their bf16 moments differently."""
     from video_style_transfer_amd.config import UNetMotionConfig
     from video_style_transfer_amd.scheduler import EulerDiscreteScheduler
     from video_style_transfer_amd.train import TrainStep, get_scheduler, make_adamw
     cfg = UNetMotionConfig.tiny()
     accum, calls, lr = 2, 8, 1e-3
-    ue, index_e = _model(cfg, cuda, 8, 4)
-    ug, index_g = _model(cfg, cuda, 8, 4)
-    pe = [p for p in ue.parameters() if p.requires_grad]
-    pg = [p for p in ug.parameters() if p.requires_grad]
-    for a, b in zip(pe, pg):
-        assert torch.equal(a, b)
+    models = [_model(cfg, cuda, 8, 4) for _ in range(3)]
+    (ue, ie), (ug, ig), (ur, ir) = models
+    pe, pg, pr = ([p for p in u.parameters() if p.requires_grad] for u, _ in models)
+    for a, b, c in zip(pe, pg, pr):
+        assert torch.equal(a, b) and torch.equal(a, c)
     enc, pooled, unc, unp = _text(cfg)
     lat = [torch.randn(1, 4, 4, 8, 8, generator=torch.Generator().manual_seed(10 + i)).to(cuda) for i in range(calls)]
     kw = dict(lambda_orth=1e-2, max_grad_norm=0.5, resolution=64, seed=9, gradient_accumulation_steps=accum)
+    adam = dict(lr=lr, betas=(0.9, 0.999), weight_decay=1e-2, eps=1e-8)
 
-    # eager = the reference's optimizer: AdamW(float lr), non-capturable; cosine, warm-up 2 of 6 optimizer steps
-    opt_e = torch.optim.AdamW(pe, lr=lr, betas=(0.9, 0.999), weight_decay=1e-2, eps=1e-8)
-    step_e = TrainStep(ue, opt_e, EulerDiscreteScheduler(), spatial_index=index_e,
-                       lr_scheduler=get_scheduler("cosine", opt_e, 2, 6), **kw)
+    def make(u, idx, opt):
+        return TrainStep(u, opt, EulerDiscreteScheduler(), spatial_index=idx,
+                         lr_scheduler=get_scheduler("cosine", opt, 2, 6), **kw), opt
 
-    # graph: a float lr with a scheduler must be refused (it would be baked into the captured AdamW)
+    step_e, opt_e = make(ue, ie, make_adamw(pe, capturable=True, **adam))
+    step_r, opt_r = make(ur, ir, torch.optim.AdamW(pr, **adam))
+
+    # a float lr with a scheduler must be refused by capture (it would be baked into the captured AdamW)
     bad = torch.optim.AdamW(pg, lr=lr, capturable=True)
     with pytest.raises(ValueError):
-        TrainStep(ug, bad, EulerDiscreteScheduler(), spatial_index=index_g, lr_scheduler=get_scheduler("cosine", bad, 2, 6),
-                  **kw).capture(lat[0], enc, pooled)
+        make(ug, ig, bad)[0].capture(lat[0], enc, pooled)
     for p in pg:
         p.grad = None
-    opt_g = make_adamw(pg, lr=lr, betas=(0.9, 0.999), weight_decay=1e-2, eps=1e-8, capturable=True)
-    step_g = TrainStep(ug, opt_g, EulerDiscreteScheduler(), spatial_index=index_g,
-                       lr_scheduler=get_scheduler("cosine", opt_g, 2, 6), **kw)
+    step_g, opt_g = make(ug, ig, make_adamw(pg, capturable=True, **adam))
     snap = [p.detach().clone() for p in pg]
     step_g.capture(lat[0], enc, pooled, uncond_prompt=unc, uncond_pooled=unp)
-    # capturing (two eager warm-up windows with optimizer steps) left the weights and the draws untouched
+    # capturing (two eager warm-up windows with optimizer steps) left the weights, the optimizer and the draws as
+    # they were
     for a, b in zip(pg, snap):
         assert torch.equal(a, b)
     assert step_g.graph_micro is not None and step_g.micro == 0
+    assert all(float(opt_g.state[p]["step"]) == 0 and not opt_g.state[p]["exp_avg"].any() for p in pg)
 
-    prev_e = [p.detach().clone() for p in pe]
+    prev_r = [p.detach().clone() for p in pr]
     prev_g = [p.detach().clone() for p in pg]
     for i in range(calls):
         oe = step_e(lat[i], enc, pooled, unc, unp)
+        orr = step_r(lat[i], enc, pooled, unc, unp)
         og = step_g.replay(lat[i])
         torch.cuda.synchronize()
-        assert oe["sync"] == og["sync"] == (i % accum == accum - 1)
+        assert oe["sync"] == og["sync"] == orr["sync"] == (i % accum == accum - 1)
         assert oe["uncond"] == og["uncond"] and torch.equal(oe["timesteps"], og["timesteps"])
-        le, lg = float(oe["loss"]), float(og["loss"])
-        assert abs(le - lg) <= 1e-3 * abs(le), (i, le, lg)
-        lr_e, lr_g = opt_e.param_groups[0]["lr"], float(opt_g.param_groups[0]["lr"])
-        assert lr_g == pytest.approx(lr_e, rel=1e-6, abs=1e-12), (i, lr_e, lr_g)
+        assert float(oe["loss"]) == float(og["loss"]), i
+        lr_e, lr_g, lr_r = float(opt_e.param_groups[0]["lr"]), float(opt_g.param_groups[0]["lr"]), \
+            opt_r.param_groups[0]["lr"]
+        assert lr_g == lr_e and lr_g == pytest.approx(lr_r, rel=1e-6, abs=1e-12), (i, lr_e, lr_g, lr_r)
+        for a, b in zip(pe, pg):
+            assert torch.equal(a, b), f"call {i}: captured step differs from the eager step"
         if og["sync"]:
-            ge, gg = float(oe["grad_norm"]), float(og["grad_norm"])
-            assert abs(ge - gg) <= 1e-2 * ge, (i, ge, gg)
-            de = torch.cat([(p.detach() - q).float().flatten() for p, q in zip(pe, prev_e)])
+            assert float(oe["grad_norm"]) == float(og["grad_norm"])
+            dr = torch.cat([(p.detach() - q).float().flatten() for p, q in zip(pr, prev_r)])
             dg = torch.cat([(p.detach() - q).float().flatten() for p, q in zip(pg, prev_g)])
             if i == accum - 1:  # the first optimizer step runs at warm-up lr 0: no parameter moves on either path
-                assert de.abs().max() == 0 and dg.abs().max() == 0
+                assert dr.abs().max() == 0 and dg.abs().max() == 0
             else:
-                e = rel(dg, de)
-                print(f"[train-graph] call {i}: lr {lr_e:.3e} loss {le:.5f}/{lg:.5f} gnorm {ge:.4e}/{gg:.4e} "
-                      f"|update| {de.norm():.3e}/{dg.norm():.3e} rel {e:.2e}")
-                assert de.norm() > 0 and e < 5e-2, (i, e)
-            prev_e = [p.detach().clone() for p in pe]
+                f32 = [(a, b) for a, b in zip(pg, pr) if a.dtype == torch.float32]
+                e32 = max(((a - b).abs().max() / b.abs().max()).item() for a, b in f32)
+                print(f"[train-graph] call {i}: lr {lr_g:.3e} loss {float(og['loss']):.5f} gnorm "
+                      f"{float(og['grad_norm']):.4e} |update| graph {dg.norm():.3e} reference AdamW {dr.norm():.3e}; "
+                      f"fp32 weights vs reference AdamW {e32:.1e}")
+                assert dr.norm() > 0 and abs(dg.norm() / dr.norm() - 1) < 2e-2, i
+                assert e32 < 1e-5, i
+            prev_r = [p.detach().clone() for p in pr]
             prev_g = [p.detach().clone() for p in pg]
         else:
             assert torch.isnan(og["grad_norm"])
             for p, q in zip(pg, prev_g):  # an accumulation call never touches the weights
                 assert torch.equal(p, q)
-    for p, q in zip(pe, pg):
-        assert rel(q, p) < 1e-2
 
 
 def test_train_step_sdxl_16x512_graph_equals_eager(cuda):
@@ -138,7 +149,7 @@ def test_train_step_sdxl_16x512_graph_equals_eager(cuda):
     kw = dict(lambda_orth=1e-4, spatial_index=index, max_grad_norm=0.5, resolution=512, seed=11)
     snap = [p.detach().clone() for p in params]
 
-    opt_e = torch.optim.AdamW(params, lr=2e-5, betas=(0.9, 0.999), weight_decay=1e-2, eps=1e-8)
+    opt_e = make_adamw(params, lr=2e-5, capturable=True)
     oe = TrainStep(unet, opt_e, EulerDiscreteScheduler(), **kw)(lat, enc, pooled, unc, unp)
     torch.cuda.synchronize()
     de = [(p.detach() - q).float() for p, q in zip(params, snap)]
@@ -157,12 +168,12 @@ def test_train_step_sdxl_16x512_graph_equals_eager(cuda):
     torch.cuda.synchronize()
     lg, gg = float(og["loss"]), float(og["grad_norm"])
     dg = [(p.detach() - q).float() for p, q in zip(params, snap)]
-    e_upd = rel(torch.cat([d.flatten() for d in dg]), torch.cat([d.flatten() for d in de]))
-    worst = max(range(len(params)), key=lambda i: rel(dg[i], de[i]) if de[i].norm() > 0 else 0.0)
+    ne = torch.cat([d.flatten() for d in de]).norm()
+    ng = torch.cat([d.flatten() for d in dg]).norm()
     print(f"[train-sdxl] loss eager {le:.6f} graph {lg:.6f} (orth {lo:.3e}); grad_norm {ge:.5e} / {gg:.5e}; "
-          f"update rel_l2 {e_upd:.2e}, worst tensor {rel(dg[worst], de[worst]):.2e}; "
-          f"peak {torch.cuda.max_memory_allocated() / 2 ** 30:.1f} GiB")
+          f"|update| {ne:.4e} / {ng:.4e}; peak {torch.cuda.max_memory_allocated() / 2 ** 30:.1f} GiB")
     assert torch.isfinite(og["loss"]) and torch.isfinite(og["grad_norm"]) and lo > 0
     assert oe["timesteps"].tolist() == og["timesteps"].tolist() and oe["uncond"] == og["uncond"]
-    assert abs(le - lg) <= 1e-4 * abs(le) and abs(ge - gg) <= 1e-3 * ge
-    assert e_upd < 1e-2
+    assert le == lg and ge == gg  # same kernels on the same inputs: bitwise-equal loss and gradient norm
+    for p, q, d in zip(params, snap, de):  # same kernels, same AdamW: the captured step IS the eager step
+        assert torch.equal(p.detach().float() - q.float(), d)
