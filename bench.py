@@ -289,6 +289,70 @@ def _cpu_model():
     return None
 
 
+# Sharded vs unsharded differ only by fp32 summation orders (per-rank GEMM tile / split choices at the smaller row
+# counts, GroupNorm sums merged across ranks); through the whole UNet those one-ulp flips reach ~1e-2 rel-L2 (the
+# chained reassociation floors of tests/test_parity_bf16_gpu.py; 1.3e-2 in the two-rank rehearsal).  A layout or
+# exchange error is O(1).
+PREFLIGHT_TOL = 0.1
+
+
+def _gather0(t, world, rank):
+    """All ranks' equal-shaped tensors -> list on rank 0 (None elsewhere); staged through host memory on gloo."""
+    import torch.distributed as dist
+    staged = str(dist.get_backend()).lower() != "nccl"
+    src = t.cpu() if staged else t.contiguous()
+    parts = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(parts, src)
+    return [p.to(t.device) for p in parts] if rank == 0 else None
+
+
+def shard_preflight(den, unet, world, rank):
+    """Before any timing of a frame-sharded N-GPU run: one eager sharded UNet forward of the step's CFG-batched
+    input (the collectives included), clip 0's noise prediction gathered to rank 0 and compared with rank 0's
+    unsharded forward of the whole clip.  The only differences allowed are fp32 summation orders (the clip-wide
+    GroupNorm sums of the motion modules are merged across ranks), so a layout or exchange error shows up as O(1).
+    Returns {"rel_l2", "rel_max"} on rank 0 (None elsewhere); the run fails on a mismatch."""
+    from video_style_transfer_amd import kernels as K
+    n, F, h, w = den.nclips, den.F, den.h, den.w
+    B = den.ncopy * n
+    den.step_idx.zero_()
+    K.pack_latents(den.lat, den.x, sigmas=den.sigmas, step_idx=den.step_idx, ncopy=den.ncopy)
+    emb = unet.embed(den.timesteps, den.pooled, den.time_ids, B, step_idx=den.step_idx)
+    with torch.no_grad():
+        noise = unet.forward_tokens(den.x, B, F, h, w, emb, den.enc, shard=den.shard)  # rows (b, f_local, p)
+    rows = F * h * w
+    pick = [0, n] if den.ncopy == 2 else [0]                                            # clip 0, both CFG copies
+    mine = torch.cat([noise[b * rows:(b + 1) * rows] for b in pick])                     # (copy, f_local, p)
+    parts = _gather0(mine, world, rank)
+    lat_parts = _gather0(den.lat[:1].contiguous(), world, rank)                          # clip 0, local frames
+    out = None
+    if rank == 0:
+        Cl = den.lat.shape[1]
+        got = torch.stack([p.view(len(pick), F, h * w, -1) for p in parts], 1)          # (copy, rank, f_local, p)
+        got = got.reshape(len(pick) * world * rows, -1)
+        lat_full = torch.cat(lat_parts, 2)                                               # (1, C, F_total, h, w)
+        x = torch.empty(len(pick) * world * rows, Cl, dtype=torch.bfloat16, device=den.x.device)
+        K.pack_latents(lat_full.repeat(len(pick), 1, 1, 1, 1).contiguous(), x, sigmas=den.sigmas,
+                       step_idx=den.step_idx, ncopy=1)
+        with torch.no_grad():
+            ref = unet.forward_tokens(x, len(pick), F * world, h, w, emb[pick].contiguous(),
+                                      den.enc[pick].contiguous())
+        e2 = ((got.float() - ref.float()).norm() / ref.float().norm()).item()
+        em = ((got.float() - ref.float()).abs().max() / ref.float().abs().max()).item()
+        out = {"rel_l2": round(e2, 6), "rel_max": round(em, 6),
+               "what": f"clip 0 (CFG pair) noise prediction, {world}-way frame-sharded eager forward vs rank 0's "
+                       f"unsharded forward of all {F * world} frames"}
+        if not (e2 <= PREFLIGHT_TOL and torch.isfinite(got.float()).all()):
+            print(json.dumps({"preflight_failed": out}), file=sys.stderr)
+    import torch.distributed as dist
+    bad = torch.tensor([0 if rank != 0 or out["rel_l2"] <= PREFLIGHT_TOL else 1], dtype=torch.int32)
+    bad = bad if str(dist.get_backend()).lower() != "nccl" else bad.to(den.x.device)
+    dist.all_reduce(bad)
+    if int(bad.item()):
+        raise SystemExit(3)
+    return out
+
+
 def bench_train(args, world, rank, local, dev):
     """BASELINE configs[4] (train_animatediff.py:212-319): SDXL UNet + AnimateDiff-SDXL motion modules (synthetic
     weights), UnZipLoRA r=8 frozen on all spatial projections, temporal LoRA r=32 injected, freeze_spatial_layers,
@@ -461,6 +525,7 @@ def main():
     den.set_prompt_embeds(enc[1:], pooled[1:], enc[:1], pooled[:1])
     den.init_latents(seed=42 + seed_rank)
     graph_note = None
+    preflight = shard_preflight(den, unet, world, rank) if shard is not None else None
     if shard is not None and not shard.graph_capturable:
         graph_note = f"{shard.backend} collectives are not graph-capturable; eager steps"
     elif not args.no_graph:
@@ -542,7 +607,7 @@ def main():
                        "graph": graphed, "cfg_streams": cfg_streams,
                        "note": graph_note},
             "roofline": rl, "step_roofline": step, "vae_decode": vae_rec, "cpu_baseline": cpu, "kernels": table,
-            "finite": ok,
+            "finite": ok, "shard_preflight": preflight,
             "setup_s": round(t_build, 1),
         }
         print(json.dumps(out))

@@ -1,0 +1,40 @@
+"""bench.py's N-GPU path rehearsed on one GPU (VERDICT r2 "RCCL readiness"): `torch.distributed.run` with two ranks,
+both on cuda:0 over gloo (VST_BENCH_REHEARSAL=gloo; RCCL cannot put two ranks on one device), frame sharding of every
+clip over the ranks.  Before anything is timed, bench.py runs its shard preflight -- one eager frame-sharded UNet
+forward, clip 0 gathered to rank 0 and compared with rank 0's unsharded forward of the whole clip -- and exits
+non-zero on a mismatch; the JSON line carries the distance.  The driver's 8-GPU run goes through the same code with
+the nccl backend (and the step captured in a HIP graph)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.gpu
+def test_bench_two_rank_frame_shard_rehearsal():
+    if torch.cuda.device_count() == 0:
+        pytest.skip("no HIP device")
+    env = dict(os.environ, VST_BENCH_REHEARSAL="gloo", OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps",
+           "1", "--warmup", "0", "--frames", "16", "--size", "256", "--no-cpu-baseline", "--no-vae", "--no-roofline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    d = json.loads(line)
+    pf = d["shard_preflight"]
+    print(f"[rehearsal] {d['config']['parallelism']}: {d['ms_per_step']} ms/step, preflight {pf}")
+    assert d["n_gpus"] == 2 and d["finite"]
+    assert pf is not None and pf["rel_l2"] <= 2e-2

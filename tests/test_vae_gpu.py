@@ -156,3 +156,20 @@ def test_vae_decode_chunking_is_exact(cuda):
     e2, _ = rel(single, whole)
     print(f"[vae] chunked decode vs whole: 2-frame chunks rel_l2={e1:.2e}, 1-frame {e2:.2e}")
     assert e1 < 2e-3 and e2 < 2e-3
+
+
+def test_vae_layout_wrappers_check_shapes(cuda):
+    """The VAE layout kernels index through n*H*W and the row stride without bounds checks: the wrappers refuse a
+    row count or leading dimension that does not match."""
+    from video_style_transfer_amd import _lib
+    from video_style_transfer_amd import kernels as K
+    x = torch.zeros(2 * 4 * 4, 8, dtype=BF, device=cuda)
+    K.nhwc_to_nchw(x, 2, 3, 4, 4)
+    K.frames_to_u8(x, 2, 3, 4, 4)
+    K.vae_sample(x, 2, 4, 4, None, 1.0)
+    for bad in (lambda: K.nhwc_to_nchw(x, 3, 3, 4, 4), lambda: K.nhwc_to_nchw(x, 2, 9, 4, 4),
+                lambda: K.frames_to_u8(x[:-1], 2, 3, 4, 4), lambda: K.vae_sample(x[:, :6], 2, 4, 4, None, 1.0),
+                lambda: K.vae_sample(x, 2, 4, 8, None, 1.0),
+                lambda: K.nchw_to_nhwc(torch.zeros(1, 4, 2, 2, device=cuda), ldd=2)):
+        with pytest.raises(_lib.VstError):
+            bad()

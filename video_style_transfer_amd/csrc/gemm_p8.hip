@@ -324,8 +324,16 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) slot[(i * 4 + j) * 512 + tid] = acc[i][j];
-      __syncthreads();  // every wave's stores have reached L2
-      if (tid == 0) __hip_atomic_store(p.sk_flags + w, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      // publish (MI355X_MICROARCH.md, inter-workgroup visibility, producer form): every storing wave waits for its
+      // own stores, the workgroup barrier, then ONE agent-scope release (L2 write-back) by lane 0, its completion
+      // waited for explicitly (the compiler may drop that wait), then the relaxed flag store
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(p.sk_flags + w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       g += ke - kb;
     }
     if (g < g1) {  // owner: k-tiles [0, ke) of this tile, then the later k-ranges from the next workgroups
@@ -337,9 +345,16 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       run_segment(0, ke);
       const int te = (tile + 1) * nk;
       for (int c = w + 1; c < G && start_of(c) < te; ++c) {
-        if (tl == 0)
-          while (__hip_atomic_load(p.sk_flags + c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0)
+        if (tl == 0) {
+          // relaxed poll (bounded, ~1 s: a missing contributor must not hang the GPU), then ONE agent acquire
+          // (invalidates this CU's L1) whose completion the barrier holds every wave behind
+          for (int spin = 0; spin < (1 << 23); ++spin) {
+            if (__hip_atomic_load(p.sk_flags + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
             __builtin_amdgcn_s_sleep(2);
+          }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         __syncthreads();
         const f32x4* slot = reinterpret_cast<const f32x4*>(p.sk_ws + (size_t)c * PSLOT);
 #pragma unroll

@@ -630,6 +630,8 @@ def nchw_to_nhwc(x: torch.Tensor, mul: float = 1.0, ldd: int | None = None) -> t
         raise _lib.VstError("nchw_to_nhwc: x must be a contiguous fp32 (n, C, H, W) device tensor")
     n, C, H, W = x.shape
     ldd = ldd or C
+    if ldd < C:
+        raise _lib.VstError(f"nchw_to_nhwc: ldd {ldd} < C {C}")
     out = torch.empty((n * H * W, ldd), dtype=BF16, device=x.device)
     _lib.call("vst_nchw_to_nhwc", _p(x), n, C, H * W, float(mul), _p(out), ldd, _stream())
     return out
@@ -638,6 +640,8 @@ def nchw_to_nhwc(x: torch.Tensor, mul: float = 1.0, ldd: int | None = None) -> t
 def nhwc_to_nchw(x: torch.Tensor, n: int, C: int, H: int, W: int) -> torch.Tensor:
     """bf16 [n*H*W, >=C] -> fp32 (n, C, H, W)."""
     _dev(x, BF16, "x")
+    if x.shape[0] != n * H * W or _ld(x) < C or x.shape[1] < C:
+        raise _lib.VstError(f"nhwc_to_nchw: x {tuple(x.shape)} (ld {_ld(x)}) vs n*H*W = {n * H * W} rows of >= C channels")
     out = torch.empty((n, C, H, W), dtype=F32, device=x.device)
     _lib.call("vst_nhwc_to_nchw", _p(x), _ld(x), n, C, H * W, _p(out), _stream())
     return out
@@ -646,6 +650,8 @@ def nhwc_to_nchw(x: torch.Tensor, n: int, C: int, H: int, W: int) -> torch.Tenso
 def frames_to_u8(x: torch.Tensor, n: int, C: int, H: int, W: int) -> torch.Tensor:
     """bf16 [n*H*W, >=C] decoder output -> uint8 (n, H, W, C) frames (inference_animatediff.py:141-143)."""
     _dev(x, BF16, "x")
+    if x.shape[0] != n * H * W or _ld(x) < C or x.shape[1] < C:
+        raise _lib.VstError(f"frames_to_u8: x {tuple(x.shape)} (ld {_ld(x)}) vs n*H*W = {n * H * W} rows of >= C channels")
     out = torch.empty((n, H, W, C), dtype=torch.uint8, device=x.device)
     _lib.call("vst_frames_to_u8", _p(x), _ld(x), n, C, H * W, _p(out), _stream())
     return out
@@ -654,6 +660,9 @@ def frames_to_u8(x: torch.Tensor, n: int, C: int, H: int, W: int) -> torch.Tenso
 def vae_sample(moments: torch.Tensor, n: int, H: int, W: int, eps: torch.Tensor | None, mul: float) -> torch.Tensor:
     """moments bf16 [n*H*W, >=8] -> fp32 (n, 4, H, W) = (mean + exp(logvar/2) * eps) * mul (eps None: mean * mul)."""
     _dev(moments, BF16, "moments")
+    if moments.shape[0] != n * H * W or _ld(moments) < 8 or moments.shape[1] < 8:
+        raise _lib.VstError(f"vae_sample: moments {tuple(moments.shape)} vs n*H*W = {n * H * W} rows of >= 8 "
+                            "channels (mean | logvar)")
     if eps is not None and (eps.dtype != F32 or not eps.is_contiguous() or eps.shape != (n, 4, H, W)):
         raise _lib.VstError("vae_sample: eps must be contiguous fp32 (n, 4, H, W)")
     out = torch.empty((n, 4, H, W), dtype=F32, device=moments.device)
