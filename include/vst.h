@@ -99,6 +99,23 @@ int vst_layernorm(const void* x, int ldx, int C, int rows, const float* gamma, c
 int vst_layernorm_lora(const void* x, int ldx, int C, int rows, const float* gamma, const float* beta, float eps,
                        const void* A, int R, void* y, int ldy, void* u, int ldu, void* stream);
 
+/* SDXL text encoders (encode_prompt, inference_animatediff.py:16-35 / train_animatediff.py:29-50; transformers
+ * CLIPTextModel / CLIPTextModelWithProjection):
+ * vst_embed_tokens: CLIPTextEmbeddings, y[r] = token_embedding[ids[r]] + position_embedding[r % L] (ids int32, in
+ *   range: checked by the caller; y fp32, the towers' residual stream);
+ * vst_residual_layernorm: the encoder layer's residual add in fp32 (h_out = h + y, y bf16 or NULL) fused with the
+ *   next LayerNorm (n = LN(h_out), bf16): the reference's fp32 text towers under bf16 autocast keep the residual
+ *   stream fp32 (CLIPEncoderLayer, layer_norm1/2 and final_layer_norm);
+ * vst_causal_attention: CLIPAttention's softmax(q k^T * scale + causal mask) v over N tokens, head_dim 64;
+ * vst_quick_gelu: the CLIP ViT-L/14 MLP activation x * sigmoid(1.702 x). */
+int vst_embed_tokens(const int* ids, int rows, int L, const void* tok, const void* pos, int C, float* y, int ldy,
+                     void* stream);
+int vst_residual_layernorm(const float* h, int ldh, const void* y, int ldy, int rows, int C, const float* gamma,
+                           const float* beta, float eps, float* h_out, int ldho, void* n, int ldn, void* stream);
+int vst_causal_attention(const void* q, int ldq, const void* k, const void* v, int ldkv, void* o, int ldo, int nbatch,
+                         int heads, int N, int head_dim, float scale, void* stream);
+int vst_quick_gelu(const void* x, void* y, size_t n, void* stream);
+
 /* Row-block permutation: rows of C bf16 indexed (i0,i1,i2,i3) over dims (d0..d3) in src; dst
  * axis k is src axis p_k.  Used for the frame-shard <-> pixel-shard exchange around the motion
  * module's frame-axis attention (the reference's (B*F,HW,C) <-> (B*HW,F,C) permutes of

@@ -156,3 +156,26 @@ def test_gemm_kernel_policy_host_only():
     assert name(2, 1280, 1280, 0).endswith("splitk>")           # temb projection: M = 2
     assert name(131072, 320, 2880, 2).endswith("conv>")
     assert name(131072, 4, 2880, 2) == "gemm_ring<128x64,conv>"  # conv_out
+
+
+def test_text_encoder_surface_cpu():
+    """The SDXL text towers keep transformers' module tree / state-dict keys (a checkpoint's text_encoder and
+    text_encoder_2 load unchanged, with or without the "text_model." prefix recent transformers drop), and refuse
+    to run from CPU weights (no CPU fallback)."""
+    import transformers
+    from video_style_transfer_amd import _lib
+    from video_style_transfer_amd import text_encoder as T
+    for cfg, ours_cls, ref_cls in ((T.CLIPTextConfig.tiny(), T.CLIPTextModel, transformers.CLIPTextModel),
+                                   (T.CLIPTextConfig.tiny("gelu"), T.CLIPTextModelWithProjection,
+                                    transformers.CLIPTextModelWithProjection)):
+        tc = transformers.CLIPTextConfig(vocab_size=cfg.vocab_size, hidden_size=cfg.hidden_size,
+                                         intermediate_size=cfg.intermediate_size,
+                                         num_hidden_layers=cfg.num_hidden_layers,
+                                         num_attention_heads=cfg.num_attention_heads, hidden_act=cfg.hidden_act,
+                                         projection_dim=cfg.projection_dim, eos_token_id=2, bos_token_id=0)
+        sd = ref_cls(tc).state_dict()
+        model = T.build_text_encoder(ours_cls, cfg, state_dict=sd, device="cpu")
+        ours = {k if k.startswith(("text_model.", "text_projection")) else "text_model." + k for k in sd}
+        assert ours == set(model.state_dict())
+        with pytest.raises(_lib.VstError):
+            model(torch.zeros(1, 77, dtype=torch.long))

@@ -44,6 +44,10 @@ SIGNATURES = {
     "vst_step_advance": (_I, [_P, _I, _P]),
     "vst_silu": (_I, [_P, _P, _S, _P]),
     "vst_add": (_I, [_P, _P, _P, _S, _P]),
+    "vst_quick_gelu": (_I, [_P, _P, _S, _P]),
+    "vst_embed_tokens": (_I, [_P, _I, _I, _P, _P, _I, _P, _I, _P]),
+    "vst_causal_attention": (_I, [_P, _I, _P, _P, _I, _P, _I, _I, _I, _I, _I, _F, _P]),
+    "vst_residual_layernorm": (_I, [_P, _I, _P, _I, _I, _I, _P, _P, _F, _P, _I, _P, _I, _P]),
     "vst_copy2d": (_I, [_P, _I, _P, _I, _I, _I, _P]),
     "vst_transpose": (_I, [_P, _I, _I, _I, _P, _I, _P]),
     "vst_layernorm_bwd_workspace_bytes": (_S, [_I, _I]),

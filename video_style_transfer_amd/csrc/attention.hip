@@ -86,7 +86,7 @@ template <int PRE>
 __global__ __launch_bounds__(256, 2) void spatial_attn_kernel(
     const bf16_t* __restrict__ Q, int ldq, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V, int ldkv,
     bf16_t* __restrict__ O, int ldo, int nbatch, int heads, int Nq, int Nk, int kv_div, float scale_log2,
-    uint32_t q_bytes, uint32_t kv_bytes, float* __restrict__ lse) {
+    uint32_t q_bytes, uint32_t kv_bytes, float* __restrict__ lse, int causal = 0) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nqb = (Nq + 127) / 128;
@@ -197,14 +197,16 @@ __global__ __launch_bounds__(256, 2) void spatial_attn_kernel(
         s[kt][qb] = a;
       }
     }
-    // ---- mask keys beyond Nk (last tile) ----
-    if ((t + 1) * SA_KT > Nk) {
+    // ---- mask keys beyond Nk (last tile); causal: keys after the query (CLIP text self-attention) ----
+    if ((t + 1) * SA_KT > Nk || causal) {
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int key = t * SA_KT + kt * 16 + g * 4 + i;
-          if (key >= Nk) { s[kt][0][i] = -INFINITY; s[kt][1][i] = -INFINITY; }
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb)
+            if (key >= Nk || (causal && key > qbase + qb * 16 + fr)) s[kt][qb][i] = -INFINITY;
         }
     }
     // ---- online softmax (lane-local rows; reduce over the 4 g-lanes) ----
@@ -1010,6 +1012,22 @@ extern "C" int vst_spatial_attention(const void* q, int ldq, const void* k, cons
     default: VST_SA_LAUNCH(0); break;
   }
 #undef VST_SA_LAUNCH
+  return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+}
+
+// Causal self-attention over N tokens, head_dim 64 (the CLIP text encoders' CLIPAttention with the causal mask of
+// transformers' CLIPTextTransformer): query i attends to keys 0..i.  Same kernel as vst_spatial_attention.
+extern "C" int vst_causal_attention(const void* q, int ldq, const void* k, const void* v, int ldkv, void* o, int ldo,
+                                    int nbatch, int heads, int N, int head_dim, float scale, void* stream) {
+  if (head_dim != 64 || !q || !k || !v || !o || nbatch <= 0 || heads <= 0 || N <= 0) return VST_ERR_ARG;
+  if ((ldq & 7) || (ldkv & 7) || (ldo & 7)) return VST_ERR_ARG;
+  const int nqb = (N + 127) / 128;
+  const uint32_t qb = clampb(((size_t)(nbatch * N - 1) * ldq + heads * 64) * 2);
+  const uint32_t kvb = clampb(((size_t)(nbatch * N - 1) * ldkv + heads * 64) * 2);
+  const dim3 grid(nqb * heads * nbatch);
+  hipLaunchKernelGGL(spatial_attn_kernel<0>, grid, dim3(256), SA_LDS, (hipStream_t)stream, (const bf16_t*)q, ldq,
+                     (const bf16_t*)k, (const bf16_t*)v, ldkv, (bf16_t*)o, ldo, nbatch, heads, N, N, 1,
+                     scale * 1.4426950408889634f, qb, kvb, (float*)nullptr, 1);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 

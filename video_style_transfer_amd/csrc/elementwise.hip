@@ -29,6 +29,24 @@ __global__ void silu_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y
     y[i] = f2bf(silu(bf2f(x[i])));
 }
 
+// transformers' quick_gelu (CLIP ViT-L/14 text MLP): x * sigmoid(1.702 x), fp32 math, one rounding
+__global__ void quick_gelu_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const float v = bf2f(x[i]);
+    y[i] = f2bf(v / (1.f + __expf(-1.702f * v)));
+  }
+}
+
+// CLIPTextEmbeddings: y[r][c] = token_embedding[ids[r]][c] + position_embedding[r % L][c], fp32 (the text towers'
+// residual stream, text_encoder.py)
+__global__ void embed_tokens_kernel(const int* __restrict__ ids, int rows, int L, const bf16_t* __restrict__ tok,
+                                    const bf16_t* __restrict__ pos, int C, float* __restrict__ y, int ldy) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= rows * C) return;
+  const int r = idx / C, c = idx - r * C;
+  y[(size_t)r * ldy + c] = bf2f(tok[(size_t)ids[r] * C + c]) + bf2f(pos[(size_t)(r % L) * C + c]);
+}
+
 __global__ void add_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b, bf16_t* __restrict__ y,
                            size_t n) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
@@ -420,6 +438,22 @@ extern "C" int vst_silu(const void* x, void* y, size_t n, void* stream) {
   if (!x || !y) return VST_ERR_ARG;
   const int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(silu_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, (bf16_t*)y, n);
+  return ok();
+}
+
+extern "C" int vst_quick_gelu(const void* x, void* y, size_t n, void* stream) {
+  if (!x || !y) return VST_ERR_ARG;
+  const int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(quick_gelu_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, (bf16_t*)y,
+                     n);
+  return ok();
+}
+
+extern "C" int vst_embed_tokens(const int* ids, int rows, int L, const void* tok, const void* pos, int C, float* y,
+                                int ldy, void* stream) {
+  if (!ids || !tok || !pos || !y || rows <= 0 || L <= 0 || C <= 0 || ldy < C) return VST_ERR_ARG;
+  hipLaunchKernelGGL(embed_tokens_kernel, dim3((rows * C + 255) / 256), dim3(256), 0, (hipStream_t)stream, ids, rows,
+                     L, (const bf16_t*)tok, (const bf16_t*)pos, C, y, ldy);
   return ok();
 }
 

@@ -953,6 +953,63 @@ extern "C" int vst_layernorm_lora(const void* x, int ldx, int C, int rows, const
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 
+// fp32 residual stream + LayerNorm (the CLIP text encoders, text_encoder.py): h_out = h + y (y bf16, optional),
+// n = LN(h_out) in bf16 (the projection input).  The reference's text towers are fp32 modules under bf16 autocast:
+// their residual stream stays fp32, only the matmul outputs are bf16 -- so this path keeps it fp32 too.  One
+// workgroup of 256 threads per row, two-pass statistics (C <= 2048).
+__global__ __launch_bounds__(256) void residual_layernorm_kernel(const float* __restrict__ h, int ldh,
+                                                                 const bf16_t* __restrict__ y, int ldy, int C,
+                                                                 const float* __restrict__ gamma,
+                                                                 const float* __restrict__ beta, float eps,
+                                                                 float* __restrict__ ho, int ldho,
+                                                                 bf16_t* __restrict__ n, int ldn) {
+  __shared__ float red[4];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  float v[8];
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = tid + 256 * e;
+    float x = 0.f;
+    if (c < C) {
+      x = h[(size_t)row * ldh + c];
+      if (y) x += bf2f(y[(size_t)row * ldy + c]);
+      ho[(size_t)row * ldho + c] = x;
+    }
+    v[e] = x;
+    s += x;
+  }
+  s = wave_sum(s);
+  if (lane == 0) red[w] = s;
+  __syncthreads();
+  const float mean = (red[0] + red[1] + red[2] + red[3]) / C;
+  __syncthreads();
+  float q = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+    if (tid + 256 * e < C) { const float d = v[e] - mean; q += d * d; }
+  q = wave_sum(q);
+  if (lane == 0) red[w] = q;
+  __syncthreads();
+  const float rstd = rsqrtf((red[0] + red[1] + red[2] + red[3]) / C + eps);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = tid + 256 * e;
+    if (c < C) n[(size_t)row * ldn + c] = f2bf((v[e] - mean) * rstd * gamma[c] + beta[c]);
+  }
+}
+
+extern "C" int vst_residual_layernorm(const float* h, int ldh, const void* y, int ldy, int rows, int C,
+                                      const float* gamma, const float* beta, float eps, float* h_out, int ldho,
+                                      void* n, int ldn, void* stream) {
+  if (!h || !h_out || !n || !gamma || !beta || rows <= 0 || C <= 0 || C > 2048 || ldh < C || ldho < C || ldn < C ||
+      (y && ldy < C))
+    return VST_ERR_ARG;
+  hipLaunchKernelGGL(residual_layernorm_kernel, dim3(rows), dim3(256), 0, (hipStream_t)stream, h, ldh,
+                     (const bf16_t*)y, ldy, C, gamma, beta, eps, h_out, ldho, (bf16_t*)n, ldn);
+  return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+}
+
 // ---- LayerNorm backward (training path) ----
 static inline int lnb_grid(int rows) { return std::max(1, std::min(512, (rows + 3) / 4)); }
 
