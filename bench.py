@@ -68,6 +68,9 @@ def parse():
     ap.add_argument("--grad-accum", type=int, default=4,
                     help="--train: gradient_accumulation_steps (train_animatediff.py:395, default 4): clips per rank "
                          "per optimizer step")
+    ap.add_argument("--sequential-accum", action="store_true",
+                    help="--train: one forward / backward per clip (the reference's loop shape) instead of the whole "
+                         "accumulation window batched (TrainStep.window; same gradient)")
     return ap.parse_args()
 
 
@@ -388,7 +391,9 @@ def bench_train(args, world, rank, local, dev):
                      seed=args.seed, lr_scheduler=lr_sched, gradient_accumulation_steps=args.grad_accum)
     g = torch.Generator().manual_seed(100 + rank)
     h = args.size // 8
-    lat = torch.randn(1, 4, args.frames, h, h, generator=g).to(dev)
+    window = not args.sequential_accum and args.grad_accum > 1
+    nclip = args.grad_accum if window else 1   # clips per forward / backward
+    lat = torch.randn(nclip, 4, args.frames, h, h, generator=g).to(dev)
     vae = frames = None
     if not args.no_vae:
         # train_animatediff.py:219-224 inside every step: the clip's frames (synthetic, in [-1, 1]) -> VAE encode ->
@@ -397,23 +402,26 @@ def bench_train(args, world, rank, local, dev):
         from video_style_transfer_amd.train import encode_frames
         from video_style_transfer_amd.vae import build_vae
         vae = build_vae(VAEConfig.sdxl(), seed=args.seed + 1, device=dev)
-        frames = (torch.rand(1, args.frames, 3, args.size, args.size, generator=g) * 2 - 1).to(dev)
+        frames = (torch.rand(nclip, args.frames, 3, args.size, args.size, generator=g) * 2 - 1).to(dev)
         vgen = torch.Generator(device=dev).manual_seed(200 + rank)
         lat = encode_frames(vae, frames, vgen)
     enc = torch.randn(1, 77, cfg.cross_attention_dim, generator=g)
     pooled = torch.randn(1, cfg.text_embed_dim, generator=g)
     unc, unp = torch.zeros_like(enc), torch.zeros_like(pooled)
     if graph:
-        step.capture(lat, enc, pooled, uncond_prompt=unc, uncond_pooled=unp)
+        step.capture(lat, enc, pooled, uncond_prompt=unc, uncond_pooled=unp, window=window)
 
         def micro():
             return step.replay(None if vae is None else encode_frames(vae, frames, vgen))
+    elif window:
+        def micro():
+            return step.window(lat if vae is None else encode_frames(vae, frames, vgen), enc, pooled, unc, unp)
     else:
         def micro():
             return step(lat if vae is None else encode_frames(vae, frames, vgen), enc, pooled, unc, unp)
 
     def run():  # one optimizer step = one accumulation window of --grad-accum clips per rank
-        for _ in range(args.grad_accum):
+        for _ in range(1 if window else args.grad_accum):
             out = micro()
         assert out["sync"]
         return out
@@ -444,8 +452,12 @@ def bench_train(args, world, rank, local, dev):
     if not args.no_roofline:
         # one instrumented eager step (HIP events around every launch on its stream)
         K.profile_launches(True)
-        for _ in range(args.grad_accum):  # one whole window, so the optimizer / clip launches are counted once
-            step(lat if vae is None else encode_frames(vae, frames, vgen), enc, pooled)
+        lat_e = lat if vae is None else encode_frames(vae, frames, vgen)
+        if window:  # one whole window, so the optimizer / clip launches are counted once
+            step.window(lat_e, enc, pooled)
+        else:
+            for _ in range(args.grad_accum):
+                step(lat_e, enc, pooled)
         rl, table = _roofline_from(K.collect_launches())
         K.profile_launches(False)
         fl = rl.pop("step_flops")
@@ -466,7 +478,9 @@ def bench_train(args, world, rank, local, dev):
             "config": {"workload": f"BASELINE configs[4]: train_animatediff.py step, {args.frames}x{args.size}x"
                                    f"{args.size} clip/GPU, temporal LoRA r=32, UnZipLoRA r={args.lora_rank} frozen, "
                                    f"orth loss 1e-4, clip 0.5, AdamW, cosine lr (100 warm-up), gradient accumulation "
-                                   f"{args.grad_accum} (one step = {args.grad_accum} clips per GPU)" + (
+                                   f"{args.grad_accum} (one step = {args.grad_accum} clips per GPU"
+                                   + (", the window batched in one fwd+bwd)" if window else ", one fwd+bwd per clip)")
+                                   + (
                                        ", from synthetic latents (no VAE encode)" if vae is None else
                                        ", VAE encode of the synthetic frames in every step"),
                        "model": "SDXL UNet + AnimateDiff-SDXL motion modules (synthetic weights)",

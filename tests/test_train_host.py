@@ -213,3 +213,36 @@ def test_train_step_accumulation_data_parallel_cpu_world2():
         p.join(timeout=60)
     for rank, status, info in res:
         assert status == "ok", f"rank {rank}: {info}"
+
+
+def test_train_step_window_equals_sequential_calls():
+    """TrainStep.window (the accumulation window as ONE batched forward / backward) == the N sequential calls it
+    replaces: same random draws (in the calls' order), same accumulated gradient, weights and lr after the step."""
+    from video_style_transfer_amd.train import get_scheduler
+    ToyStep = _toy_step_cls()
+    accum = 3
+    lat = torch.cat([b[0] for b in _batches(2 * accum, seed=21)])
+    enc, pool = torch.zeros(1, 77, 8), torch.zeros(1, 8)
+
+    def make():
+        torch.manual_seed(3)
+        m = _Toy()
+        ps = [p for p in m.parameters() if p.requires_grad]
+        opt = torch.optim.AdamW(ps, lr=1e-2)
+        return m, ps, opt, ToyStep(m, opt, _Sched(), max_grad_norm=0.05, seed=4,
+                                   lr_scheduler=get_scheduler("cosine", opt, 2, 10), gradient_accumulation_steps=accum,
+                                   num_processes=1)
+    m1, p1, o1, s1 = make()
+    m2, p2, o2, s2 = make()
+    for w in range(2):  # two windows: the second one moves the weights (warm-up lr 0 on the first)
+        chunk = lat[w * accum:(w + 1) * accum]
+        outs = [s1(chunk[i:i + 1], enc, pool, enc, pool) for i in range(accum)]
+        ow = s2.window(chunk, enc, pool, enc, pool)
+        assert [o["uncond"] for o in outs] == ow["uncond"]
+        assert torch.equal(torch.cat([o["timesteps"] for o in outs]), ow["timesteps"])
+        assert float(ow["loss"]) == pytest.approx(sum(float(o["loss"]) for o in outs) / accum, rel=1e-5)
+        assert float(ow["grad_norm"]) == pytest.approx(float(outs[-1]["grad_norm"]), rel=1e-5)
+        for a, b in zip(p1, p2):
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-7)
+        assert o1.param_groups[0]["lr"] == o2.param_groups[0]["lr"] and s1.micro == s2.micro == 0
+        assert s1.lr_scheduler._step_count == s2.lr_scheduler._step_count

@@ -182,3 +182,51 @@ def test_train_step_sdxl_16x512_graph_equals_eager(cuda):
     assert le == lg and ge == gg  # same kernels on the same inputs: bitwise-equal loss and gradient norm
     for p, w in zip(params, we):  # same kernels, same AdamW: the captured step IS the eager step
         assert torch.equal(p.detach(), w)
+
+
+def test_train_step_window_graph_and_sequential(cuda):
+    """TrainStep.window -- the accumulation window (2 micro-batches here) as ONE batched forward / backward -- on the
+    HIP UNet: its captured graph equals the eager window bit for bit, and both match the sequential calls it
+    replaces (the reference's loop): same draws, loss and gradient norm to fp32 / bf16 summation order, same update
+    sizes, over two optimizer steps with the cosine warm-up moving the lr."""
+    from video_style_transfer_amd.config import UNetMotionConfig
+    from video_style_transfer_amd.scheduler import EulerDiscreteScheduler
+    from video_style_transfer_amd.train import TrainStep, get_scheduler, make_adamw
+    cfg = UNetMotionConfig.tiny()
+    accum = 2
+    models = [_model(cfg, cuda, 8, 4) for _ in range(3)]
+    enc, pooled, unc, unp = _text(cfg)
+    lat = torch.randn(2 * accum, 4, 4, 8, 8, generator=torch.Generator().manual_seed(31)).to(cuda)
+    kw = dict(lambda_orth=1e-2, max_grad_norm=0.5, resolution=64, seed=13, gradient_accumulation_steps=accum)
+    steps = []
+    for u, idx in models:
+        ps = [p for p in u.parameters() if p.requires_grad]
+        opt = make_adamw(ps, lr=1e-3, capturable=True)
+        steps.append((TrainStep(u, opt, EulerDiscreteScheduler(), spatial_index=idx,
+                                lr_scheduler=get_scheduler("cosine", opt, 1, 6), **kw), ps))
+    (sw, pw), (sg, pg), (ss, ps_) = steps
+    sg.capture(lat[:accum], enc, pooled, uncond_prompt=unc, uncond_pooled=unp, window=True)
+    assert sg.graph_micro is None
+    prev = [p.detach().clone() for p in ps_]
+    for w in range(2):
+        chunk = lat[w * accum:(w + 1) * accum]
+        ow = sw.window(chunk, enc, pooled, unc, unp)
+        og = sg.replay(chunk)
+        os_ = [ss(chunk[i:i + 1], enc, pooled, unc, unp) for i in range(accum)]
+        torch.cuda.synchronize()
+        assert ow["uncond"] == og["uncond"] == [o["uncond"] for o in os_]
+        assert float(ow["loss"]) == float(og["loss"]) and float(ow["grad_norm"]) == float(og["grad_norm"])
+        for a, b in zip(pw, pg):
+            assert torch.equal(a, b), f"window {w}: captured window differs from the eager window"
+        ls = sum(float(o["loss"]) for o in os_) / accum
+        gs = float(os_[-1]["grad_norm"])
+        dw = torch.cat([(a.detach().float() - b.float()).flatten() for a, b in zip(pw, prev)])
+        ds = torch.cat([(a.detach().float() - b.float()).flatten() for a, b in zip(ps_, prev)])
+        print(f"[train-window] window {w}: loss {float(ow['loss']):.6f} / sequential {ls:.6f}; grad norm "
+              f"{float(ow['grad_norm']):.5e} / {gs:.5e}; |update| {dw.norm():.4e} / {ds.norm():.4e}")
+        assert abs(float(ow["loss"]) - ls) <= 2e-3 * ls and abs(float(ow["grad_norm"]) - gs) <= 2e-2 * gs
+        if w == 0:
+            assert dw.abs().max() == 0 and ds.abs().max() == 0  # warm-up lr 0
+        else:
+            assert abs(dw.norm() / ds.norm() - 1) < 2e-2
+        prev = [p.detach().clone() for p in ps_]

@@ -246,7 +246,8 @@ class TrainStep:
         pool = pool.expand(B, -1).contiguous()
         return enc, pool
 
-    def _body(self, latents, noise, t, enc, pool, sync: bool = True, zero_in_place: bool = False) -> Dict:
+    def _body(self, latents, noise, t, enc, pool, sync: bool = True, zero_in_place: bool = False,
+              div: Optional[int] = None) -> Dict:
         """Forward, losses, backward (gradients accumulate into p.grad); on a sync call also gradient averaging,
         clipping and the optimizer step.  Device tensors only (no host synchronisation: the body is what
         TrainStep.capture records into a HIP graph).  zero_in_place: the sync body ends by zeroing the gradient
@@ -255,7 +256,8 @@ class TrainStep:
         loss, loss_mse, loss_orth = self._loss(latents, noise, t, enc, pool)
         if self.reducer is not None:
             self.reducer.sync = sync                                                       # DDP no_sync otherwise
-        (loss / self.accum if self.accum > 1 else loss).backward()                         # :314 accelerator.backward
+        div = self.accum if div is None else div
+        (loss / div if div > 1 else loss).backward()                                       # :314 accelerator.backward
         if sync:
             if self.reducer is not None:
                 self.reducer.finish()
@@ -335,8 +337,63 @@ class TrainStep:
         out.update(uncond=use_uncond, timesteps=t, sync=sync)
         return out
 
+    # ---- a whole accumulation window as one batched forward + backward -----------------------------------------
+    def _window_draws(self, latents, has_uncond, noise=None, timesteps=None, use_uncond=None):
+        """The draws of the window's N sequential calls, in their order (so the RNG stream is the per-call one)."""
+        N = self.accum
+        B = latents.shape[0]
+        if B % N:
+            raise ValueError(f"TrainStep.window: {B} clips do not split into {N} micro-batches")
+        mb = B // N
+        ns, ts, us = [], [], []
+        for i in range(N):
+            sl = slice(i * mb, (i + 1) * mb)
+            n_i, t_i, u_i = self._draw(latents[sl], None if noise is None else noise[sl],
+                                       None if timesteps is None else timesteps[sl],
+                                       None if use_uncond is None else use_uncond[i], has_uncond)
+            ns.append(n_i)
+            ts.append(t_i)
+            us.append(bool(u_i))
+        return torch.cat(ns), torch.cat(ts), us
+
+    def window(self, latents: torch.Tensor, prompt, pooled, uncond_prompt=None, uncond_pooled=None, *,
+               noise: Optional[torch.Tensor] = None, timesteps: Optional[torch.Tensor] = None,
+               use_uncond: Optional[List[bool]] = None) -> Dict:
+        """A whole accumulation window -- the gradient_accumulation_steps calls of one optimizer step -- as ONE
+        forward + backward over the window's clips stacked on the batch axis (latents: (N * micro_batch, C, F, h,
+        w)), then the sync call's all-reduce / clip / AdamW / zero and the scheduler bookkeeping of N calls.
+
+        Same gradient as the N sequential calls: every op of the UNet is per clip (no batch mixing), the mean MSE
+        over the N equal-sized micro-batches is the mean of their means, and the orth loss, identical in every call
+        of a window (the weights only change at its end), enters once instead of N times 1/N.  Each clip keeps its
+        own noise, timestep and unconditional-prompt coin, drawn in the sequential calls' order.  What changes is
+        only the shape of every GEMM (M x N clips), i.e. fp32 summation orders."""
+        if self.micro != 0:
+            raise RuntimeError("TrainStep.window: call at the start of an accumulation window")
+        dev = latents.device
+        has_u = uncond_prompt is not None
+        noise, t, us = self._window_draws(latents, has_u, noise, timesteps, use_uncond)
+        mb = latents.shape[0] // self.accum
+        encs, pools = [], []
+        for u in us:
+            e, p_ = self._text(uncond_prompt if u else prompt, uncond_pooled if u else pooled, mb, dev)
+            encs.append(e)
+            pools.append(p_)
+        if self.graph is not None:
+            torch._foreach_zero_([p.grad for p in self.params if p.grad is not None])
+        else:
+            self.opt.zero_grad(set_to_none=True)
+        out = self._body(latents, noise.to(dev, torch.float32), t.to(dev), torch.cat(encs), torch.cat(pools),
+                         sync=True, div=1)
+        for _ in range(self.accum - 1):
+            self._advance(False)
+        self._advance(True)
+        out.update(uncond=us, timesteps=t, sync=True)
+        return out
+
     # ---- HIP-graph capture of the whole step (single process) ------------------------------------------------
-    def capture(self, latents: torch.Tensor, prompt, pooled, warmup: int = 2, uncond_prompt=None, uncond_pooled=None):
+    def capture(self, latents: torch.Tensor, prompt, pooled, warmup: int = 2, uncond_prompt=None, uncond_pooled=None,
+                window: bool = False):
         """Record the step into HIP graphs on static buffers: one graph for the sync call (forward, backward,
         clipping, AdamW, zeroing) and, with gradient accumulation, one for the other calls (forward + backward
         accumulating into the static .grad tensors).  `warmup` eager windows run first on a side stream (they fill
@@ -345,7 +402,8 @@ class TrainStep:
         The optimizer must be capturable; with an lr scheduler its lr must be a device tensor (make_adamw) so the
         schedule reaches the replays.  Per-call host work left outside the graphs: the random draws (copied into
         the static noise / timestep / text buffers) and the scheduler step.  Single process only (the reducer's
-        collectives stay eager)."""
+        collectives stay eager).  window=True: one graph of the whole accumulation window as TrainStep.window runs
+        it (latents then hold the window's N micro-batches); replay() then runs a whole optimizer step."""
         if self.reducer is not None and self.reducer.world > 1:
             raise NotImplementedError("TrainStep.capture: data-parallel steps run eagerly")
         dev = latents.device
@@ -358,13 +416,17 @@ class TrainStep:
         if self.micro != 0:
             raise RuntimeError("TrainStep.capture: call at the start of an accumulation window")
         B = latents.shape[0]
+        if window and B % self.accum:
+            raise ValueError(f"TrainStep.capture(window=True): {B} clips do not split into {self.accum} micro-batches")
+        self.window_mode = window
+        mb = B // self.accum if window else B
         self.s_lat = latents.detach().clone()
         self.s_noise = torch.zeros_like(self.s_lat)
         self.s_t = torch.zeros(B, dtype=torch.long, device=dev)
         self.s_enc, self.s_pool = self._text(prompt, pooled, B, dev)
-        # the two text conditions a step can draw (:248-254), copied into the static buffers before each replay
-        self.text_cond = (self.s_enc.clone(), self.s_pool.clone())
-        self.text_uncond = None if uncond_prompt is None else self._text(uncond_prompt, uncond_pooled, B, dev)
+        # the two text conditions a call can draw (:248-254), per micro-batch, copied into the static buffers
+        self.text_cond = self._text(prompt, pooled, mb, dev)
+        self.text_uncond = None if uncond_prompt is None else self._text(uncond_prompt, uncond_pooled, mb, dev)
 
         # training state the warm-up must not change
         gen_state = self.gen.get_state()
@@ -381,6 +443,13 @@ class TrainStep:
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
             for _ in range(warmup):
+                if window:
+                    noise, t, _ = self._window_draws(self.s_lat, False)
+                    self.s_noise.copy_(noise)
+                    self.s_t.copy_(t)
+                    self._body(self.s_lat, self.s_noise, self.s_t, self.s_enc, self.s_pool, sync=True,
+                               zero_in_place=True, div=1)
+                    continue
                 for k in range(self.accum):
                     noise, t, _ = self._draw(self.s_lat)
                     self.s_noise.copy_(noise)
@@ -407,8 +476,8 @@ class TrainStep:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.s_out = self._body(self.s_lat, self.s_noise, self.s_t, self.s_enc, self.s_pool, sync=True,
-                                    zero_in_place=True)
-        if self.accum > 1:
+                                    zero_in_place=True, div=1 if window else None)
+        if self.accum > 1 and not window:
             self.graph_micro = torch.cuda.CUDAGraph()  # own memory pool: its temporaries never alias s_out
             with torch.cuda.graph(self.graph_micro):
                 self.s_out_micro = self._body(self.s_lat, self.s_noise, self.s_t, self.s_enc, self.s_pool,
@@ -420,6 +489,20 @@ class TrainStep:
         returned tensors are the graph's static outputs: read them before the next replay of the same graph."""
         if latents is not None:
             self.s_lat.copy_(latents)
+        if getattr(self, "window_mode", False):
+            noise, t, us = self._window_draws(self.s_lat, self.text_uncond is not None)
+            self.s_noise.copy_(noise)
+            self.s_t.copy_(t)
+            L, mb = self.text_cond[0].shape[0], self.text_cond[1].shape[0]
+            for i, u in enumerate(us):
+                enc, pool = self.text_uncond if u else self.text_cond
+                self.s_enc[i * L:(i + 1) * L].copy_(enc)
+                self.s_pool[i * mb:(i + 1) * mb].copy_(pool)
+            self.graph.replay()
+            for _ in range(self.accum - 1):
+                self._advance(False)
+            self._advance(True)
+            return dict(self.s_out, uncond=us, timesteps=t, sync=True)
         noise, t, use_uncond = self._draw(self.s_lat, has_uncond=self.text_uncond is not None)
         self.s_noise.copy_(noise)
         self.s_t.copy_(t)
