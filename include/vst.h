@@ -184,6 +184,11 @@ int vst_temporal_attention_bwd(const void* q, const void* k, const void* v, int 
                                void* dq, void* dk, void* dv, int lddqkv, int nclip, int F, int HW, int heads,
                                int head_dim, float scale, void* stream);
 int vst_geglu_bwd(const void* p, int ldp, const void* g, int ldg, int M, int Nh, void* dp, int lddp, void* stream);
+/* vst_colsum: y[N] (fp32) = column sums of the bf16 [M, N] view x (the bias gradients db = g^T 1 of the trainable
+ * linears / GEGLU projections; torch's g.float().sum(0) in autograd's Linear backward), N % 8 == 0.  Deterministic
+ * two-pass reduction through a workspace of vst_colsum_workspace_bytes(M, N) bytes (no atomics, no memset). */
+size_t vst_colsum_workspace_bytes(int M, int N);
+int vst_colsum(const void* x, int ldx, int M, int N, float* y, void* workspace, void* stream);
 
 /* ---- SDXL VAE (diffusers AutoencoderKL, fp32 in the reference: inference_animatediff.py:164-169) decode of the
  * denoised clip (inference_animatediff.py:137-144) and encode of training frames (train_animatediff.py:219-224),

@@ -137,10 +137,12 @@ def test_train_step_graph_equals_eager_accumulation_and_schedule(cuda):
                 assert torch.equal(p, q)
 
 
-def test_train_step_sdxl_16x512_graph_equals_eager(cuda):
+@pytest.mark.parametrize("window", [False, True])
+def test_train_step_sdxl_16x512_graph_equals_eager(cuda, window):
     """BASELINE configs[4] at its own size: SDXL UNet + 15 motion modules, UnZipLoRA r=8 frozen on all 560 spatial
     projections, temporal LoRA r=32 on the 120 motion projections, one 16-frame 512^2 clip, orth loss 1e-4,
-    clip_grad_norm_(0.5), AdamW(2e-5) -- eager vs captured on the same draws and the same starting weights."""
+    clip_grad_norm_(0.5), AdamW(2e-5) -- eager vs captured on the same draws and the same starting weights.
+    window=True: an accumulation window of two clips as one batched step (TrainStep.window), eager vs captured."""
     from video_style_transfer_amd.config import UNetMotionConfig
     from video_style_transfer_amd.scheduler import EulerDiscreteScheduler
     from video_style_transfer_amd.train import TrainStep, make_adamw
@@ -149,12 +151,15 @@ def test_train_step_sdxl_16x512_graph_equals_eager(cuda):
     params = [p for p in unet.parameters() if p.requires_grad]
     assert 150e6 < sum(p.numel() for p in params) < 160e6
     enc, pooled, unc, unp = _text(cfg, 6)
-    lat = torch.randn(1, 4, 16, 64, 64, generator=torch.Generator().manual_seed(7)).to(cuda)
-    kw = dict(lambda_orth=1e-4, spatial_index=index, max_grad_norm=0.5, resolution=512, seed=11)
+    nb = 2 if window else 1
+    lat = torch.randn(nb, 4, 16, 64, 64, generator=torch.Generator().manual_seed(7)).to(cuda)
+    kw = dict(lambda_orth=1e-4, spatial_index=index, max_grad_norm=0.5, resolution=512, seed=11,
+              gradient_accumulation_steps=nb)
     snap = [p.detach().clone() for p in params]
 
     opt_e = make_adamw(params, lr=2e-5, capturable=True)
-    oe = TrainStep(unet, opt_e, EulerDiscreteScheduler(), **kw)(lat, enc, pooled, unc, unp)
+    st_e = TrainStep(unet, opt_e, EulerDiscreteScheduler(), **kw)
+    oe = st_e.window(lat, enc, pooled, unc, unp) if window else st_e(lat, enc, pooled, unc, unp)
     torch.cuda.synchronize()
     we = [p.detach().clone() for p in params]
     de = [(p.detach().float() - q.float()) for p, q in zip(params, snap)]
@@ -168,14 +173,14 @@ def test_train_step_sdxl_16x512_graph_equals_eager(cuda):
 
     opt_g = make_adamw(params, lr=2e-5, capturable=True)
     step = TrainStep(unet, opt_g, EulerDiscreteScheduler(), **kw)
-    step.capture(lat, enc, pooled, uncond_prompt=unc, uncond_pooled=unp)
+    step.capture(lat, enc, pooled, uncond_prompt=unc, uncond_pooled=unp, window=window)
     og = step.replay()
     torch.cuda.synchronize()
     lg, gg = float(og["loss"]), float(og["grad_norm"])
     dg = [(p.detach().float() - q.float()) for p, q in zip(params, snap)]
     ne = torch.cat([d.flatten() for d in de]).norm()
     ng = torch.cat([d.flatten() for d in dg]).norm()
-    print(f"[train-sdxl] loss eager {le:.6f} graph {lg:.6f} (orth {lo:.3e}); grad_norm {ge:.5e} / {gg:.5e}; "
+    print(f"[train-sdxl{' window' if window else ''}] loss eager {le:.6f} graph {lg:.6f} (orth {lo:.3e}); grad_norm {ge:.5e} / {gg:.5e}; "
           f"|update| {ne:.4e} / {ng:.4e}; peak {torch.cuda.max_memory_allocated() / 2 ** 30:.1f} GiB")
     assert torch.isfinite(og["loss"]) and torch.isfinite(og["grad_norm"]) and lo > 0
     assert oe["timesteps"].tolist() == og["timesteps"].tolist() and oe["uncond"] == og["uncond"]

@@ -527,3 +527,31 @@ def test_unet_training_step_grads_vs_oracle(cuda, config):
     bad = {n: (e, yerr[n]) for n, e in errs.items() if e >= max(5e-2, 1.5 * yerr[n])}
     assert not bad, bad
     assert errs[order[len(order) // 2]] <= max(3e-2, 1.5 * yorder[len(yorder) // 2])
+
+
+@pytest.mark.parametrize("M,N,ld", [(512, 512, 512), (65536, 1280, 1280), (1000, 64, 72), (3, 8, 8),
+                                    (16384, 2560, 3840)])
+def test_colsum(cuda, M, N, ld):
+    """vst_colsum (bias gradients db = g^T 1) against an fp64 column sum; deterministic (two calls and a captured
+    replay bit for bit equal)."""
+    from video_style_transfer_amd import kernels as K
+    g = torch.Generator(device=cuda).manual_seed(M + N)
+    x = torch.randn(M, ld, generator=g, device=cuda).to(torch.bfloat16)[:, :N]
+    want = x.double().sum(0)
+    y = K.colsum(x)
+    y2 = K.colsum(x)
+    torch.cuda.synchronize()
+    e = ((y.double() - want).norm() / want.norm()).item()
+    assert e <= 1e-6, e
+    assert torch.equal(y, y2)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        K.colsum(x)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        yg = K.colsum(x)
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(yg, y)

@@ -53,6 +53,8 @@ SIGNATURES = {
     "vst_layernorm_bwd_workspace_bytes": (_S, [_I, _I]),
     "vst_layernorm_bwd": (_I, [_P, _I, _P, _I, _I, _I, _P, _F, _P, _I, _P, _P, _P, _P]),
     "vst_geglu_bwd": (_I, [_P, _I, _P, _I, _I, _I, _P, _I, _P]),
+    "vst_colsum_workspace_bytes": (_S, [_I, _I]),
+    "vst_colsum": (_I, [_P, _I, _I, _I, _P, _P, _P]),
     "vst_groupnorm_bwd_workspace_bytes": (_S, [_I, _I, _I, _I]),
     "vst_groupnorm_bwd": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _F, _P, _P, _I, _P, _I, _P, _P, _P, _P]),
     "vst_spatial_attention_bwd_workspace_bytes": (_S, [_I, _I, _I, _I]),

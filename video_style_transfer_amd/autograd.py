@@ -119,16 +119,18 @@ class LoRALinearFn(torch.autograd.Function):
             Mp = (M + 7) // 8 * 8
             if need_w or need_a:
                 xT = _transpose_padded(x2d, Mp)                                  # [in, Mp]
+            if need_w or need_bb:
+                gT = _transpose_padded(g, Mp)                                    # [N, Mp]
             if need_w:
-                dW = K.linear(_transpose_padded(g, Mp), xT).to(W.dtype)          # [N, in] = g^T x
+                dW = K.linear(gT, xT).to(W.dtype)                                # [N, in] = g^T x
             if need_a:
                 vT = _transpose_padded(v, Mp)                                    # [P, Mp]
                 dA = (K.linear(vT, xT)[:r].float() * s).to(A.dtype)             # [r, in] = s v^T x
             if need_bb:
                 uT = _transpose_padded(u, Mp)                                    # [P, Mp]
-                dB = (K.linear(_transpose_padded(g, Mp), uT)[:, :r].float() * s).to(B.dtype)  # [N, r] = s g^T u
+                dB = (K.linear(gT, uT)[:, :r].float() * s).to(B.dtype)          # [N, r] = s g^T u
             if need_b:
-                db = g.float().sum(0).to(ctx.b_dtype)
+                db = K.colsum(g).to(ctx.b_dtype)                                 # [N] = g^T 1
         return dX, dW, db, dA, dB, None, None
 
 
@@ -158,7 +160,7 @@ class PlainLinearFn(torch.autograd.Function):
             Mp = (M + 7) // 8 * 8
             dW = K.linear(_transpose_padded(g, Mp), _transpose_padded(x2d, Mp)).to(W.dtype)
         if need_b:
-            db = g.float().sum(0).to(ctx.b_dtype)
+            db = K.colsum(g).to(ctx.b_dtype)
         return dX, dW, db
 
 
@@ -296,7 +298,7 @@ class GEGLUFn(torch.autograd.Function):
             Mp = (M + 7) // 8 * 8
             dW = _deinterleave32(K.linear(_transpose_padded(dp, Mp), _transpose_padded(x2d, Mp))).to(ctx.w_dtype)
         if need_b:
-            db = _deinterleave32(dp.float().sum(0)).to(ctx.b_dtype)
+            db = _deinterleave32(K.colsum(dp)).to(ctx.b_dtype)
         return dX, dW, db, None
 
 

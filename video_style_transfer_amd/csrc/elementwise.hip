@@ -611,3 +611,94 @@ extern "C" int vst_softmax_rows(const float* S, int lds, int rows, int n, float 
 }
 
 extern "C" const char* vst_version(void) { return "vst-hip 0.1 gfx950"; }
+
+// ---- column sums (training path: bias gradients db = g^T 1) ------------------------------------------------------
+// bf16 [M, N] row-major view -> fp32 [N], deterministic and graph-safe: pass 1 writes one fp32 partial row per
+// row block (lane = 8-column chunk, 16-B loads; the block's 4 waves stride the rows and are combined in LDS in wave
+// order), pass 2 sums the partial rows in row-block order.  No atomics and no memset, so a captured HIP graph
+// replays it bit for bit; and no fp32 copy of g (torch's g.float().sum(0) writes and re-reads one).
+namespace {
+struct ColsumPlan {
+  int gx, R, rows_per_blk;
+};
+ColsumPlan colsum_plan(int M, int N) {
+  ColsumPlan p;
+  p.gx = (N / 8 + 63) / 64;
+  int R = (2048 + p.gx - 1) / p.gx;                       // ~2048 workgroups in pass 1
+  R = std::max(1, std::min(R, (M + 63) / 64));            // >= 64 rows per block
+  p.rows_per_blk = ((M + R - 1) / R + 3) / 4 * 4;
+  p.R = (M + p.rows_per_blk - 1) / p.rows_per_blk;
+  return p;
+}
+}  // namespace
+
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const bf16_t* __restrict__ x, int ldx, int M, int N,
+                                                             int rows_per_blk, float* __restrict__ part) {
+  __shared__ float red[3][64][8];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int chunk = blockIdx.x * 64 + lane;
+  const bool active = chunk < N / 8;
+  const int r0 = blockIdx.y * rows_per_blk;
+  const int r1 = min(M, r0 + rows_per_blk);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (active) {
+    const bf16_t* base = x + (size_t)chunk * 8;
+    int r = r0 + wave;
+    for (; r + 12 < r1; r += 16) {  // four rows in flight per lane
+      u32x4 a = *reinterpret_cast<const u32x4*>(base + (size_t)r * ldx);
+      u32x4 b = *reinterpret_cast<const u32x4*>(base + (size_t)(r + 4) * ldx);
+      u32x4 c = *reinterpret_cast<const u32x4*>(base + (size_t)(r + 8) * ldx);
+      u32x4 d = *reinterpret_cast<const u32x4*>(base + (size_t)(r + 12) * ldx);
+      float va[8], vb[8], vc[8], vd[8];
+      unpack8(a, va);
+      unpack8(b, vb);
+      unpack8(c, vc);
+      unpack8(d, vd);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += ((va[e] + vb[e]) + (vc[e] + vd[e]));
+    }
+    for (; r < r1; r += 4) {
+      float v[8];
+      unpack8(*reinterpret_cast<const u32x4*>(base + (size_t)r * ldx), v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v[e];
+    }
+  }
+  if (wave > 0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[wave - 1][lane][e] = acc[e];
+  }
+  __syncthreads();
+  if (wave == 0 && active) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = ((acc[e] + red[0][lane][e]) + red[1][lane][e]) + red[2][lane][e];
+    float4* dst = reinterpret_cast<float4*>(part + (size_t)blockIdx.y * N + (size_t)chunk * 8);
+    dst[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    dst[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+  }
+}
+
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int R, int N,
+                                                           float* __restrict__ y) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= N) return;
+  float s = 0.f;
+  for (int r = 0; r < R; ++r) s += part[(size_t)r * N + col];
+  y[col] = s;
+}
+
+extern "C" size_t vst_colsum_workspace_bytes(int M, int N) {
+  if (M <= 0 || N <= 0) return 0;
+  const ColsumPlan p = colsum_plan(M, N);
+  return (size_t)p.R * N * sizeof(float);
+}
+
+extern "C" int vst_colsum(const void* x, int ldx, int M, int N, float* y, void* workspace, void* stream) {
+  if (!x || !y || !workspace || M <= 0 || N <= 0 || N % 8 || (ldx & 7) || ldx < N) return VST_ERR_ARG;
+  const ColsumPlan p = colsum_plan(M, N);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3(p.gx, p.R), dim3(256), 0, s, (const bf16_t*)x, ldx, M, N,
+                     p.rows_per_blk, (float*)workspace);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 255) / 256), dim3(256), 0, s, (const float*)workspace, p.R, N, y);
+  return ok();
+}

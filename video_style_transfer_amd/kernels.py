@@ -431,6 +431,18 @@ def group_norm_bwd(x, g, nsamples, rows_per_sample, groups, eps, gamma, beta, *,
     return dx, dgamma, dbeta
 
 
+def colsum(x, out=None):
+    """fp32 [N] column sums of a bf16 [M, N] row-major view (bias gradients), deterministic (vst_colsum)."""
+    _dev(x, BF16, "x")
+    M, N = x.shape
+    if out is None:
+        out = torch.empty(N, dtype=F32, device=x.device)
+    ws = torch.empty((_lib.load().vst_colsum_workspace_bytes(M, N) + 3) // 4, dtype=F32, device=x.device)
+    with _Rec("colsum", 0.0, 2.0 * M * N):
+        _lib.call("vst_colsum", _p(x), _ld(x), M, N, _p(out), _p(ws), _stream())
+    return out
+
+
 def geglu_bwd(p, g, out=None):
     """dp (32-interleaved like p) from p = the GEGLU projection output and g = dL/d(h * gelu(gate))."""
     _dev(p, BF16, "p")
