@@ -474,7 +474,8 @@ def test_add_row_table_and_unpack(cuda, K):
     assert torch.equal(out.cpu(), x5.to(torch.bfloat16).float())
 
 
-@pytest.mark.parametrize("rows,C,R", [(300, 320, 64), (1000, 1280, 32), (77, 640, 48), (64, 64, 16), (33, 1280, 64)])
+@pytest.mark.parametrize("rows,C,R", [(300, 320, 64), (1000, 1280, 32), (77, 640, 48), (64, 64, 16), (33, 1280, 64),
+                                      (8192, 1280, 48), (4100, 640, 16), (2049, 96, 32)])
 def test_layer_norm_lora(cuda, K, rows, C, R):
     """LayerNorm + UnZipLoRA down-projection in one pass: y = LN(x) (bf16), u = y @ A^T."""
     g = torch.Generator().manual_seed(rows + C + R)
