@@ -530,7 +530,7 @@ def test_unet_training_step_grads_vs_oracle(cuda, config):
 
 
 @pytest.mark.parametrize("M,N,ld", [(512, 512, 512), (65536, 1280, 1280), (1000, 64, 72), (3, 8, 8),
-                                    (16384, 2560, 3840)])
+                                    (16384, 2560, 3840), (262144, 320, 320), (131072, 2560, 2560), (70000, 40, 40)])
 def test_colsum(cuda, M, N, ld):
     """vst_colsum (bias gradients db = g^T 1) against an fp64 column sum; deterministic (two calls and a captured
     replay bit for bit equal)."""

@@ -613,21 +613,24 @@ extern "C" int vst_softmax_rows(const float* S, int lds, int rows, int n, float 
 extern "C" const char* vst_version(void) { return "vst-hip 0.1 gfx950"; }
 
 // ---- column sums (training path: bias gradients db = g^T 1) ------------------------------------------------------
-// bf16 [M, N] row-major view -> fp32 [N], deterministic and graph-safe: pass 1 writes one fp32 partial row per
-// row block (lane = 8-column chunk, 16-B loads; the block's 4 waves stride the rows and are combined in LDS in wave
-// order), pass 2 sums the partial rows in row-block order.  No atomics and no memset, so a captured HIP graph
-// replays it bit for bit; and no fp32 copy of g (torch's g.float().sum(0) writes and re-reads one).
+// bf16 [M, N] row-major view -> fp32 [N], deterministic and graph-safe (no atomics, no memset; a captured HIP graph
+// replays it bit for bit; torch's g.float().sum(0) also writes and re-reads an fp32 copy of g):
+//   pass 1: R row blocks x (N/512) column blocks; lane = 8-column chunk (16-B loads, 4 rows in flight per lane), the
+//           4 waves stride the block's rows and are combined in LDS in wave order -> part1 [R][N];
+//   pass 2: part1 summed in groups of 32 rows (unrolled) -> part2 [ceil(R/32)][N];
+//   pass 3: part2 summed (<= 32 rows) -> y.  Every pass has fixed summation order and short dependent chains.
 namespace {
 struct ColsumPlan {
-  int gx, R, rows_per_blk;
+  int gx, R, rows_per_blk, R2;
 };
 ColsumPlan colsum_plan(int M, int N) {
   ColsumPlan p;
   p.gx = (N / 8 + 63) / 64;
   int R = (2048 + p.gx - 1) / p.gx;                       // ~2048 workgroups in pass 1
-  R = std::max(1, std::min(R, (M + 63) / 64));            // >= 64 rows per block
+  R = std::max(1, std::min(std::min(R, 1024), (M + 63) / 64));  // >= 64 rows per block, R2 <= 32
   p.rows_per_blk = ((M + R - 1) / R + 3) / 4 * 4;
   p.R = (M + p.rows_per_blk - 1) / p.rows_per_blk;
+  p.R2 = (p.R + 31) / 32;
   return p;
 }
 }  // namespace
@@ -678,27 +681,39 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const bf16_t* __res
   }
 }
 
-__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int R, int N,
-                                                           float* __restrict__ y) {
+// y[g][col] = sum of rows 32g .. min(R, 32g + 32) of part[R][N] (in order); grid (ceil(N/256), ceil(R/32))
+__global__ __launch_bounds__(256) void colsum_rows32_kernel(const float* __restrict__ part, int R, int N,
+                                                            float* __restrict__ y) {
   const int col = blockIdx.x * 256 + threadIdx.x;
   if (col >= N) return;
-  float s = 0.f;
-  for (int r = 0; r < R; ++r) s += part[(size_t)r * N + col];
-  y[col] = s;
+  const int r0 = blockIdx.y * 32, n = min(32, R - r0);
+  const float* src = part + (size_t)r0 * N + col;
+  float v[32];
+#pragma unroll
+  for (int r = 0; r < 32; ++r) v[r] = r < n ? src[(size_t)r * N] : 0.f;
+#pragma unroll
+  for (int w = 16; w > 0; w >>= 1)
+#pragma unroll
+    for (int r = 0; r < w; ++r) v[r] += v[r + w];  // fixed pairwise tree
+  y[(size_t)blockIdx.y * N + col] = v[0];
 }
 
 extern "C" size_t vst_colsum_workspace_bytes(int M, int N) {
   if (M <= 0 || N <= 0) return 0;
   const ColsumPlan p = colsum_plan(M, N);
-  return (size_t)p.R * N * sizeof(float);
+  return ((size_t)p.R + p.R2) * N * sizeof(float);
 }
 
 extern "C" int vst_colsum(const void* x, int ldx, int M, int N, float* y, void* workspace, void* stream) {
   if (!x || !y || !workspace || M <= 0 || N <= 0 || N % 8 || (ldx & 7) || ldx < N) return VST_ERR_ARG;
   const ColsumPlan p = colsum_plan(M, N);
   hipStream_t s = (hipStream_t)stream;
+  float* part1 = (float*)workspace;
+  float* part2 = part1 + (size_t)p.R * N;
   hipLaunchKernelGGL(colsum_partial_kernel, dim3(p.gx, p.R), dim3(256), 0, s, (const bf16_t*)x, ldx, M, N,
-                     p.rows_per_blk, (float*)workspace);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 255) / 256), dim3(256), 0, s, (const float*)workspace, p.R, N, y);
+                     p.rows_per_blk, part1);
+  hipLaunchKernelGGL(colsum_rows32_kernel, dim3((N + 255) / 256, p.R2), dim3(256), 0, s, (const float*)part1, p.R, N,
+                     part2);
+  hipLaunchKernelGGL(colsum_rows32_kernel, dim3((N + 255) / 256, 1), dim3(256), 0, s, (const float*)part2, p.R2, N, y);
   return ok();
 }
