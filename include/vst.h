@@ -9,7 +9,8 @@
  *     except none at all — workspaces are caller-provided (see *_workspace_bytes);
  *   - activations are token-major NHWC: row = (frame * H*W + pixel), C contiguous;
  *   - `stream` is a hipStream_t; every call is asynchronous on it and graph-capturable;
- *   - return 0 (VST_OK) on success, 1 for a bad argument, 2 for a launch failure.
+ *   - return 0 (VST_OK) on success, 1 for a bad argument, 2 for a launch failure, 3 for a
+ *     supported-shape refusal (vst_gemm_lora only).
  */
 #ifndef VST_H
 #define VST_H
@@ -38,6 +39,24 @@ int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int K1, const 
                 void* C, int ldc, int epilogue, int tile, int splits, void* workspace, size_t ws_bytes,
                 void* stream);
 size_t vst_gemm_workspace_bytes(int M, int N, int K);
+
+/* Fused base + LoRA projection with the LoRA down-projection computed INSIDE the GEMM:
+ *   C = [x | bf16(x.Acat^T)] . W^T (+bias) (+R),  W = [W_base | V] of width ldw >= K + P,
+ * where Acat [P][K] (row stride ld_acat, zero rows past the real rank) holds the stacked down
+ * factors (UnZipLoRA: [A_c; A_s]) and V's column block [g*group_r, (g+1)*group_r) carries the up
+ * factors (s.(B (.) merger)) of the output columns n with n / group_n == g (q/k/v stacked: group_n =
+ * C, group_r = 2r).  The 8-phase kernel accumulates u = x.Acat^T from the x tiles it already
+ * streams, rounds it to bf16 (the reference's rounding point of the down output) and adds u.V^T
+ * as one extra k-step: no separate pass over x (replaces the down half of
+ * UnZipLoRALinearLayerInfer.forward, unziplora_unet/unziplora_linear_layer.py:298-346, inside
+ * LoRACompatibleLinear.forward, unziplora_unet/lora_linear.py:74-81).  Returns 3
+ * (VST_ERR_UNSUPPORTED) when the shape is not on the 8-phase kernel or a tile would need u columns
+ * outside one 16-aligned block; vst_gemm_lora_supported answers that without a launch (0, or the
+ * tile width 256 / 192 it uses). */
+int vst_gemm_lora(const void* x, int ldx, const void* Acat, int ld_acat, int P, int group_n, int group_r,
+                  const void* W, int ldw, int M, int N, int K, const float* bias, const void* R, int ldr,
+                  void* C, int ldc, void* stream);
+int vst_gemm_lora_supported(int M, int N, int K, int P, int group_n, int group_r);
 
 /* Diagnostics: short name of the kernel (tile shape, epilogue, split-K) that a vst_gemm_ex
  * (kind 0 linear, 1 GEGLU) or vst_conv3x3_ex (kind 2, kind 3 = Cin not a multiple of 64) call with

@@ -40,6 +40,23 @@ def test_bad_arguments_rejected_without_gpu():
                                          0.125, 1, None) == 1  # no lse
 
 
+def test_gemm_lora_policy_without_gpu():
+    """vst_gemm_lora_supported (host policy, no launch): the SDXL UnZipLoRA r=8 projections run the down-projection
+    inside the 8-phase GEMM; a tile that straddles two u blocks, or a rank wider than one block, is refused."""
+    from video_style_transfer_amd import _lib
+    lib = _lib.load()
+    q = lib.vst_gemm_lora_supported
+    assert q(8192, 1280, 1280, 32, 1280, 16) == 192   # to_out / attn2 q at 16x16
+    assert q(8192, 3840, 1280, 64, 1280, 16) == 256   # attn1 q/k/v at 16x16
+    assert q(32768, 640, 640, 32, 640, 16) == 192     # to_out at 32x32
+    assert q(32768, 1920, 640, 64, 640, 16) == 0      # q/k boundary inside a 256-wide tile
+    assert q(8192, 1280, 1280, 32, 1280, 32) == 0     # r = 16 UnZipLoRA: 32 u columns per projection
+    assert q(1024, 1280, 1280, 32, 1280, 16) == 0     # grid too small for the 8-phase kernel
+    # a refused shape returns status 3 from the launch entry as well, before touching the pointers
+    assert lib.vst_gemm_lora(1, 1280, 1, 640, 64, 640, 16, 1, 704, 32768, 1920, 640, None, None, 0, 1, 1920,
+                             None) == 3
+
+
 @pytest.mark.parametrize("cfgname", ["tiny", "sdxl"])
 def test_param_inventory_matches_module_tree(cfgname):
     from video_style_transfer_amd.config import UNetMotionConfig

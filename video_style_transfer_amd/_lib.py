@@ -22,6 +22,8 @@ SIGNATURES = {
     "vst_gemm_ex": (_I, [_P, _I, _P, _I, _I, _P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _I, _P, _I, _I, _I, _I, _P, _S,
                          _P]),
     "vst_gemm_workspace_bytes": (_S, [_I, _I, _I]),
+    "vst_gemm_lora": (_I, [_P, _I, _P, _I, _I, _I, _I, _P, _I, _I, _I, _I, _P, _P, _I, _P, _I, _P]),
+    "vst_gemm_lora_supported": (_I, [_I, _I, _I, _I, _I, _I]),
     "vst_gemm_kernel_name": (ctypes.c_char_p, [_I, _I, _I, _I, _I, _I, _S]),
     "vst_conv3x3": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P, _I, _P, _I, _P]),
     "vst_conv3x3_ex": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _I, _P, _I, _P, _I, _I, _I, _P,
@@ -109,5 +111,6 @@ def exported_symbols() -> list[str]:
 def call(name: str, *args):
     rc = getattr(load(), name)(*args)
     if rc != 0:
-        raise VstError(f"{name} failed with status {rc} ({'bad argument' if rc == 1 else 'launch failure'})")
+        why = {1: "bad argument", 2: "launch failure", 3: "unsupported shape"}.get(rc, "error")
+        raise VstError(f"{name} failed with status {rc} ({why})")
     return rc

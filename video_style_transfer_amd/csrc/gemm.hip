@@ -554,6 +554,7 @@ static void choose(int M, int N, int K, int geglu, int conv, size_t ws_bytes, in
 
 int launch_gemm_ring(const GemmArgs& a, int amode, int epi, int tile, int splits, hipStream_t s);
 int launch_gemm_p8(const GemmArgs& a, int epi, int bn, hipStream_t s);
+int launch_gemm_p8_lora(const GemmArgs& a, int bn, hipStream_t s);
 
 // 8-phase 256x256x64 kernel (gemm_p8.hip) for plain / LoRA-augmented projections and GEGLU (see p8_auto).
 static int gemm_p8_env() {
@@ -745,6 +746,61 @@ extern "C" size_t vst_gemm_workspace_bytes(int M, int N, int K) {
   int tile = 0, splits = 0;
   choose(M, N, K, 0, 0, (size_t)-1, tile, splits);
   return splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
+}
+
+// ---- fused base + LoRA projection with the down-projection inside the 8-phase GEMM (gemm_p8.hip LORA) ----
+// VST_LORA_INGEMM=0 turns it off (the host then runs the separate down-projection pass, A/B).
+static bool lora_ingemm_env() {
+  static const int v = [] {
+    const char* e = getenv("VST_LORA_INGEMM");
+    return e ? atoi(e) : 1;
+  }();
+  return v != 0;
+}
+
+// 0 = not supported (the host falls back to u = x.Acat^T + vst_gemm_ex), else the 8-phase tile width (256 / 192).
+// Every tile's output columns must need u columns inside one 16-aligned block of 16.
+static int lora_ingemm_bn(int M, int N, int K, int P, int gn, int gr) {
+  if (!lora_ingemm_env() || M <= 0 || N <= 0 || K < 128 || (K & 7) || P <= 0 || (P & 15) || P > 256 || gn <= 0 ||
+      gr <= 0 || N % gn || (N / gn) * gr > P)
+    return 0;
+  if (!p8_auto(M, N, K, false)) return 0;
+  const int bn = p8_bn192(M, N, false) ? 192 : 256;
+  for (int n0 = 0; n0 < N; n0 += bn) {
+    const int g0 = n0 / gn, g1 = (std::min(n0 + bn, N) - 1) / gn;
+    const int lo = (g0 * gr) & ~15, hi = (g1 + 1) * gr;
+    if (hi > lo + 16 || lo + 16 > P) return 0;
+  }
+  return bn;
+}
+
+extern "C" int vst_gemm_lora_supported(int M, int N, int K, int P, int group_n, int group_r) {
+  return lora_ingemm_bn(M, N, K, P, group_n, group_r);
+}
+
+extern "C" int vst_gemm_lora(const void* x, int ldx, const void* Acat, int ld_acat, int P, int group_n, int group_r,
+                             const void* W, int ldw, int M, int N, int K, const float* bias, const void* R, int ldr,
+                             void* C, int ldc, void* stream) {
+  if (!x || !Acat || !W || !C || M <= 0 || N <= 0 || K <= 0) return VST_ERR_ARG;
+  if ((ldx & 7) || (ld_acat & 7) || (ldw & 7) || (ldc & 7) || ldx < K || ld_acat < K || ldw < K + P) return VST_ERR_ARG;
+  if (R && ((ldr & 7) || ldr < N)) return VST_ERR_ARG;
+  const int bn = lora_ingemm_bn(M, N, K, P, group_n, group_r);
+  if (!bn) return VST_ERR_UNSUPPORTED;
+  GemmArgs a{};
+  a.A1 = (const bf16_t*)x; a.A2 = nullptr; a.lda1 = ldx; a.lda2 = 0; a.K1 = K;
+  a.Wt = (const bf16_t*)W; a.ldw = ldw; a.M = M; a.N = N; a.K = K;
+  a.bias = bias; a.R = (const bf16_t*)R; a.ldr = ldr; a.C = (bf16_t*)C; a.ldc = ldc;
+  a.a1_bytes = clamp_bytes(((size_t)(M - 1) * ldx + K) * 2);
+  a.w_bytes = clamp_bytes(((size_t)(N - 1) * ldw + K) * 2);
+  a.wtail_bytes = clamp_bytes(((size_t)(N - 1) * ldw + K + P) * 2);
+  a.r_bytes = R ? clamp_bytes(((size_t)(M - 1) * ldr + N) * 2) : 0;
+  a.la = (const bf16_t*)Acat; a.lda_la = ld_acat; a.la_p = P; a.la_gn = group_n; a.la_gr = group_r;
+  a.la_bytes = clamp_bytes((size_t)P * ld_acat * 2);
+  a.stride = 1; a.splits = 1;
+  a.p8_bn = bn;
+  a.ablate = 0;
+  a.group_m = 0;
+  return launch_gemm_p8_lora(a, bn, (hipStream_t)stream);
 }
 
 // Name of the kernel a vst_gemm_ex / vst_conv3x3_ex call with these arguments launches (the

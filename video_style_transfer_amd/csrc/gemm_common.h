@@ -29,6 +29,12 @@ struct GemmArgs {
   float* sk_ws;
   int* sk_flags;
   uint32_t a1_bytes, a2_bytes, w_bytes, r_bytes;
+  // in-GEMM LoRA down-projection (gemm_p8.hip LORA, vst_gemm_lora): Acat [la_p][K] bf16 (row stride lda_la); the
+  // output columns of group g = n / la_gn use u columns [g la_gr, (g + 1) la_gr), whose up-projection sits in W's
+  // columns K + that range (ldw >= K + la_p); wtail_bytes covers those columns
+  const bf16_t* la;
+  int lda_la, la_p, la_gn, la_gr;
+  uint32_t la_bytes, wtail_bytes;
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) {

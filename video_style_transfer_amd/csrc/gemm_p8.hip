@@ -43,8 +43,12 @@ struct P8Cfg {  // the epilogue's view of the tile (same wave tiling as RingCfg<
   static constexpr int BUF = 3 * SLOT + SLOT_B1;
   static constexpr int EPI_BYTES = BM * (BN * 2 + 16);
   static constexpr int LDS = 2 * BUF > EPI_BYTES ? 2 * BUF : EPI_BYTES;
+  // LORA: two 2-KiB Acat slots ([16 u columns][64 k] per k-tile) + 1 KiB sink for the waves without a piece, then
+  // the tile's up-projection columns V [BN rows][16] (32-B rows), staged once in the prologue
+  static constexpr int LORA_OFF = 2 * BUF, V_OFF = 2 * BUF + 5 * 1024, LORA_END = V_OFF + 256 * 32;
+  static constexpr int LDS_LORA = LORA_END > EPI_BYTES ? LORA_END : EPI_BYTES;
   static_assert(BN == 256 || BN == 192, "tile width");
-  static_assert(LDS <= 160 * 1024, "LDS budget");
+  static_assert(LDS <= 160 * 1024 && LDS_LORA <= 160 * 1024, "LDS budget");
 };
 
 template <int N>
@@ -85,12 +89,23 @@ __device__ __forceinline__ void p8_barrier() {
 // their partial slot, then raise their flag (agent-scope release).  The owner adds the partials in workgroup order
 // (deterministic), clears the flags for the next launch, and runs the epilogue.  Only owners wait, and only on
 // higher-numbered workgroups that wait on nobody, and the grid is at most one workgroup per CU: no cycle.
-template <int EPI, bool SK, int BN>
+//
+// LORA (vst_gemm_lora, UnZipLoRA / LoRA projections): the down-projection u = x . Acat^T is accumulated inside the
+// k-loop from the A fragments already in registers, so no separate pass over x produces it.  Each k-tile also
+// stages Acat's 16 u columns of this tile ([16][64] bf16, one extra DMA per wave issued with slot Amq0: waves 0-1
+// move the two 1-KiB pieces, the others a zero piece into a sink, so every wave's vmcnt counts stay uniform); in I0
+// and I1 every wave adds one 16-row block of u (row block wc of the current row quadrant: 2 MFMAs each).  After the
+// loop u is rounded to bf16 (the reference's rounding point of lora_layer's down output), exchanged through LDS and
+// multiplied by the tile's up-projection columns of W (K + ub0 ...) as one extra 16x16x32 step per accumulator —
+// the same operands, in the same order, as the [x | u] . [W | V]^T k-tile it replaces.
+template <int EPI, bool SK, int BN, bool LORA = false>
 __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using Cfg = P8Cfg<BN>;
   static_assert(!SK || BN == 256, "stream-K partial slots are 256 x 256");
   static_assert(EPI != 1 || BN == 256, "GEGLU needs 64-column [hidden | gate] blocks");
+  static_assert(!LORA || (!SK && EPI != 1), "in-GEMM LoRA: data-parallel tiles, linear epilogue");
+  constexpr int LX = LORA ? 1 : 0;  // the Acat DMA in the vmcnt counts
   constexpr int SLOT = Cfg::SLOT, BUF = Cfg::BUF, RB1 = Cfg::RB1, NJ1 = Cfg::NJ1, NPB1 = Cfg::NPB1;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -124,7 +139,19 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   const int PB = wid;
   uint32_t base1[4][NPC], base2[2][NPC];
   int c8[4][NPC];
+  const auto rl = make_rsrc(LORA ? p.la : p.Wt, LORA ? p.la_bytes : 0u);
+  int ub0 = 0, lc8 = 0;          // LORA: the tile's first u column (16-aligned); this lane's Acat chunk * 8
+  uint32_t lbase = (uint32_t)kOOB;  // LORA: this lane's Acat source row / chunk (waves 0-1)
+  int n0_tile = 0;
   auto setup_tile = [&](int m0, int n0) {
+    n0_tile = n0;
+    if constexpr (LORA) {
+      ub0 = __builtin_amdgcn_readfirstlane(((n0 / p.la_gn) * p.la_gr) & ~15);
+      const int r = 8 * wid + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      lc8 = c * 8;
+      lbase = wid < 2 ? (uint32_t)((ub0 + r) * p.lda_la + c * 8) * 2u : (uint32_t)kOOB;
+    }
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -186,7 +213,21 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     }
   };
 
+  // LORA: Acat columns of k-tile kt into its slot (buffer kt & 1); waves 2-7 write a zero piece into the sink
+  auto dma_lora = [&](int kt, int kend, bool checked) {
+    if constexpr (LORA) {
+      char* dst = wid < 2 ? smem + Cfg::LORA_OFF + (kt & 1) * 2048 + wid * 1024 : smem + Cfg::LORA_OFF + 4096;
+      const int k0 = kt * 64;
+      const bool kin = wid < 2 && (!checked || (kt < kend && k0 + lc8 < p.K));
+      p8_dma16(rl, dst, kin ? (int)(lbase + (uint32_t)k0 * 2u) : kOOB);
+    }
+  };
+
   f32x4 acc[8][Cfg::NJ];
+  f32x4 acc_u[2];   // LORA: u of row block wc of row quadrants 0 / 1 (this wave's row half)
+  bf16x8 fl[2];     // LORA: Acat fragments of the current k-tile (16 u columns x 2 k-halves)
+  bf16x8 fu[2];     // LORA: A fragments of row block wc of the current row quadrant (a copy of fa[wc], read
+                    // separately so the u MFMAs index no register array by the runtime wc)
   bf16x8 fa[4][2];         // A fragments of the current row quadrant (mq): 4 x 16 rows x 2 k-halves
   bf16x8 fb0[2][2], fb1[2][2];  // W fragments of column quadrants nq0 / nq1
 #ifdef VST_P8_TRACE
@@ -200,6 +241,10 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int h = 0; h < 2; ++h) fa[i][h] = *reinterpret_cast<const bf16x8*>(S + p8_off(wr * 64 + i * 16 + fr, h * 4 + fq));
+    if constexpr (LORA) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) fu[h] = *reinterpret_cast<const bf16x8*>(S + p8_off(wr * 64 + wc * 16 + fr, h * 4 + fq));
+    }
   };
   auto read_b = [&](int buf, int nq, bf16x8 (&fb)[2][2]) {
     if (abl & 16) return;
@@ -209,6 +254,17 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     for (int j = 0; j < (nq == 0 ? 2 : NJ1); ++j)
 #pragma unroll
       for (int h = 0; h < 2; ++h) fb[j][h] = *reinterpret_cast<const bf16x8*>(S + p8_off(wc * rb + j * 16 + fr, h * 4 + fq));
+  };
+  auto read_l = [&](int buf) {
+    if constexpr (LORA) {
+      const char* S = smem + Cfg::LORA_OFF + buf * 2048;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) fl[h] = *reinterpret_cast<const bf16x8*>(S + p8_off(fr, h * 4 + fq));
+    }
+  };
+  // LORA: u rows of row block wc of the current row quadrant
+  auto lora_mfma = [&](f32x4& au, int h) {
+    if constexpr (LORA) au = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fl[h], fu[h], au, 0, 0, 0);
   };
 #define VST_P8_QUAD(MQ, NQ, FB)                                                                        \
   if (!(abl & 2)) {                                                                                  \
@@ -223,15 +279,23 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < Cfg::NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc_u[0] = acc_u[1] = f32x4{0.f, 0.f, 0.f, 0.f};
     // Three barrier intervals per k-tile: I0 = {read Amq0, Bnq0} | Q(0,0) + Q(0,1) (32 MFMAs, fb1 = Bnq1(t) read in
     // I2 of t-1); I1 = {read Amq1} | Q(1,1); I2 = {read Bnq1(t+1)} | Q(1,0).  (Four phases of 16 MFMAs, one per
     // quadrant, measured 0.3 ms per step slower: 8 barriers per k-tile instead of 6, profiles/r2_ab_p8_3ph.txt.)  A slot read in interval I is refilled
     // in interval I+2 (both halves' reads retired), and waited for in the interval before its first read:
     //   I0(t): wait Amq1(t), issue Amq1(t+1);  I1(t): wait Bnq1(t+1), issue Bnq1(t+2);
     //   I2(t): wait Amq0/Bnq0(t+1), issue Amq0/Bnq0(t+2).   (2 DMAs per slot per wave)
-    dma_slot(0, kb, ke); dma_slot(2, kb, ke); dma_slot(3, kb, ke);
-    dma_slot(1, kb, ke); dma_slot(3, kb + 1, ke); dma_slot(0, kb + 1, ke); dma_slot(2, kb + 1, ke);
-    p8_vmwait<6 + NPB1>();  // Amq0, Bnq0, Bnq1 of kb landed
+    if constexpr (LORA) {  // V [BN][16] of this tile (older than every slot DMA: the first wait below covers it)
+      const int row = wid * 32 + (lane >> 1), n = n0_tile + row;
+      const bool ok = row < BN && n < p.N;
+      p8_dma16(make_rsrc(p.Wt, p.wtail_bytes), smem + Cfg::V_OFF + wid * 1024,
+               ok ? (int)(((uint32_t)n * p.ldw + p.K + ub0 + 8 * (lane & 1)) * 2u) : kOOB);
+    }
+    dma_slot(0, kb, ke); dma_lora(kb, ke, true); dma_slot(2, kb, ke); dma_slot(3, kb, ke);
+    dma_slot(1, kb, ke); dma_slot(3, kb + 1, ke); dma_slot(0, kb + 1, ke); dma_lora(kb + 1, ke, true);
+    dma_slot(2, kb + 1, ke);
+    p8_vmwait<6 + NPB1 + LX>();  // Amq0, (Acat,) Bnq0, Bnq1 of kb landed
     p8_barrier();
     VST_P8_STAMP(1)
     read_b(kb & 1, 1, fb1);
@@ -246,23 +310,29 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       // I0
       read_a(buf, 0);
       read_b(buf, 0, fb0);
-      if (!(abl & 4)) p8_vmwait<4 + NPB1>();  // Amq1(t) landed
+      read_l(buf);
+      if (!(abl & 4)) p8_vmwait<4 + NPB1 + LX>();  // Amq1(t) landed
       dma(1, t + 1);
       p8_barrier();
+      lora_mfma(acc_u[0], 0);
       VST_P8_QUAD(0, 0, fb0)
       VST_P8_QUAD(0, 1, fb1)
+      lora_mfma(acc_u[0], 1);
       p8_barrier();
       // I1
       read_a(buf, 1);
-      if (!(abl & 4)) p8_vmwait<6>();  // Bnq1(t+1) landed
+      if (!(abl & 4)) p8_vmwait<6 + LX>();  // Bnq1(t+1) landed
       dma(3, t + 2);
       p8_barrier();
+      lora_mfma(acc_u[1], 0);
       VST_P8_QUAD(1, 1, fb1)
+      lora_mfma(acc_u[1], 1);
       p8_barrier();
       // I2
       read_b(buf ^ 1, 1, fb1);
       if (!(abl & 4)) p8_vmwait<2 + NPB1>();  // Amq0(t+1), Bnq0(t+1) landed
       dma(0, t + 2);
+      dma_lora(t + 2, ke, !FAST);
       dma(2, t + 2);
       p8_barrier();
       VST_P8_QUAD(1, 0, fb0)
@@ -285,6 +355,36 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     setup_tile(m0, n0);
     run_segment(0, nk);
     VST_P8_STAMP(2)
+    if constexpr (LORA) {
+      // u (bf16) -> LDS [256 rows][16 columns] (the drained ring), then acc += u . V^T over the 32-wide window
+      // (columns 16-31 zero: the [x | u] k-tile's second u half), V = W[n][K + ub0 ...]
+      char* U = smem;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        u32x2 v;
+        v[0] = pack2bf(acc_u[q][0], acc_u[q][1]);
+        v[1] = pack2bf(acc_u[q][2], acc_u[q][3]);
+        *reinterpret_cast<u32x2*>(U + (wr * 128 + q * 64 + wc * 16 + fr) * 32 + fq * 8) = v;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      const bf16x8 zero8 = {};
+      bf16x8 fv[Cfg::NJ];
+#pragma unroll
+      for (int j = 0; j < Cfg::NJ; ++j) {
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + Cfg::V_OFF + (wc * Cfg::WN + j * 16 + fr) * 32 + (fq & 1) * 16);
+        fv[j] = fq < 2 ? v : zero8;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        bf16x8 fu = *reinterpret_cast<const bf16x8*>(U + (wr * 128 + i * 16 + fr) * 32 + (fq & 1) * 16);
+        fu = fq < 2 ? fu : zero8;
+#pragma unroll
+        for (int j = 0; j < Cfg::NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fv[j], fu, acc[i][j], 0, 0, 0);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // every wave's u reads done before the epilogue stages the tile over them
+    }
     tile_epilogue<Cfg, EPI>(p, smem, m0, n0, acc, wr, wc);
 #ifdef VST_P8_TRACE
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -370,17 +470,24 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   }
 }
 
-template <int EPI, bool SK, int BN>
+template <int EPI, bool SK, int BN, bool LORA = false>
 static int launch_p8_epi(const GemmArgs& a, hipStream_t s) {
   static bool attr = false;
+  constexpr int lds = LORA ? P8Cfg<BN>::LDS_LORA : P8Cfg<BN>::LDS;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_p8_kernel<EPI, SK, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              P8Cfg<BN>::LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_p8_kernel<EPI, SK, BN, LORA>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              lds);
     attr = true;
   }
   const int nwg = SK ? a.sk_grid : ((a.M + 255) / 256) * ((a.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_p8_kernel<EPI, SK, BN>), dim3(nwg), dim3(512), P8Cfg<BN>::LDS, s, a);
+  hipLaunchKernelGGL((gemm_p8_kernel<EPI, SK, BN, LORA>), dim3(nwg), dim3(512), lds, s, a);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+}
+
+// in-GEMM LoRA down-projection (a.la set): epilogue 0 (bias / residual), bn 256 or 192
+int launch_gemm_p8_lora(const GemmArgs& a, int bn, hipStream_t s) {
+  if (!a.la || a.sk_grid > 0) return VST_ERR_ARG;
+  return bn == 192 ? launch_p8_epi<0, false, 192, true>(a, s) : launch_p8_epi<0, false, 256, true>(a, s);
 }
 
 // epi: 0 bias / row bias / residual, 1 GEGLU, 3 bias + GELU; bn: 256 or 192 (not with GEGLU or stream-K)

@@ -116,3 +116,4 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 #define VST_OK 0
 #define VST_ERR_ARG 1
 #define VST_ERR_LAUNCH 2
+#define VST_ERR_UNSUPPORTED 3

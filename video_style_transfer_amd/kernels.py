@@ -148,6 +148,56 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
     return out
 
 
+_LORA_BN = {}
+
+
+def gemm_lora_tile(M, N, K, P, group_n, group_r):
+    """Tile width (256 / 192) of the in-GEMM LoRA projection (vst_gemm_lora) for this shape, 0 = not supported
+    (the caller then runs the down-projection as its own pass).  Host-side policy only; no launch."""
+    key = (M, N, K, P, group_n, group_r)
+    bn = _LORA_BN.get(key)
+    if bn is None:
+        bn = _LORA_BN[key] = int(_lib.load().vst_gemm_lora_supported(M, N, K, P, group_n, group_r))
+    return bn
+
+
+def linear_lora(x: torch.Tensor, w: torch.Tensor, a: torch.Tensor, group_n: int, group_r: int,
+                bias: torch.Tensor | None = None, *, residual: torch.Tensor | None = None,
+                out: torch.Tensor | None = None, r_alg: int | None = None) -> torch.Tensor:
+    """out = [x | bf16(x @ a^T)] @ w^T + bias (+ residual), the down-projection computed inside the GEMM
+    (vst_gemm_lora).  w: [N, K + P] = [W | V], a: [P, K]; output columns n use u columns of group n // group_n."""
+    _dev(x, BF16, "x")
+    _dev(w, BF16, "w")
+    _dev(a, BF16, "a")
+    M, K = x.shape
+    N = w.shape[0]
+    P = a.shape[0]
+    if a.shape[1] != K or w.shape[1] != K + P:
+        raise _lib.VstError(f"linear_lora: x {tuple(x.shape)} a {tuple(a.shape)} w {tuple(w.shape)}")
+    if out is None:
+        out = torch.empty((M, N), dtype=BF16, device=x.device)
+    _dev(out, BF16, "out")
+    if out.shape != (M, N):
+        raise _lib.VstError(f"linear_lora: out shape {tuple(out.shape)} != {(M, N)}")
+    if bias is not None and (bias.dtype != F32 or bias.numel() != N or not bias.is_cuda):
+        raise _lib.VstError("linear_lora: bias must be fp32 [N] on device")
+    if residual is not None:
+        _dev(residual, BF16, "residual")
+        if residual.shape != (M, N):
+            raise _lib.VstError("linear_lora: residual shape mismatch")
+    bn = gemm_lora_tile(M, N, K, P, group_n, group_r)
+    if not bn:
+        raise _lib.VstError(f"linear_lora: shape M={M} N={N} K={K} P={P} groups ({group_n}, {group_r}) unsupported")
+    r = P if r_alg is None else r_alg
+    # algorithmic work: base + up-projection (as the unfused "gemm_lora" counts it) + the down-projection once
+    flops = 2.0 * M * N * (K + r) + 2.0 * M * K * r
+    nbytes = 2.0 * (M * K + N * (K + r) + r * K + M * N * (2 if residual is not None else 1))
+    with _Rec("gemm_lora", flops, nbytes, lambda: f"gemm_p8<256x{bn},lora>", (M, N, K + P)):
+        _lib.call("vst_gemm_lora", _p(x), _ld(x), _p(a), _ld(a), P, group_n, group_r, _p(w), _ld(w), M, N, K,
+                  _p(bias), _p(residual), 0 if residual is None else _ld(residual), _p(out), _ld(out), _stream())
+    return out
+
+
 def conv3x3(x1: torch.Tensor, nimg: int, H: int, W: int, w: torch.Tensor, bias: torch.Tensor | None, *,
             x2: torch.Tensor | None = None, stride: int = 1, upsample: bool = False,
             row_bias: torch.Tensor | None = None, row_bias_div: int = 1, residual: torch.Tensor | None = None,

@@ -98,6 +98,8 @@ class ProjOps:
     k1: int
     n: int
     r: int = 0                       # real (unpadded) low-rank width
+    gn: int = 0                      # output columns per projection when every projection has the same width and
+    gr: int = 0                      # rank (u columns [g gr, (g+1) gr) feed rows [g gn, (g+1) gn)); 0 = irregular
 
 
 def _linear_parts(lin):
@@ -171,16 +173,30 @@ def build_ops(lins: Sequence[nn.Module], scale: float = 1.0, mode: Optional[str]
         if any(b is not None for b in bs):
             bias = torch.cat([b if b is not None else torch.zeros(w.shape[0], device=dev) for w, b in zip(Ws, bs)])
             bias = bias.contiguous()
-        ops = ProjOps(W_all.to(torch.bfloat16).contiguous(), a_bf, bias, K1, N, R if a_bf is not None else 0)
+        gn = gr = 0
+        if a_bf is not None and len({w.shape[0] for w in Ws}) == 1 and \
+                len({0 if a is None else a.shape[0] for a in As}) == 1:
+            gn, gr = Ws[0].shape[0], As[0].shape[0]
+        ops = ProjOps(W_all.to(torch.bfloat16).contiguous(), a_bf, bias, K1, N, R if a_bf is not None else 0, gn, gr)
     if cacheable:
         cache[key] = (skey, ops)
     return ops
 
 
+def lora_in_gemm(ops: ProjOps, rows: int) -> bool:
+    """True when run_ops(x, ops) over `rows` rows computes the LoRA down-projection inside the projection GEMM
+    (K.linear_lora), so a producer need not emit u = x @ ops.a^T (LayerNorm.run_lora checks this first)."""
+    return ops.a is not None and ops.gn > 0 and \
+        K.gemm_lora_tile(rows, ops.n, ops.k1, ops.a.shape[0], ops.gn, ops.gr) > 0
+
+
 def run_ops(x2d: torch.Tensor, ops: ProjOps, residual=None, out=None, geglu=False, u=None) -> torch.Tensor:
-    """`u` = x2d @ ops.a^T when the producer already computed it (K.layer_norm_lora)."""
+    """`u` = x2d @ ops.a^T when the producer already computed it (K.layer_norm_lora); otherwise the down-projection
+    runs inside the projection GEMM where the shape allows (K.linear_lora), else as its own skinny GEMM."""
     if ops.a is None:
         return K.linear(x2d, ops.w, ops.bias, residual=residual, out=out, geglu=geglu)
+    if u is None and not geglu and lora_in_gemm(ops, x2d.shape[0]):
+        return K.linear_lora(x2d, ops.w, ops.a, ops.gn, ops.gr, ops.bias, residual=residual, out=out, r_alg=ops.r)
     if u is None:
         u = K.linear(x2d, ops.a, kind="gemm_lora_down", alg_n=ops.r)
     return K.linear(x2d, ops.w, ops.bias, x2=u, residual=residual, out=out, geglu=geglu, alg_k2=ops.r)

@@ -31,7 +31,7 @@ from torch import nn
 from . import kernels as K
 from .attention_processor import Attention, input_lora_ops
 from .config import UNetMotionConfig
-from .lora_linear import LoRACompatibleLinear, build_ops, run_ops
+from .lora_linear import LoRACompatibleLinear, build_ops, lora_in_gemm, run_ops
 from .weights import sinusoid_table
 
 BF16 = torch.bfloat16
@@ -70,7 +70,7 @@ class LayerNorm(nn.LayerNorm):
         """(LN(x), LN(x) @ ops.a^T or None): the LoRA down-projection fused into the normalisation pass when
         the consuming projections carry one and the shapes suit the fused kernel."""
         C = x.shape[1]
-        if ops is None or ops.a is None or ops.a.shape[0] > 64 or C % 32 or C > 1280:
+        if ops is None or ops.a is None or ops.a.shape[0] > 64 or C % 32 or C > 1280 or lora_in_gemm(ops, x.shape[0]):
             return self.run(x), None
         return K.layer_norm_lora(x, f32(self.weight), f32(self.bias), self.eps, ops.a, r_alg=ops.r)
 
