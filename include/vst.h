@@ -10,7 +10,7 @@
  *   - activations are token-major NHWC: row = (frame * H*W + pixel), C contiguous;
  *   - `stream` is a hipStream_t; every call is asynchronous on it and graph-capturable;
  *   - return 0 (VST_OK) on success, 1 for a bad argument, 2 for a launch failure, 3 for a
- *     supported-shape refusal (vst_gemm_lora only).
+ *     supported-shape refusal (vst_gemm_lora, vst_gemm_cross_attention).
  */
 #ifndef VST_H
 #define VST_H
@@ -57,6 +57,21 @@ int vst_gemm_lora(const void* x, int ldx, const void* Acat, int ld_acat, int P, 
                   const void* W, int ldw, int M, int N, int K, const float* bias, const void* R, int ldr,
                   void* C, int ldc, void* stream);
 int vst_gemm_lora_supported(int M, int N, int K, int P, int group_n, int group_r);
+
+/* attn2 of a BasicTransformerBlock as ONE launch: the q projection (vst_gemm_lora when Acat != NULL, else
+ * [x].[W]^T) with the cross-attention over the text tokens as its epilogue,
+ *   O[m, 64h .. 64h+63] = softmax(q_h K_h^T * scale) V_h,  q = bf16(x.W^T (+bias) (+LoRA)),
+ * K/V rows [(frame / kv_div) * Nk + key] (frame = m / Nq; nkv_rows rows in all, row stride ldkv, head h at
+ * columns 64h).  q never reaches HBM.  Replaces to_q (lora_linear.py:74-81) + F.scaled_dot_product_attention
+ * (animatediff/attention_processor.py:78-80) of AnimateDiffAttnProcessor2_0 with encoder_hidden_states.
+ * Needs Nq % 256 == 0, Nk <= 80, N % 64 == 0 and the 8-phase kernel's 256x192 tiles for (M, N); returns 3
+ * (VST_ERR_UNSUPPORTED) otherwise.  _supported answers without a launch (lora: Acat will be non-NULL). */
+int vst_gemm_cross_attention(const void* x, int ldx, const void* Acat, int ld_acat, int P, int group_n, int group_r,
+                             const void* W, int ldw, const float* bias, int M, int N, int K, const void* Kt,
+                             const void* Vt, int ldkv, int nkv_rows, int Nq, int Nk, int kv_div, float scale, void* O,
+                             int ldo, void* stream);
+int vst_gemm_cross_attention_supported(int M, int N, int K, int lora, int P, int group_n, int group_r, int Nq,
+                                       int Nk);
 
 /* Diagnostics: short name of the kernel (tile shape, epilogue, split-K) that a vst_gemm_ex
  * (kind 0 linear, 1 GEGLU) or vst_conv3x3_ex (kind 2, kind 3 = Cin not a multiple of 64) call with

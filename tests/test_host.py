@@ -52,6 +52,13 @@ def test_gemm_lora_policy_without_gpu():
     assert q(32768, 1920, 640, 64, 640, 16) == 0      # q/k boundary inside a 256-wide tile
     assert q(8192, 1280, 1280, 32, 1280, 32) == 0     # r = 16 UnZipLoRA: 32 u columns per projection
     assert q(1024, 1280, 1280, 32, 1280, 16) == 0     # grid too small for the 8-phase kernel
+    # attn2 as one launch (q projection + text cross-attention epilogue): 256-row tiles inside a frame, <= 80 keys
+    xq = lib.vst_gemm_cross_attention_supported
+    assert xq(8192, 1280, 1280, 1, 32, 1280, 16, 256, 77) == 1    # 16x16 level, UnZipLoRA r=8
+    assert xq(8192, 1280, 1280, 0, 0, 0, 0, 256, 77) == 1         # no LoRA (configs[1])
+    assert xq(32768, 640, 640, 1, 32, 640, 16, 1024, 77) == 1     # 32x32 level
+    assert xq(8192, 1280, 1280, 1, 32, 1280, 16, 320, 77) == 0    # tiles would straddle frames
+    assert xq(8192, 1280, 1280, 1, 32, 1280, 16, 256, 81) == 0    # more keys than the LDS holds
     # a refused shape returns status 3 from the launch entry as well, before touching the pointers
     assert lib.vst_gemm_lora(1, 1280, 1, 640, 64, 640, 16, 1, 704, 32768, 1920, 640, None, None, 0, 1, 1920,
                              None) == 3

@@ -118,17 +118,33 @@ class AnimateDiffAttnProcessor2_0:
             be, L, D = enc.shape
             if batch % be:
                 raise ValueError(f"encoder batch {be} does not divide hidden batch {batch}")
-            q = run_ops(x, build_ops([attn.to_q], s), u=lora_u)
+            q_ops = build_ops([attn.to_q], s)
             kv = _text_kv(attn, enc, s)
             if hd != 64:
                 raise NotImplementedError("spatial cross-attention kernel is specialised for head_dim 64 (SDXL)")
-            o = K.spatial_attention(q, kv[:, :inner], kv[:, inner:], batch, heads, N, L, batch // be, scale=hd ** -0.5)
+            if lora_u is None and _cross_fusable(q_ops, batch * N, N, L):
+                # q projection (+ in-GEMM UnZipLoRA) and the text cross-attention as one launch: q stays on chip
+                o = K.linear_cross_attention(x, q_ops.w, q_ops.a, q_ops.gn, q_ops.gr, q_ops.bias, kv[:, :inner],
+                                             kv[:, inner:], Nq=N, Nk=L, kv_div=batch // be, scale=hd ** -0.5,
+                                             r_alg=q_ops.r)
+            else:
+                q = run_ops(x, q_ops, u=lora_u)
+                o = K.spatial_attention(q, kv[:, :inner], kv[:, inner:], batch, heads, N, L, batch // be,
+                                        scale=hd ** -0.5)
         res2d = None if fused_residual is None else fused_residual.reshape(batch * N, -1)
         out = run_ops(o, build_ops([attn.to_out[0]], s), residual=res2d)
         out = out.view(batch, N, -1)
         if input_ndim == 4:
             out = out.transpose(-1, -2).reshape(b4, c4, h4, w4)
         return _finish(attn, out, hidden_states)
+
+
+def _cross_fusable(ops, M: int, Nq: int, Nk: int) -> bool:
+    """attn2's q projection ops (as build_ops made them) and the cross-attention fit vst_gemm_cross_attention."""
+    lora = ops.a is not None
+    if lora and ops.gn <= 0:
+        return False
+    return K.cross_attention_fusable(M, ops.n, ops.k1, lora, 0 if not lora else ops.a.shape[0], ops.gn, ops.gr, Nq, Nk)
 
 
 def input_lora_ops(attn, self_attention: bool, scale: float = 1.0):

@@ -555,6 +555,7 @@ static void choose(int M, int N, int K, int geglu, int conv, size_t ws_bytes, in
 int launch_gemm_ring(const GemmArgs& a, int amode, int epi, int tile, int splits, hipStream_t s);
 int launch_gemm_p8(const GemmArgs& a, int epi, int bn, hipStream_t s);
 int launch_gemm_p8_lora(const GemmArgs& a, int bn, hipStream_t s);
+int launch_gemm_p8_xattn(const GemmArgs& a, hipStream_t s);
 
 // 8-phase 256x256x64 kernel (gemm_p8.hip) for plain / LoRA-augmented projections and GEGLU (see p8_auto).
 static int gemm_p8_env() {
@@ -801,6 +802,57 @@ extern "C" int vst_gemm_lora(const void* x, int ldx, const void* Acat, int ld_ac
   a.ablate = 0;
   a.group_m = 0;
   return launch_gemm_p8_lora(a, bn, (hipStream_t)stream);
+}
+
+// ---- attn2: q projection (+ in-GEMM LoRA) with the cross-attention over the text tokens as its epilogue ----
+// VST_XATTN_FUSE=0 turns it off (the host then runs the q GEMM and vst_spatial_attention, A/B).
+static bool xattn_env() {
+  static const int v = [] {
+    const char* e = getenv("VST_XATTN_FUSE");
+    return e ? atoi(e) : 1;
+  }();
+  return v != 0;
+}
+
+static bool xattn_ok(int M, int N, int K, const void* Acat, int P, int gn, int gr, int Nq, int Nk) {
+  if (!xattn_env() || M <= 0 || N <= 0 || N % 64 || K < 128 || (K & 7) || Nq <= 0 || Nq % 256 || M % Nq || Nk < 1 ||
+      Nk > 80)
+    return false;
+  if (!p8_auto(M, N, K, false) || !p8_bn192(M, N, false)) return false;
+  return !Acat || lora_ingemm_bn(M, N, K, P, gn, gr) == 192;
+}
+
+extern "C" int vst_gemm_cross_attention_supported(int M, int N, int K, int lora, int P, int group_n, int group_r,
+                                                  int Nq, int Nk) {
+  return xattn_ok(M, N, K, lora ? (const void*)1 : nullptr, P, group_n, group_r, Nq, Nk) ? 1 : 0;
+}
+
+extern "C" int vst_gemm_cross_attention(const void* x, int ldx, const void* Acat, int ld_acat, int P, int group_n,
+                                        int group_r, const void* W, int ldw, const float* bias, int M, int N, int K,
+                                        const void* Kt, const void* Vt, int ldkv, int nkv_rows, int Nq, int Nk,
+                                        int kv_div, float scale, void* O, int ldo, void* stream) {
+  if (!x || !W || !Kt || !Vt || !O || M <= 0 || N <= 0 || K <= 0 || kv_div <= 0 || nkv_rows <= 0) return VST_ERR_ARG;
+  if ((ldx & 7) || (ldw & 7) || (ldo & 7) || (ldkv & 7) || ldx < K || ldo < N || ldkv < N) return VST_ERR_ARG;
+  if (Acat && ((ld_acat & 7) || ld_acat < K || ldw < K + P)) return VST_ERR_ARG;
+  if (!Acat && ldw < K) return VST_ERR_ARG;
+  if (!xattn_ok(M, N, K, Acat, P, group_n, group_r, Nq, Nk)) return VST_ERR_UNSUPPORTED;
+  if ((M / Nq - 1) / kv_div >= nkv_rows / Nk) return VST_ERR_ARG;  // every frame's text batch inside K/V
+  GemmArgs a{};
+  a.A1 = (const bf16_t*)x; a.lda1 = ldx; a.K1 = K;
+  a.Wt = (const bf16_t*)W; a.ldw = ldw; a.M = M; a.N = N; a.K = K;
+  a.bias = bias; a.C = (bf16_t*)O; a.ldc = ldo;
+  a.a1_bytes = clamp_bytes(((size_t)(M - 1) * ldx + K) * 2);
+  a.w_bytes = clamp_bytes(((size_t)(N - 1) * ldw + K) * 2);
+  if (Acat) {
+    a.wtail_bytes = clamp_bytes(((size_t)(N - 1) * ldw + K + P) * 2);
+    a.la = (const bf16_t*)Acat; a.lda_la = ld_acat; a.la_p = P; a.la_gn = group_n; a.la_gr = group_r;
+    a.la_bytes = clamp_bytes((size_t)P * ld_acat * 2);
+  }
+  a.xa_k = (const bf16_t*)Kt; a.xa_v = (const bf16_t*)Vt; a.xa_ldkv = ldkv; a.xa_nk = Nk; a.xa_nq = Nq;
+  a.xa_kvdiv = kv_div; a.xa_scale_log2 = scale * 1.4426950408889634f;
+  a.xa_kv_bytes = clamp_bytes(((size_t)(nkv_rows - 1) * ldkv + N) * 2);
+  a.stride = 1; a.splits = 1; a.p8_bn = 192;
+  return launch_gemm_p8_xattn(a, (hipStream_t)stream);
 }
 
 // Name of the kernel a vst_gemm_ex / vst_conv3x3_ex call with these arguments launches (the

@@ -35,6 +35,14 @@ struct GemmArgs {
   const bf16_t* la;
   int lda_la, la_p, la_gn, la_gr;
   uint32_t la_bytes, wtail_bytes;
+  // cross-attention epilogue (gemm_p8.hip EPI 4, vst_gemm_cross_attention): the GEMM output is the q of a
+  // BasicTransformerBlock's attn2; instead of storing it, each tile writes softmax(q K^T scale) V of its heads over
+  // the xa_nk text keys of text batch (m / xa_nq) / xa_kvdiv (K/V rows [batch * xa_nk + key], row stride xa_ldkv)
+  const bf16_t* xa_k;
+  const bf16_t* xa_v;
+  int xa_ldkv, xa_nk, xa_nq, xa_kvdiv;
+  float xa_scale_log2;
+  uint32_t xa_kv_bytes;
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) {

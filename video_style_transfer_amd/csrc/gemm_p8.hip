@@ -22,6 +22,7 @@
 // (counted s_waitcnt vmcnt, 2 DMAs per slot per wave) in the interval before its first read (RAW).  Past the last
 // k-tile the same DMAs are issued with out-of-range offsets (zeros), so the counts are the same in every interval;
 // they are drained before the epilogue reuses the LDS.
+#include "attn_common.h"
 #include "gemm_common.h"
 #include "gemm_epilogue.h"
 
@@ -82,6 +83,205 @@ __device__ __forceinline__ void p8_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// EPI 4: cross-attention over the text tokens as the epilogue of the attn2 q projection (BasicTransformerBlock,
+// unziplora_unet/unzip_attention.py:188-212; the SDPA core of AnimateDiffAttnProcessor2_0,
+// animatediff/attention_processor.py:78-80).  A 256-row tile lies inside one frame (HW % 256 == 0) and its 192
+// columns are 3 heads of 64, so the tile holds every query of those (frame, head) pairs: the q tile is staged once
+// in LDS as bf16 (the reference's rounding point of to_q's output), the heads' K/V (<= 80 text keys each, zero rows
+// past Nk) are brought in by LDS-DMA, and each wave computes 32 queries x 3 heads of softmax(q K^T / 8) V with
+// S^T = K.Q^T and O^T = V^T.P^T on MFMA (the spatial_attn_kernel layouts, one pass over all keys).  q is never
+// written to HBM and read back, and the separate attention launch disappears.  LDS: 256 x 400 B of q + 3 x 20 KiB of
+// K/V = 160 KiB exactly.
+template <class Cfg>
+__device__ __forceinline__ void xattn_epilogue(const GemmArgs& p, char* smem, const int m0, const int n0,
+                                               f32x4 (&acc)[Cfg::MI][Cfg::NJ], const int wr, const int wc) {
+  constexpr int BM = Cfg::BM, BN = Cfg::BN, NH = BN / 64;
+  constexpr int LROW = BN * 2 + 16;
+  constexpr int KVH = 80 * 128;  // one operand of one head: [80 keys][64 d] bf16, 128-B rows
+  constexpr int KV_OFF = BM * LROW;
+  static_assert(BN == 192 && KV_OFF + NH * 2 * KVH <= 160 * 1024, "q tile + 3 heads of K/V in 160 KiB");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int bkv = __builtin_amdgcn_readfirstlane((m0 / p.xa_nq) / p.xa_kvdiv);
+  const int h0 = n0 / 64, nh = min(NH, (p.N - n0) / 64);
+  // K/V pieces first (their latency overlaps the q staging): 20 per head (10 x 8 rows of K, then of V), the tile
+  // swizzles k_off / v_off applied to the source chunk (the DMA writes lane-linearly); keys >= Nk read as zeros
+  {
+    const auto rk = make_rsrc(p.xa_k, p.xa_kv_bytes), rv = make_rsrc(p.xa_v, p.xa_kv_bytes);
+    for (int pc = wid; pc < NH * 20; pc += 8) {
+      const int hh = pc / 20, q = pc - hh * 20, op = q / 10, r8 = q - op * 10;
+      const int row = r8 * 8 + (lane >> 3), slot = lane & 7;
+      const int c = op == 0 ? slot ^ ((row >> 1) & 7) : slot ^ (((row >> 1) & 3) << 1);
+      const bool ok = hh < nh && row < p.xa_nk;
+      const int off = ok ? ((bkv * p.xa_nk + row) * p.xa_ldkv + (h0 + hh) * 64 + c * 8) * 2 : kOOB;
+      char* dst = smem + KV_OFF + hh * 2 * KVH + op * KVH + r8 * 1024;
+      if (op == 0) p8_dma16(rk, dst, off); else p8_dma16(rv, dst, off);
+    }
+  }
+  // q (+ bias) -> bf16 tile [256][BN] in LDS
+  {
+    const int lrow0 = wr * Cfg::WM + fr, lcol0 = wc * Cfg::WN + 4 * fq;
+#pragma unroll
+    for (int j = 0; j < Cfg::NJ; ++j) {
+      f32x4 b4 = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (p.bias) {
+        const int n = n0 + lcol0 + j * 16;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) b4[e] = n + e < p.N ? p.bias[n + e] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < Cfg::MI; ++i) {
+        const f32x4 a4 = acc[i][j] + b4;
+        u32x2 v;
+        v[0] = pack2bf(a4[0], a4[1]);
+        v[1] = pack2bf(a4[2], a4[3]);
+        *reinterpret_cast<u32x2*>(smem + (lrow0 + i * 16) * LROW + (lcol0 + j * 16) * 2) = v;
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  // wave w: queries [32 w, 32 w + 32) of the tile, every head of it
+  const float sl2 = p.xa_scale_log2;
+  const int qbase = 32 * wid;
+  int voff[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) {
+    const int r0 = fq * 4 + (fr >> 2), col = db * 16 + (fr & 3) * 4;
+    voff[db] = v_off(r0, col >> 3) + (col & 7) * 2;
+  }
+  for (int hh = 0; hh < nh; ++hh) {
+    const char* Ks = smem + KV_OFF + hh * 2 * KVH;
+    const char* Vs = Ks + KVH;
+    bf16x8 qf[2][2];  // Q^T fragments: lane (q, g) holds Q[q][32 kk + 8 g .. +7]
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        qf[qb][kk] = *reinterpret_cast<const bf16x8*>(smem + (qbase + qb * 16 + fr) * LROW + (hh * 64 + kk * 32 + fq * 8) * 2);
+    f32x4 s[5][2];  // S^T: lane col q, rows key = 16 kt + 4 g + i
+#pragma unroll
+    for (int kt = 0; kt < 5; ++kt) {
+      bf16x8 kf[2];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) kf[kk] = *reinterpret_cast<const bf16x8*>(Ks + k_off(kt * 16 + fr, kk * 4 + fq));
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        f32x4 a{0.f, 0.f, 0.f, 0.f};
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[0], qf[qb][0], a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[1], qf[qb][1], a, 0, 0, 0);
+        s[kt][qb] = a;
+      }
+    }
+    // softmax in the standalone kernel's order (spatial_attn_kernel, PRE tiles of 64 keys): keys 0-63 with their own
+    // max, then keys 64-79 with an online rescale, P rounded to bf16 unnormalised, 1/l at the end -- the same bf16
+    // roundings as the two-launch path, so the fused and unfused attn2 agree to fp32 summation order
+    float m0r[2], lrun[2], alpha[2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (kt * 16 + fq * 4 + i >= p.xa_nk) s[kt][qb][i] = -INFINITY;
+          mx = fmaxf(mx, s[kt][qb][i]);
+        }
+      mx = group_max(mx);
+      m0r[qb] = mx;
+      const float mb = mx * sl2;
+      float ls = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float pv = fast_exp2(s[kt][qb][i] * sl2 - mb);
+          s[kt][qb][i] = pv;
+          ls += pv;
+        }
+      lrun[qb] = ls;
+      // second key tile (64-79 live): its max, the rescale of the first tile's state, its P
+      float mx1 = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (64 + fq * 4 + i >= p.xa_nk) s[4][qb][i] = -INFINITY;
+        mx1 = fmaxf(mx1, s[4][qb][i]);
+      }
+      mx1 = group_max(mx1);
+      const float mnew = fmaxf(mx, mx1);
+      alpha[qb] = fast_exp2((mx - mnew) * sl2);
+      const float mb1 = mnew * sl2;
+      float ls1 = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float pv = fast_exp2(s[4][qb][i] * sl2 - mb1);
+        s[4][qb][i] = pv;
+        ls1 += pv;
+      }
+      lrun[qb] = lrun[qb] * alpha[qb] + ls1;
+    }
+    (void)m0r;
+    // O^T = V^T P^T: keys 0-31 and 32-63 as two 32-deep steps (P blocks 2 st, 2 st + 1), rescaled by alpha, then
+    // keys 64-79 as one 16-deep step
+    f32x4 o[4][2];
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) o[db][qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      bf16x8 pf[2];
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+        pf[qb] = pack_p8(s[2 * st][qb][0], s[2 * st][qb][1], s[2 * st][qb][2], s[2 * st][qb][3], s[2 * st + 1][qb][0],
+                         s[2 * st + 1][qb][1], s[2 * st + 1][qb][2], s[2 * st + 1][qb][3]);
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const bf16x8 vf = cat_tr(ds_read_tr(Vs + voff[db] + st * 4096), ds_read_tr(Vs + voff[db] + st * 4096 + 2048));
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) o[db][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qb], o[db][qb], 0, 0, 0);
+      }
+    }
+    {
+      s16x4 p4[2];
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        const u32x2 w{pack2bf(s[4][qb][0], s[4][qb][1]), pack2bf(s[4][qb][2], s[4][qb][3])};
+        p4[qb] = __builtin_bit_cast(s16x4, w);
+#pragma unroll
+        for (int db = 0; db < 4; ++db) o[db][qb] *= alpha[qb];
+      }
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const s16x4 vf = ds_read_tr(Vs + voff[db] + 2 * 4096);
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) o[db][qb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vf, p4[qb], o[db][qb], 0, 0, 0);
+      }
+    }
+    float inv[2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      float l = lrun[qb];
+      l += __shfl_xor(l, 16);
+      l += __shfl_xor(l, 32);
+      inv[qb] = 1.0f / l;
+    }
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const int m = m0 + qbase + qb * 16 + fr;
+      if (m >= p.M) continue;
+      bf16_t* orow = p.C + (size_t)m * p.ldc + n0 + hh * 64;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const f32x4 v = o[db][qb] * inv[qb];
+        const u32x2 w{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+        *reinterpret_cast<u32x2*>(orow + db * 16 + fq * 4) = w;
+      }
+    }
+  }
+}
+
 // SK = stream-K: one workgroup per CU, each taking an equal share of the (tile, k-tile) iteration space, so grids of
 // 160 tiles (M = 8192, N = 1280: 62 % of the CUs under plain tiling) keep every CU busy.  A tile split between
 // workgroups is finished by its OWNER (the workgroup that runs its k-tile 0; that is always the owner's last
@@ -105,6 +305,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   static_assert(!SK || BN == 256, "stream-K partial slots are 256 x 256");
   static_assert(EPI != 1 || BN == 256, "GEGLU needs 64-column [hidden | gate] blocks");
   static_assert(!LORA || (!SK && EPI != 1), "in-GEMM LoRA: data-parallel tiles, linear epilogue");
+  static_assert(EPI != 4 || (!SK && BN == 192), "cross-attention epilogue: 192-column tiles (3 heads)");
   constexpr int LX = LORA ? 1 : 0;  // the Acat DMA in the vmcnt counts
   constexpr int SLOT = Cfg::SLOT, BUF = Cfg::BUF, RB1 = Cfg::RB1, NJ1 = Cfg::NJ1, NPB1 = Cfg::NPB1;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -385,7 +586,8 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // every wave's u reads done before the epilogue stages the tile over them
     }
-    tile_epilogue<Cfg, EPI>(p, smem, m0, n0, acc, wr, wc);
+    if constexpr (EPI == 4) xattn_epilogue<Cfg>(p, smem, m0, n0, acc, wr, wc);
+    else tile_epilogue<Cfg, EPI>(p, smem, m0, n0, acc, wr, wc);
 #ifdef VST_P8_TRACE
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -473,7 +675,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
 template <int EPI, bool SK, int BN, bool LORA = false>
 static int launch_p8_epi(const GemmArgs& a, hipStream_t s) {
   static bool attr = false;
-  constexpr int lds = LORA ? P8Cfg<BN>::LDS_LORA : P8Cfg<BN>::LDS;
+  constexpr int lds = EPI == 4 ? 160 * 1024 : (LORA ? P8Cfg<BN>::LDS_LORA : P8Cfg<BN>::LDS);
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gemm_p8_kernel<EPI, SK, BN, LORA>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               lds);
@@ -488,6 +690,12 @@ static int launch_p8_epi(const GemmArgs& a, hipStream_t s) {
 int launch_gemm_p8_lora(const GemmArgs& a, int bn, hipStream_t s) {
   if (!a.la || a.sk_grid > 0) return VST_ERR_ARG;
   return bn == 192 ? launch_p8_epi<0, false, 192, true>(a, s) : launch_p8_epi<0, false, 256, true>(a, s);
+}
+
+// cross-attention epilogue (a.xa_k set), 256x192 tiles, with or without the in-GEMM LoRA
+int launch_gemm_p8_xattn(const GemmArgs& a, hipStream_t s) {
+  if (!a.xa_k || !a.xa_v || a.sk_grid > 0) return VST_ERR_ARG;
+  return a.la ? launch_p8_epi<4, false, 192, true>(a, s) : launch_p8_epi<4, false, 192, false>(a, s);
 }
 
 // epi: 0 bias / row bias / residual, 1 GEGLU, 3 bias + GELU; bn: 256 or 192 (not with GEGLU or stream-K)

@@ -198,6 +198,64 @@ def linear_lora(x: torch.Tensor, w: torch.Tensor, a: torch.Tensor, group_n: int,
     return out
 
 
+_XATTN_OK = {}
+
+
+def cross_attention_fusable(M, N, K, lora, P, group_n, group_r, Nq, Nk):
+    """Whether vst_gemm_cross_attention runs attn2 (q projection + text cross-attention) as one launch for this shape
+    (host policy only, no launch)."""
+    key = (M, N, K, bool(lora), P, group_n, group_r, Nq, Nk)
+    ok = _XATTN_OK.get(key)
+    if ok is None:
+        ok = _XATTN_OK[key] = bool(_lib.load().vst_gemm_cross_attention_supported(M, N, K, int(bool(lora)), P,
+                                                                                   group_n, group_r, Nq, Nk))
+    return ok
+
+
+def linear_cross_attention(x: torch.Tensor, w: torch.Tensor, a: torch.Tensor | None, group_n: int, group_r: int,
+                           bias: torch.Tensor | None, k: torch.Tensor, v: torch.Tensor, *, Nq: int, Nk: int,
+                           kv_div: int, scale: float, out: torch.Tensor | None = None,
+                           r_alg: int | None = None) -> torch.Tensor:
+    """o = softmax(q_h k_h^T scale) v_h per head (head_dim 64) with q = [x | bf16(x a^T)] w^T + bias computed in the
+    same launch (vst_gemm_cross_attention); k / v: [text_batches * Nk, N] views (row stride >= N), the text batch of
+    frame f = (m // Nq) is f // kv_div."""
+    _dev(x, BF16, "x")
+    _dev(w, BF16, "w")
+    _dev(k, BF16, "k")
+    _dev(v, BF16, "v")
+    M, K = x.shape
+    N = w.shape[0]
+    P = 0 if a is None else a.shape[0]
+    if a is not None:
+        _dev(a, BF16, "a")
+        if a.shape[1] != K or w.shape[1] != K + P:
+            raise _lib.VstError(f"linear_cross_attention: x {tuple(x.shape)} a {tuple(a.shape)} w {tuple(w.shape)}")
+    elif w.shape[1] != K:
+        raise _lib.VstError(f"linear_cross_attention: x {tuple(x.shape)} w {tuple(w.shape)}")
+    if k.shape != v.shape or k.shape[1] != N or k.shape[0] % Nk or _ld(k) != _ld(v):
+        raise _lib.VstError(f"linear_cross_attention: k {tuple(k.shape)} v {tuple(v.shape)} N={N} Nk={Nk}")
+    if M % Nq or (M // Nq - 1) // kv_div >= k.shape[0] // Nk:
+        raise _lib.VstError(f"linear_cross_attention: M={M} Nq={Nq} kv_div={kv_div} vs {k.shape[0] // Nk} text rows")
+    if bias is not None and (bias.dtype != F32 or bias.numel() != N or not bias.is_cuda):
+        raise _lib.VstError("linear_cross_attention: bias must be fp32 [N] on device")
+    if not cross_attention_fusable(M, N, K, a is not None, P, group_n, group_r, Nq, Nk):
+        raise _lib.VstError(f"linear_cross_attention: M={M} N={N} K={K} Nq={Nq} Nk={Nk} not fusable")
+    if out is None:
+        out = torch.empty((M, N), dtype=BF16, device=x.device)
+    _dev(out, BF16, "out")
+    if out.shape != (M, N):
+        raise _lib.VstError(f"linear_cross_attention: out shape {tuple(out.shape)} != {(M, N)}")
+    r = P if r_alg is None else r_alg
+    flops = 2.0 * M * N * (K + r) + 2.0 * M * K * r + 4.0 * M * N * Nk
+    nbytes = 2.0 * (M * K + N * (K + r) + r * K + 2 * (k.shape[0]) * N + M * N)
+    sym = "gemm_p8<256x192,lora,xattn>" if a is not None else "gemm_p8<256x192,xattn>"
+    with _Rec("gemm_xattn", flops, nbytes, lambda: sym, (M, N, K + P)):
+        _lib.call("vst_gemm_cross_attention", _p(x), _ld(x), _p(a), 0 if a is None else _ld(a), P, group_n, group_r,
+                  _p(w), _ld(w), _p(bias), M, N, K, _p(k), _p(v), _ld(k), k.shape[0], Nq, Nk, kv_div, float(scale),
+                  _p(out), _ld(out), _stream())
+    return out
+
+
 def conv3x3(x1: torch.Tensor, nimg: int, H: int, W: int, w: torch.Tensor, bias: torch.Tensor | None, *,
             x2: torch.Tensor | None = None, stride: int = 1, upsample: bool = False,
             row_bias: torch.Tensor | None = None, row_bias_div: int = 1, residual: torch.Tensor | None = None,
