@@ -1,5 +1,5 @@
 #!/bin/bash
-# SQ counter passes over isolated 8-phase GEMM shapes (tools/gemm_ablate.py): MFMA busy vs wave cycles, LDS
+# SQ counter passes over isolated 8-phase GEMM shapes (tools/p8_one.py): MFMA busy vs wave cycles, LDS
 # activity and bank conflicts.  Via gpurun; one --pmc pass per counter group.
 set -o pipefail
 export TMPDIR=/tmp
@@ -9,7 +9,7 @@ P2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES 
 i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
-  SHAPES="proj1280 ff1_1280_geglu qkv1280" timeout -s KILL 90 rocprofv3 --pmc $P --kernel-trace --output-format csv -d gpurun_out/gpmc$i -o g -- python -u tools/gemm_ablate.py > gpurun_out/gpmc$i.out 2> gpurun_out/gpmc$i.err || { tail -5 gpurun_out/gpmc$i.err; exit 1; }
+  timeout -s KILL 90 rocprofv3 --pmc $P --kernel-trace --output-format csv -d gpurun_out/gpmc$i -o g -- python -u tools/p8_one.py proj1280 geglu1280 qkv1280 proj320 > gpurun_out/gpmc$i.out 2> gpurun_out/gpmc$i.err || { tail -5 gpurun_out/gpmc$i.err; exit 1; }
   F=$(find gpurun_out/gpmc$i -name '*counter_collection.csv' | head -1)
   python - "$F" <<'PY' | tee -a gpurun_out/p8_pmc.txt
 import csv, sys, collections
