@@ -7,7 +7,9 @@ mkdir -p gpurun_out
 for tag in "$@"; do
   base=$(echo $tag | sed 's/[0-9]*$//')  # trailing digits: repeats of the same build
   unset VST_GEMM_P8
-  unset VST_LN_GENERIC VST_P8_BN VST_CFG_STREAMS VST_LORA_INGEMM VST_XATTN_FUSE
+  unset VST_LN_GENERIC VST_P8_BN VST_CFG_STREAMS VST_LORA_INGEMM VST_XATTN_FUSE VST_LN_RIT
+  if [ "$base" = lnritx ]; then export VST_LN_RIT=2; base=new; fi  # LayerNorm: 2 row passes per wave at every C
+  if [ "$base" = lnrity ]; then export VST_LN_RIT=1; base=new; fi  # LayerNorm: 1 row pass per wave at every C
   if [ "$base" = noxattn ]; then export VST_XATTN_FUSE=0; base=new; fi  # attn2 as q GEMM + attention kernel
   if [ "$base" = nolora ]; then export VST_LORA_INGEMM=0; base=new; fi  # LoRA down-projection as its own pass
   if [ "$base" = cfgstreams ]; then export VST_CFG_STREAMS=1; base=new; fi  # CFG branches on two streams (B=1 each)

@@ -900,18 +900,25 @@ extern "C" int vst_layernorm(const void* x, int ldx, int C, int rows, const floa
                      blk, 0, s, (const bf16_t*)x, ldx, C, rows, gamma, beta, eps, pe, pe_div, pe_mod, (bf16_t*)y, ldy)
   static const bool generic_only = getenv("VST_LN_GENERIC") != nullptr;  // A/B switch (tools/ab_bench.sh)
   const bool g16 = !generic_only && ((uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)pe) % 16 == 0;
-  if (g16 && C == 320) {
-    VST_LNG(8, 2);
-    return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+  // RIT = row passes per wave whose loads are all in flight before the first reduction.  C = 1280 (M = 8192 rows in the
+  // step): 1 pass, 1024 workgroups: 9.8 -> 9.2 us per launch graph-timed, step -0.15..-0.2 ms same-box
+  // (profiles/r3_ab_ln_rit.txt); VST_LN_RIT (1 / 2 / 4) overrides every width for A/B.
+  static const int rit_env = [] {
+    const char* e = getenv("VST_LN_RIT");
+    return e ? atoi(e) : 0;
+  }();
+#define VST_LNG_RIT(LPR, DEF)                                        \
+  {                                                                  \
+    const int rit = rit_env ? rit_env : (DEF);                       \
+    if (rit == 1) VST_LNG(LPR, 1);                                   \
+    else if (rit == 4) VST_LNG(LPR, 4);                              \
+    else VST_LNG(LPR, 2);                                            \
+    return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH; \
   }
-  if (g16 && C == 640) {
-    VST_LNG(16, 2);
-    return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
-  }
-  if (g16 && C == 1280) {
-    VST_LNG(32, 2);
-    return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
-  }
+  if (g16 && C == 320) VST_LNG_RIT(8, 2)
+  if (g16 && C == 640) VST_LNG_RIT(16, 2)
+  if (g16 && C == 1280) VST_LNG_RIT(32, 1)
+#undef VST_LNG_RIT
 #undef VST_LNG
 #define VST_LN(MC, R)                                                                                          \
   hipLaunchKernelGGL((layernorm_kernel<MC, R>), dim3((rows + 4 * R - 1) / (4 * R)), blk, 0, s, (const bf16_t*)x, ldx, \
