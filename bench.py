@@ -543,9 +543,29 @@ def main():
     if shard is not None and not shard.graph_capturable:
         graph_note = f"{shard.backend} collectives are not graph-capturable; eager steps"
     elif not args.no_graph:
-        # no silent eager fallback: a step (or an RCCL collective inside it) that cannot be captured fails the run,
-        # so an N-GPU line is never an uncaptured number; --no-graph measures eager launches on purpose
-        den.capture()
+        # N = 1: a step that cannot be captured fails the run.  N > 1: an RCCL collective that refuses HIP-graph capture
+        # must not cost the whole scaling line, so every rank learns whether all captured (one eager all-reduce after
+        # the attempt) and, if any failed, ALL ranks time eager steps -- reported loudly in the line ("graph": false,
+        # "note"), never silently
+        err = None
+        try:
+            den.capture()
+        except Exception as e:  # noqa: BLE001 -- re-raised at N = 1
+            if world == 1:
+                raise
+            err = e
+            den.graph = None
+            torch.cuda.synchronize()
+        if world > 1:
+            import torch.distributed as dist
+            flag = torch.tensor([0.0 if err is None else 1.0], device="cpu" if rehearsal else dev)
+            dist.all_reduce(flag)
+            if flag.item() > 0:
+                den.graph = None
+                graph_note = (f"HIP-graph capture of the frame-sharded step failed on {int(flag.item())} of {world} "
+                              f"ranks{'' if err is None else ' (' + type(err).__name__ + ': ' + str(err)[:160] + ')'}; "
+                              f"eager steps")
+                print(f"[bench] rank {rank}: {graph_note}", file=sys.stderr, flush=True)
     t_build = time.perf_counter() - t_build
 
     def one_step():
