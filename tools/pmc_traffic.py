@@ -29,10 +29,12 @@ def bench_symbol(name: str) -> str:
         tag = {("0", "0"): "", ("0", "1"): ",geglu", ("1", "0"): ",conv", ("0", "2"): ",splitk",
                ("1", "2"): ",splitk"}.get((amode, epi), f",a{amode}e{epi}")
         return f"gemm_ring<{bm}x{bn}{tag}{',streamk' if sk == 'true' else ''}>"
-    m = re.search(r"gemm_p8_kernel<(\d), (true|false)(?:, (\d+))?>", name)
+    m = re.search(r"gemm_p8_kernel<(\d), (true|false)(?:, (\d+))?(?:, (true|false))?>", name)
     if m:
-        epi, sk, bn = m.groups()
-        return f"gemm_p8<256x{bn or 256}{',geglu' if epi == '1' else ''}{',streamk' if sk == 'true' else ''}>"
+        epi, sk, bn, lora = m.groups()
+        tags = (",lora" if lora == "true" else "") + (",geglu" if epi == "1" else "") + \
+            (",xattn" if epi == "4" else "") + (",streamk" if sk == "true" else "")
+        return f"gemm_p8<256x{bn or 256}{tags}>"
     if "layernorm_lora_kernel" in name:
         return "layernorm_lora"
     for k, v in (("gemm_skinny", "gemm_skinny"), ("spatial_attn_kernel", "spatial_attn_kernel"),
