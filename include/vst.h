@@ -104,6 +104,20 @@ int vst_spatial_attention(const void* q, int ldq, const void* k, const void* v, 
 int vst_temporal_attention(const void* q, const void* k, const void* v, int ldqkv, void* o, int ldo, int nclip,
                            int F, int HW, int heads, int head_dim, float scale, void* stream);
 
+/* One attention half of a motion-module BasicTransformerBlock in ONE launch (the fused temporal block of SURVEY
+ * §8(d)):  y = x + to_out(softmax_over_frames(q k^T * scale) v),  [q | k | v] = (LayerNorm(x) + pe[frame]) . wqkv^T
+ * (+ bqkv), to_out = . wo^T + bo; token (clip b, frame f, pixel p) at row (b*F + f)*HW + p; pe: [F][C] fp32 or NULL.
+ * Replaces norm1/norm2 (+ the sinusoidal PE, animatediff/temporal_transformer.py:11-27), attn1/attn2 with the default
+ * processor and the residual add of the motion module's BasicTransformerBlock (unziplora_unet/unzip_attention.py:
+ * 150-151, 196-197; core: temporal_transformer.py:66-68).  C = 320 (the 64x64 level), 8 heads, F = 16, HW % 8 == 0;
+ * returns 3 (VST_ERR_UNSUPPORTED) otherwise, which _supported answers without a launch.  Out of place (y != x).
+ * The UNet uses it only with VST_MOTION_FUSE=1: it measured slower than the four launches. */
+int vst_motion_attention_block(const void* x, int ldx, int nclip, int F, int HW, int C, int heads, const float* gamma,
+                               const float* beta, float eps, const float* pe, const void* wqkv, int ldw,
+                               const float* bqkv, const void* wo, int ldwo, const float* bo, float scale, void* y,
+                               int ldy, void* stream);
+int vst_motion_attention_block_supported(int C, int F, int HW, int heads);
+
 /* GroupNorm (+SiLU) over NHWC samples of rows_per_sample rows; optional 2-source channel concat. */
 size_t vst_groupnorm_workspace_bytes(int nsamples, int rows_per_sample, int groups, int C);
 int vst_groupnorm(const void* x1, int ld1, int C1, const void* x2, int ld2, int C2, int nsamples,

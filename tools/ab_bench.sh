@@ -7,7 +7,8 @@ mkdir -p gpurun_out
 for tag in "$@"; do
   base=$(echo $tag | sed 's/[0-9]*$//')  # trailing digits: repeats of the same build
   unset VST_GEMM_P8
-  unset VST_LN_GENERIC VST_P8_BN VST_CFG_STREAMS VST_LORA_INGEMM VST_XATTN_FUSE VST_LN_RIT
+  unset VST_LN_GENERIC VST_P8_BN VST_CFG_STREAMS VST_LORA_INGEMM VST_XATTN_FUSE VST_LN_RIT VST_MOTION_FUSE
+  if [ "$base" = motionfuse ]; then export VST_MOTION_FUSE=1; base=new; fi  # fused motion attention blocks (opt-in)
   if [ "$base" = lnritx ]; then export VST_LN_RIT=2; base=new; fi  # LayerNorm: 2 row passes per wave at every C
   if [ "$base" = lnrity ]; then export VST_LN_RIT=1; base=new; fi  # LayerNorm: 1 row pass per wave at every C
   if [ "$base" = noxattn ]; then export VST_XATTN_FUSE=0; base=new; fi  # attn2 as q GEMM + attention kernel

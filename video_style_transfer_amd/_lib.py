@@ -33,6 +33,9 @@ SIGNATURES = {
                             _S, _P]),
     "vst_spatial_attention": (_I, [_P, _I, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _F, _P, _P]),
     "vst_temporal_attention": (_I, [_P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _F, _P]),
+    "vst_motion_attention_block": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _F, _P, _P, _I, _P, _P, _I, _P, _F, _P, _I,
+                                        _P]),
+    "vst_motion_attention_block_supported": (_I, [_I, _I, _I, _I]),
     "vst_groupnorm_workspace_bytes": (_S, [_I, _I, _I, _I]),
     "vst_groupnorm_sums": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "vst_groupnorm_apply_sums": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _P, ctypes.c_double, _F, _P, _P, _I, _P,

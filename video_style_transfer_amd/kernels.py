@@ -343,6 +343,41 @@ def temporal_attention(q, k, v, nclip, F, HW, heads, head_dim, out=None, scale=N
     return out
 
 
+def motion_block_fusable(C, F, HW, heads):
+    """vst_motion_attention_block takes this motion-module shape (host policy only)."""
+    return bool(_lib.load().vst_motion_attention_block_supported(C, F, HW, heads))
+
+
+def motion_attention_block(x, nclip, F, HW, heads, gamma, beta, eps, pe, wqkv, bqkv, wo, bo, *, scale=None, out=None):
+    """y = x + (attention over the F frames of (LayerNorm(x) * gamma + beta + pe[frame]) . wqkv^T (+ bqkv)) . wo^T + bo
+    in one launch; x: [nclip * F * HW, C] token rows (b * F + f) * HW + p."""
+    _dev(x, BF16, "x")
+    _dev(wqkv, BF16, "wqkv")
+    _dev(wo, BF16, "wo")
+    T, C = x.shape
+    if T != nclip * F * HW or wqkv.shape != (3 * C, C) or wo.shape != (C, C):
+        raise _lib.VstError(f"motion_attention_block: x {tuple(x.shape)} wqkv {tuple(wqkv.shape)} wo {tuple(wo.shape)}")
+    for n, t, k in (("gamma", gamma, C), ("beta", beta, C), ("bqkv", bqkv, 3 * C), ("bo", bo, C)):
+        if t is not None and (t.dtype != F32 or not t.is_cuda or t.numel() != k or not t.is_contiguous()):
+            raise _lib.VstError(f"motion_attention_block: {n} must be fp32 [{k}] on device")
+    if pe is not None and (pe.dtype != F32 or not pe.is_cuda or pe.shape[0] < F or pe.shape[-1] != C
+                           or not pe.is_contiguous()):
+        raise _lib.VstError("motion_attention_block: pe must be fp32 [>= F, C] on device")
+    if any(t is not None and t.data_ptr() % 16 for t in (gamma, beta, pe)):
+        raise _lib.VstError("motion_attention_block: gamma / beta / pe must be 16-byte aligned (vector loads)")
+    if out is None:
+        out = torch.empty((T, C), dtype=BF16, device=x.device)
+    _dev(out, BF16, "out")
+    D = C // heads
+    scale = D ** -0.5 if scale is None else scale
+    flops = 2.0 * T * C * 4 * C + 4.0 * T * F * C
+    with _Rec("motion_block", flops, 2.0 * (2 * T * C + 4 * C * C), lambda: "motion_attn_block_kernel", (T, 4 * C, C)):
+        _lib.call("vst_motion_attention_block", _p(x), _ld(x), nclip, F, HW, C, heads, _p(gamma), _p(beta), float(eps),
+                  _p(pe), _p(wqkv), _ld(wqkv), _p(bqkv), _p(wo), _ld(wo), _p(bo), float(scale), _p(out), _ld(out),
+                  _stream())
+    return out
+
+
 def group_norm(x1, nsamples, rows_per_sample, groups, eps, gamma, beta, *, silu=False, x2=None, out=None):
     _dev(x1, BF16, "x1")
     C = x1.shape[1] + (0 if x2 is None else x2.shape[1])

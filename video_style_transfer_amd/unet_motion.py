@@ -21,6 +21,8 @@ Block semantics (diffusers ~0.30, restated in oracle/unet.py with citations):
 """
 from __future__ import annotations
 
+import os
+
 import dataclasses
 from dataclasses import dataclass
 from typing import Optional
@@ -190,11 +192,22 @@ class BasicTransformerBlock(nn.Module):
         if temporal:
             self.pos_embed = _SinusoidalPE(dim, max_seq_length)
 
+    def _fused_motion_ops(self, C, F, HW):
+        return _fused_motion_ops_impl(self, C, F, HW)
+
     def run(self, x, nimg, N, ctx: FwdCtx):
         """x: [nimg*N, C] -> same."""
         C = x.shape[1]
         if self.temporal:
             pe = f32(self.pos_embed.pe).view(-1, C)
+            fused = self._fused_motion_ops(C, ctx.F, N)
+            if fused is not None:
+                # each attention half (norm + PE, q/k/v, frame attention, to_out, residual) as one launch
+                for norm, (qkv, o) in zip((self.norm1, self.norm2), fused):
+                    x = K.motion_attention_block(x, nimg // ctx.F, ctx.F, N, self.attn1.heads, f32(norm.weight),
+                                                 f32(norm.bias), norm.eps, pe, qkv.w, qkv.bias, o.w, o.bias)
+                n = self.norm3.run(x)
+                return self.ff.run(n, residual=x)
             kw = dict(pe=pe, pe_div=N, pe_mod=ctx.F)
             n = self.norm1.run(x, **kw)
             x = self.attn1(n.view(nimg, N, C), num_frames=ctx.F, _vst_residual=x).view(-1, C)
@@ -209,6 +222,25 @@ class BasicTransformerBlock(nn.Module):
                            **ctx.cross_kwargs).view(-1, C)
         n = self.norm3.run(x)
         return self.ff.run(n, residual=x)
+
+
+def _fused_motion_ops_impl(block, C, F, HW):
+    """[(qkv ops, out ops)] for attn1 / attn2 when vst_motion_attention_block can run them: the default processor,
+    no LoRA on any projection (temporal LoRA trains through the autograd path), the kernel's shape."""
+    from .attention_processor import AttnProcessor2_0
+    # opt-in (VST_MOTION_FUSE=1): the fused block is correct but measured slower than the four launches (DESIGN §9)
+    if os.environ.get("VST_MOTION_FUSE") != "1" or not K.motion_block_fusable(C, F, HW, block.attn1.heads):
+        return None
+    out = []
+    for attn in (block.attn1, block.attn2):
+        if type(attn.processor) is not AttnProcessor2_0 or attn.heads != block.attn1.heads:
+            return None
+        qkv = build_ops([attn.to_q, attn.to_k, attn.to_v], 1.0)
+        o = build_ops([attn.to_out[0]], 1.0)
+        if qkv.a is not None or o.a is not None or qkv.w.shape != (3 * C, C) or o.w.shape != (C, C):
+            return None
+        out.append((qkv, o))
+    return out
 
 
 class _SinusoidalPE(nn.Module):
