@@ -29,7 +29,8 @@ def bench_symbol(name: str) -> str:
         tag = {("0", "0"): "", ("0", "1"): ",geglu", ("1", "0"): ",conv", ("0", "2"): ",splitk",
                ("1", "2"): ",splitk"}.get((amode, epi), f",a{amode}e{epi}")
         return f"gemm_ring<{bm}x{bn}{tag}{',streamk' if sk == 'true' else ''}>"
-    m = re.search(r"gemm_p8_kernel<(\d), (true|false)(?:, (\d+))?(?:, (true|false))?>", name)
+    # optional 4th / 5th template arguments: LORA, PERS (the persistent variant reports under the same symbol)
+    m = re.search(r"gemm_p8_kernel<(\d), (true|false)(?:, (\d+))?(?:, (true|false))?(?:, (?:true|false))?>", name)
     if m:
         epi, sk, bn, lora = m.groups()
         tags = (",lora" if lora == "true" else "") + (",geglu" if epi == "1" else "") + \
