@@ -335,6 +335,7 @@ extern "C" int vst_motion_attention_block(const void* x, int ldx, int nclip, int
   if (!vst_motion_attention_block_supported(C, F, HW, heads)) return VST_ERR_UNSUPPORTED;
   if ((ldx & 7) || (ldw & 7) || (ldwo & 7) || (ldy & 7) || ldx < C || ldy < C || ldw < C || ldwo < C) return VST_ERR_ARG;
   if (x == y) return VST_ERR_ARG;  // the residual is re-read at the end: out of place only
+  if (((uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)pe) & 15) return VST_ERR_ARG;  // 16-B vector loads
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)motion_attn_block_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
