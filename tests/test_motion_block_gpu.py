@@ -93,3 +93,37 @@ def test_motion_block_refuses_other_shapes(cuda, K):
     x, gamma, beta, pe, wqkv, bqkv, wo, bo = _operands(1, 64, False, 1, cuda)
     with pytest.raises(_lib.VstError):
         K.motion_attention_block(x, 2, 8, 64, HEADS, gamma, beta, 1e-5, pe, wqkv, bqkv, wo, bo)
+
+
+def test_motion_module_opt_in_matches_default(cuda, K, monkeypatch):
+    """A whole MotionModule (GroupNorm, proj_in, the transformer block, proj_out) at the 64x64-level shape with the
+    fused attention halves switched on (VST_MOTION_FUSE=1) against the default four-launch path: the opt-in is a
+    drop-in for the same module tree and weights."""
+    from video_style_transfer_amd.unet_motion import FwdCtx, MotionModule
+    torch.manual_seed(5)
+    mm = MotionModule(C).to(cuda)
+    with torch.no_grad():
+        for name, p in mm.named_parameters():
+            if p.dim() == 2:
+                p.normal_(0.0, 0.4 * p.shape[1] ** -0.5)
+            elif "norm" in name and name.endswith("weight"):
+                p.normal_(1.0, 0.1)
+            else:
+                p.normal_(0.0, 0.05)
+    for p in mm.parameters():
+        p.requires_grad_(False)
+    nclip, H, W = 2, 16, 16
+    x = (torch.randn(nclip * F * H * W, C, device=cuda) * 0.7).to(torch.bfloat16)
+    ctx = FwdCtx(B=nclip, F=F, emb_silu=None, enc=None, cross_kwargs={})
+    monkeypatch.delenv("VST_MOTION_FUSE", raising=False)
+    K.profile_launches(True)
+    y_def = mm.run(x, nclip * F, H, W, ctx)
+    kinds_def = [r[0] for r in K.collect_launches()]
+    K.profile_launches(False)
+    monkeypatch.setenv("VST_MOTION_FUSE", "1")
+    K.profile_launches(True)
+    y_fused = mm.run(x, nclip * F, H, W, ctx)
+    kinds_fused = [r[0] for r in K.collect_launches()]
+    K.profile_launches(False)
+    assert "motion_block" not in kinds_def and kinds_fused.count("motion_block") == 2, (kinds_def, kinds_fused)
+    check(y_fused, y_def, 2e-3, 1e-2, "motion module fused vs default")

@@ -16,6 +16,12 @@ SHAPES = {  # name: M, N, K, geglu, tile
     "geglu1280": (8192, 10240, 1280, True, 8),
     "qkv1280": (8192, 3840, 1280, False, 8),
     "proj320": (131072, 320, 320, False, 9),
+    "qkv320_256": (131072, 960, 320, False, 8),
+    "qkv320_192": (131072, 960, 320, False, 9),
+    "qkv640_256": (32768, 1920, 640, False, 8),
+    "qkv640_192": (32768, 1920, 640, False, 9),
+    "mqkv1280_256": (8192, 3840, 1280, False, 8),
+    "mqkv1280_192": (8192, 3840, 1280, False, 9),
 }
 
 
