@@ -3,7 +3,7 @@ rocprofv3 --kernel-trace --stats): the kernel names encode the library's tile / 
 configuration, a yardstick for tuning the ring GEMM."""
 import torch
 
-SHAPES = [(8192, 3840, 1344), (8192, 1280, 5120), (32768, 640, 2560), (131072, 320, 2880), (4096, 4096, 4096)]
+SHAPES = [(8192, 10240, 1280), (8192, 1280, 5120), (8192, 3840, 1280), (32768, 5120, 640), (32768, 640, 2560), (8192, 1280, 1280)]
 
 
 def main():
