@@ -255,7 +255,7 @@ __global__ __launch_bounds__(512) void temporal_attn_kernel(
   constexpr int DB = (D + 15) / 16;  // 16-wide d blocks for O
   constexpr int NF = 16 * NT;
   constexpr int VROW = DB * 32;      // bytes per V row in LDS
-  extern __shared__ __attribute__((aligned(16))) char vsm[];  // [waves][NF * VROW]
+  extern __shared__ __attribute__((aligned(16))) char vsm[];  // [waves][NV KiB]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int unit = blockIdx.x * (blockDim.x >> 6) + wid;
   const int nunits = nclip * HW * heads;
@@ -270,14 +270,20 @@ __global__ __launch_bounds__(512) void temporal_attn_kernel(
   const auto rv = make_rsrc(V, qkv_bytes);
   auto row_of = [&](int f) { return (b * F + f) * HW + p; };
 
-  // ---- stage V rows (zero rows >= F and columns >= D) ----
-  char* vs = vsm + wid * (NF * VROW);
+  // ---- V rows into registers (zero rows >= F and columns >= D); they go to LDS after the S MFMAs, so the V, K and
+  // Q loads are in flight together (one memory round trip per wave instead of two) ----
   constexpr int CPR = VROW / 16;  // 16-B chunks per LDS row
-  for (int idx = lane; idx < NF * CPR; idx += 64) {
+  constexpr int NV = (NF * CPR + 63) / 64;
+  char* vs = vsm + wid * (NV * 1024);  // one wave's tile, padded to whole 1-KiB pieces (every lane stores)
+  u32x4 vreg[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int idx = lane + 64 * j;
     const int f = idx / CPR, c = idx - f * CPR;
-    const int off = (f < F && c * 8 < D) ? (row_of(f) * ldqkv + h * D + c * 8) * 2 : kOOB;
-    *reinterpret_cast<u32x4*>(vs + f * VROW + c * 16) = buf_load16(rv, off);
+    const int off = (idx < NF * CPR && f < F && c * 8 < D) ? (row_of(f) * ldqkv + h * D + c * 8) * 2 : kOOB;
+    vreg[j] = buf_load16(rv, off);
   }
+  __builtin_amdgcn_sched_barrier(0);  // every V load issues before the K / Q loads (the compiler sinks them otherwise)
 
   // ---- S^T = K Q^T ----
   f32x4 s[NT][NT];
@@ -301,6 +307,9 @@ __global__ __launch_bounds__(512) void temporal_attn_kernel(
 #pragma unroll
       for (int c = 0; c < NT; ++c) s[a][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[a], qf[c], s[a][c], 0, 0, 0);
   }
+#pragma unroll
+  for (int j = 0; j < NV; ++j)  // chunk idx = f * CPR + c sits at byte idx * 16; the pad chunks get zeros
+    *reinterpret_cast<u32x4*>(vs + (lane + 64 * j) * 16) = vreg[j];
   // mask keys >= F
 #pragma unroll
   for (int a = 0; a < NT; ++a)
@@ -922,7 +931,7 @@ template <int NT, int D>
 static int launch_temporal(const bf16_t* Q, const bf16_t* K, const bf16_t* V, int ld, bf16_t* O, int ldo,
                            int nclip, int F, int HW, int heads, float sl2, uint32_t bytes, hipStream_t s) {
   const int units = nclip * HW * heads;
-  constexpr int VBYTES = 16 * NT * ((D + 15) / 16) * 32;  // one wave's V tile
+  constexpr int VBYTES = (16 * NT * ((D + 15) / 16) * 32 + 1023) / 1024 * 1024;  // one wave's V tile, 1-KiB pieces
   // all heads of a (clip, pixel) in one workgroup when they fit (<= 8 waves, <= 64 KiB of V tiles), else 4 units
   const int wpg = (heads <= 8 && heads * VBYTES <= 64 * 1024) ? heads : 4;
   hipLaunchKernelGGL((temporal_attn_kernel<NT, D>), dim3((units + wpg - 1) / wpg), dim3(64 * wpg), wpg * VBYTES, s,
