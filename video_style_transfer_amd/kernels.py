@@ -365,9 +365,13 @@ def motion_attention_block(x, nclip, F, HW, heads, gamma, beta, eps, pe, wqkv, b
         raise _lib.VstError("motion_attention_block: pe must be fp32 [>= F, C] on device")
     if any(t is not None and t.data_ptr() % 16 for t in (gamma, beta, pe)):
         raise _lib.VstError("motion_attention_block: gamma / beta / pe must be 16-byte aligned (vector loads)")
+    if gamma is None or beta is None:
+        raise _lib.VstError("motion_attention_block: gamma and beta are required")
     if out is None:
         out = torch.empty((T, C), dtype=BF16, device=x.device)
     _dev(out, BF16, "out")
+    if out.shape != (T, C):
+        raise _lib.VstError(f"motion_attention_block: out shape {tuple(out.shape)} != {(T, C)}")
     D = C // heads
     scale = D ** -0.5 if scale is None else scale
     flops = 2.0 * T * C * 4 * C + 4.0 * T * F * C
