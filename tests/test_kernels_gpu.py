@@ -301,6 +301,44 @@ def test_conv3x3(cuda, K, n, Ci, Co, H, W, stride, up):
     check(out, to_nhwc(ref), name="conv")
 
 
+@pytest.mark.parametrize("M,N,Kd", [(2, 1280, 320), (2, 1280, 2816), (2, 13760, 1280), (1, 8, 8), (3, 104, 40),
+                                    (5, 640, 1288), (8, 336, 4096)])
+@pytest.mark.parametrize("epi", ["bias", "residual", "gelu", "rowbias"])
+def test_gemm_rows_small_m(cuda, K, M, N, Kd, epi):
+    """gemm_rows_kernel (M <= 8: the time-embedding MLPs, the batched time_emb_proj) vs fp32, every epilogue."""
+    g = torch.Generator().manual_seed(M * 1000 + N + Kd)
+    x, w = rnd(M, Kd, gen=g), rnd(N, Kd, scale=Kd ** -0.5, gen=g)
+    b = torch.randn(N, generator=g)
+    y = x.float() @ w.float().t() + b
+    assert K.gemm_kernel_name(M, N, Kd, 0) == "gemm_rows"
+    if epi == "bias":
+        out, ref = K.linear(x.to(cuda), w.to(cuda), b.to(cuda)), y
+    elif epi == "gelu":
+        out, ref = K.linear(x.to(cuda), w.to(cuda), b.to(cuda), act="gelu"), F.gelu(y)
+    elif epi == "residual":
+        r = rnd(M, N, gen=g)
+        out = K.linear(x.to(cuda), w.to(cuda), b.to(cuda), residual=r.to(cuda))
+        ref = y.to(torch.bfloat16).float() + r.float()
+    else:
+        rb = torch.randn(1, N, generator=g)
+        out = K.linear(x.to(cuda), w.to(cuda), b.to(cuda), row_bias=rb.to(cuda), row_bias_div=8)
+        ref = y.to(torch.bfloat16).float() + rb
+    check(out, ref, name=f"gemm_rows {M}x{N}x{Kd} {epi}")
+
+
+def test_gemm_rows_column_independent_of_n(cuda, K):
+    """The batched time_emb_proj (one GEMM over every resnet's rows) equals each resnet's own Linear bit for bit."""
+    g = torch.Generator().manual_seed(5)
+    x = rnd(2, 1280, gen=g).to(cuda)
+    w = rnd(13760, 1280, scale=1280 ** -0.5, gen=g).to(cuda)
+    b = torch.randn(13760, generator=g).to(cuda)
+    full = K.linear(x, w, b)
+    o = 0
+    for c in (320, 640, 1280, 960, 40):
+        assert torch.equal(K.linear(x, w[o:o + c], b[o:o + c]), full[:, o:o + c]), (o, c)
+        o += c
+
+
 def test_conv3x3_concat_temb_residual(cuda, K):
     g = torch.Generator().manual_seed(11)
     n, C1, C2, Co, H, W = 4, 128, 64, 128, 8, 8

@@ -41,7 +41,8 @@ def bench_symbol(name: str) -> str:
     for k, v in (("gemm_skinny", "gemm_skinny"), ("spatial_attn_kernel", "spatial_attn_kernel"),
                  ("layernorm_g_kernel", "layernorm_kernel"),
                  ("temporal_attn_kernel", "temporal_attn_kernel"), ("layernorm_kernel", "layernorm_kernel"),
-                 ("gn_", "gn_stats/gn_finalize/gn_apply"), ("gemm_kernel<2", "gemm_kernel<conv_in>")):
+                 ("gn_", "gn_stats/gn_finalize/gn_apply"), ("gemm_kernel<2", "gemm_kernel<conv_in>"),
+                 ("gemm_rows_kernel", "gemm_rows")):
         if k in name:
             return v
     return name.split("(")[0][:80]

@@ -421,6 +421,86 @@ static int launch_skinny(const GemmArgs& a, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 
+// Row-vector GEMM for M <= 8 (the time-embedding MLPs and the batched time_emb_proj of every ResnetBlock2D: M = the
+// CFG pair, unet_motion.UNetMotionModel.embed / batched_temb; diffusers TimestepEmbedding, ResnetBlock2D).  These
+// read N x K weights once to make 2 x N outputs: HBM-bound on W, nothing for MFMA to do.  The 128x128 split-K tiles
+// they used to run on spent 46 us per launch on 2 live rows of 128 (0.4 TF/s, profiles/r3s9_kernel_stats.csv).
+// A wave owns CPW output columns: lane l reads 16-B k-chunks l, l + 64, ... of each weight row (NT chunks per row in
+// flight at once) and the same chunks of the M activation rows (L1/L2 hits: every wave reads the same x), sums in
+// fp32, reduces across the wave, then the ring epilogue's rounding points: bias (+GELU) -> bf16 -> + row bias
+// + residual -> bf16.  Each output's k order is fixed by (K, lane), so a column's value does not depend on N:
+// the batched time_emb_proj equals the per-resnet Linear bit for bit.
+template <int MR>
+__global__ __launch_bounds__(256) void gemm_rows_kernel(GemmArgs p) {
+  constexpr int CPW = 2, NT = MR <= 2 ? 4 : 2;
+  const int lane = threadIdx.x & 63;
+  const int nb = (blockIdx.x * 4 + (threadIdx.x >> 6)) * CPW;
+  if (nb >= p.N) return;  // no barriers below
+  const auto ra = make_rsrc(p.A1, p.a1_bytes);
+  const auto rw = make_rsrc(p.Wt, p.w_bytes);
+  float acc[MR][CPW];
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) acc[m][c] = 0.f;
+  const int nch = p.K >> 3;
+  for (int q0 = 0; q0 < nch; q0 += 64 * NT) {
+    u32x4 wv[NT][CPW], xv[NT][MR];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int q = q0 + t * 64 + lane;
+      const bool in = q < nch;
+#pragma unroll
+      for (int c = 0; c < CPW; ++c)
+        wv[t][c] = buf_load16(rw, in && nb + c < p.N ? ((nb + c) * p.ldw + q * 8) * 2 : kOOB);
+#pragma unroll
+      for (int m = 0; m < MR; ++m) xv[t][m] = buf_load16(ra, in && m < p.M ? (m * p.lda1 + q * 8) * 2 : kOOB);
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int c = 0; c < CPW; ++c) {
+        float w8[8];
+        unpack8(wv[t][c], w8);
+#pragma unroll
+        for (int m = 0; m < MR; ++m) {
+          float x8[8];
+          unpack8(xv[t][m], x8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[m][c] = fmaf(x8[e], w8[e], acc[m][c]);
+        }
+      }
+  }
+  float v = 0.f;
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+      const float s = wave_sum(acc[m][c]);
+      if (lane == m * CPW + c) v = s;
+    }
+  const int m = lane / CPW, n = nb + lane % CPW;
+  if (lane >= MR * CPW || m >= p.M || n >= p.N) return;
+  if (p.bias) v += p.bias[n];
+  if (p.act) v = gelu_erf(v);
+  if (p.rbias || p.R) {
+    v = round_bf(v);
+    if (p.rbias) v += p.rbias[(size_t)(m / p.rbias_div) * p.ldrb + n];
+    if (p.R) v += bf2f(p.R[(size_t)m * p.ldr + n]);
+  }
+  p.C[(size_t)m * p.ldc + n] = f2bf(v);
+}
+
+static bool rows_applies(int M, int N, int K) { return M >= 1 && M <= 8 && N >= 1 && K >= 8 && !(K & 7); }
+
+static int launch_rows(const GemmArgs& a, hipStream_t s) {
+  const dim3 grid((a.N + 7) / 8);
+  if (a.M <= 2) hipLaunchKernelGGL(gemm_rows_kernel<2>, grid, dim3(256), 0, s, a);
+  else if (a.M <= 4) hipLaunchKernelGGL(gemm_rows_kernel<4>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(gemm_rows_kernel<8>, grid, dim3(256), 0, s, a);
+  return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+}
+
 __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(GemmArgs p, int geglu) {
   const int Nout = geglu ? p.N / 2 : p.N;
   const int CPR = (Nout + 7) / 8;
@@ -871,6 +951,7 @@ extern "C" const char* vst_gemm_kernel_name(int M, int N, int K, int kind, int t
                                        "gemm_ring<256x256,splitk>", "gemm_ring<256x128,splitk>", "",
                                        "gemm_ring<256x160,splitk>", "gemm_ring<192x256,splitk>"};
   if (kind == 3) return "gemm_kernel<conv_in>";
+  if (kind == 0 && tile == 0 && rows_applies(M, N, K)) return "gemm_rows";
   if (kind == 0 && (tile == 5 || (tile == 0 && N <= 64 && M >= 1024))) return "gemm_skinny";  // no-epilogue calls
   if (kind < 0 || kind > 3 || tile < 0 || tile > 9 || tile == 5 || splits < 0) return "";
   if (tile == 9) return kind == 0 ? "gemm_p8<256x192>" : "";
@@ -927,6 +1008,7 @@ extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int
   a.C1 = 0; a.C2 = 0; a.stride = 1; a.up = 0;
   a.act = epilogue == 2 ? 1 : 0;
   if (epilogue == 2) epilogue = 0;
+  if (tile == 0 && !A2 && epilogue != 1 && rows_applies(M, N, K)) return launch_rows(a, (hipStream_t)stream);
   if (tile == 0 && skinny_ok && M >= 1024) tile = 5;  // LoRA down-projection: skinny kernel
   if (tile == 5) return run_gemm(a, 0, 0, 5, 1, (hipStream_t)stream);
   const size_t slab_bytes = (workspace && ws_bytes > kFlagBytes) ? ws_bytes - kFlagBytes : 0;
