@@ -124,17 +124,23 @@ int vst_groupnorm(const void* x1, int ld1, int C1, const void* x2, int ld2, int 
                   int rows_per_sample, int groups, float eps, const float* gamma, const float* beta, int silu_act,
                   void* y, int ldy, void* workspace, void* stream);
 
-/* Frame-sharded motion-module GroupNorm (diffusers AnimateDiffTransformer3D norm: statistics over
- * every frame of a clip, inference_animatediff.py:213-214 keeps it on the motion path).  When a
- * clip's frames are spread over ranks, each rank computes per-(sample, group) double (sum, sumsq)
- * over its rows, the host all-reduces them (RCCL), and every rank normalises its own rows with the
- * clip-wide statistics; `count` = elements per (sample, group) over the whole clip. */
-int vst_groupnorm_sums(const void* x1, int ld1, int C1, const void* x2, int ld2, int C2, int nsamples,
-                       int rows_per_sample, int groups, double* sums, void* workspace, void* stream);
-int vst_groupnorm_apply_sums(const void* x1, int ld1, int C1, const void* x2, int ld2, int C2, int nsamples,
-                             int rows_per_sample, int groups, const double* sums, double count, float eps,
-                             const float* gamma, const float* beta, int silu_act, void* y, int ldy, void* workspace,
-                             void* stream);
+/* GroupNorm (+SiLU) over NHWC samples of rows_per_sample rows; a frame's statistics depend only on its own rows
+ * (the chunking is a function of rows_per_sample, not of how many samples share the launch). */
+
+/* Motion-module GroupNorm (diffusers AnimateDiffTransformer3D norm, built at animatediff/utils.py:31: statistics
+ * over every frame of a clip), frame-sharded or not.  vst_groupnorm_frame_partials writes fp32 (sum, sumsq) chunk
+ * partials per frame, [nframes][vst_groupnorm_frame_chunks(rows_per_frame)][groups][2]; a frame's partials depend
+ * only on that frame.  vst_groupnorm_apply_partials merges the partials of every frame of each clip in one fixed
+ * order (fp64) and normalises this rank's rows: `part` is the rank-major all-gather of every rank's partials,
+ * [nranks][nclips][frames_local][chunks][groups][2] (nranks = 1: this process holds the whole clip), so a
+ * frame-sharded forward gets bit-identical statistics to the unsharded one.  scale_shift: caller-owned fp32
+ * [2 * nclips * C], 16-byte aligned. */
+int vst_groupnorm_frame_chunks(int rows_per_frame);
+int vst_groupnorm_frame_partials(const void* x1, int ld1, int C1, int nframes, int rows_per_frame, int groups,
+                                 float* part, void* stream);
+int vst_groupnorm_apply_partials(const void* x1, int ld1, int C1, int nclips, int frames_local, int rows_per_frame,
+                                 int groups, const float* part, int nranks, float eps, const float* gamma,
+                                 const float* beta, int silu_act, void* y, int ldy, float* scale_shift, void* stream);
 
 /* LayerNorm over C (+ sinusoidal PE row pe[(row/pe_div)%pe_mod], temporal_transformer.py:6-27). */
 int vst_layernorm(const void* x, int ldx, int C, int rows, const float* gamma, const float* beta, float eps,

@@ -529,14 +529,16 @@ def test_unet_training_step_grads_vs_oracle(cuda, config):
     assert errs[order[len(order) // 2]] <= max(3e-2, 1.5 * yorder[len(yorder) // 2])
 
 
-@pytest.mark.parametrize("M,N,ld", [(512, 512, 512), (65536, 1280, 1280), (1000, 64, 72), (3, 8, 8),
-                                    (16384, 2560, 3840), (262144, 320, 320), (131072, 2560, 2560), (70000, 40, 40)])
-def test_colsum(cuda, M, N, ld):
+@pytest.mark.parametrize("M,N,ld,c0", [(512, 512, 512, 0), (65536, 1280, 1280, 0), (1000, 64, 72, 0), (3, 8, 8, 0),
+                                       (16384, 2560, 3840, 0), (262144, 320, 320, 0), (131072, 2560, 2560, 0),
+                                       (70000, 40, 40, 0), (1000, 37, 40, 0), (512, 64, 72, 3), (77, 5, 9, 1)])
+def test_colsum(cuda, M, N, ld, c0):
     """vst_colsum (bias gradients db = g^T 1) against an fp64 column sum; deterministic (two calls and a captured
-    replay bit for bit equal)."""
+    replay bit for bit equal); widths that are not a multiple of 8 and column-offset views (unaligned base) go through
+    the zero-padded copy."""
     from video_style_transfer_amd import kernels as K
     g = torch.Generator(device=cuda).manual_seed(M + N)
-    x = torch.randn(M, ld, generator=g, device=cuda).to(torch.bfloat16)[:, :N]
+    x = torch.randn(M, ld, generator=g, device=cuda).to(torch.bfloat16)[:, c0:c0 + N]
     want = x.double().sum(0)
     y = K.colsum(x)
     y2 = K.colsum(x)

@@ -23,19 +23,18 @@ import sys
 
 def bench_symbol(name: str) -> str:
     """rocprof kernel name -> the symbol bench.py / vst_gemm_kernel_name report."""
-    m = re.search(r"gemm_ring_kernel<vst::RingCfg<(\d+), (\d+), \d+, \d+, \d+>, (\d), (\d), (true|false)>", name)
+    m = re.search(r"gemm_ring_kernel<vst::RingCfg<(\d+), (\d+), \d+, \d+, \d+>, (\d), (\d)>", name)
     if m:
-        bm, bn, amode, epi, sk = m.groups()
+        bm, bn, amode, epi = m.groups()
         tag = {("0", "0"): "", ("0", "1"): ",geglu", ("1", "0"): ",conv", ("0", "2"): ",splitk",
                ("1", "2"): ",splitk"}.get((amode, epi), f",a{amode}e{epi}")
-        return f"gemm_ring<{bm}x{bn}{tag}{',streamk' if sk == 'true' else ''}>"
-    # optional 4th / 5th template arguments: LORA, PERS (the persistent variant reports under the same symbol)
-    m = re.search(r"gemm_p8_kernel<(\d), (true|false)(?:, (\d+))?(?:, (true|false))?(?:, (?:true|false))?>", name)
+        return f"gemm_ring<{bm}x{bn}{tag}>"
+    # gemm_p8_kernel<EPI, BN, LORA>
+    m = re.search(r"gemm_p8_kernel<(\d), (\d+)(?:, (true|false))?>", name)
     if m:
-        epi, sk, bn, lora = m.groups()
-        tags = (",lora" if lora == "true" else "") + (",geglu" if epi == "1" else "") + \
-            (",xattn" if epi == "4" else "") + (",streamk" if sk == "true" else "")
-        return f"gemm_p8<256x{bn or 256}{tags}>"
+        epi, bn, lora = m.groups()
+        tags = (",lora" if lora == "true" else "") + (",geglu" if epi == "1" else "") + (",xattn" if epi == "4" else "")
+        return f"gemm_p8<256x{bn}{tags}>"
     if "layernorm_lora_kernel" in name:
         return "layernorm_lora"
     for k, v in (("gemm_skinny", "gemm_skinny"), ("spatial_attn_kernel", "spatial_attn_kernel"),

@@ -37,9 +37,9 @@ SIGNATURES = {
                                         _P]),
     "vst_motion_attention_block_supported": (_I, [_I, _I, _I, _I]),
     "vst_groupnorm_workspace_bytes": (_S, [_I, _I, _I, _I]),
-    "vst_groupnorm_sums": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
-    "vst_groupnorm_apply_sums": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _P, ctypes.c_double, _F, _P, _P, _I, _P,
-                                      _I, _P, _P]),
+    "vst_groupnorm_frame_chunks": (_I, [_I]),
+    "vst_groupnorm_frame_partials": (_I, [_P, _I, _I, _I, _I, _I, _P, _P]),
+    "vst_groupnorm_apply_partials": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _I, _F, _P, _P, _I, _P, _I, _P, _P]),
     "vst_permute_rows": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "vst_groupnorm": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _F, _P, _P, _I, _P, _I, _P, _P]),
     "vst_layernorm_lora": (_I, [_P, _I, _I, _I, _P, _P, _F, _P, _I, _P, _I, _P, _I, _P]),

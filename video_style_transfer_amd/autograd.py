@@ -330,14 +330,21 @@ class TemporalAttentionFn(torch.autograd.Function):
 
 class GroupNormFn(torch.autograd.Function):
     """GroupNorm (+SiLU) over `nsamples` groups of `rows_per_sample` token rows (the motion module's clip-wide GN:
-    rows_per_sample = F*H*W; per-frame GN: H*W) with the HIP forward (vst_groupnorm) and backward
+    rows_per_sample = F*H*W, frames = F; per-frame GN: H*W) with the HIP forward (vst_groupnorm, or for a clip-wide
+    GN the inference path's per-frame partials, vst_groupnorm_frame_partials / _apply_partials) and backward
     (vst_groupnorm_bwd)."""
 
     @staticmethod
-    def forward(ctx, x2d, gamma, beta, nsamples: int, rows_per_sample: int, groups: int, eps: float, silu: bool):
+    def forward(ctx, x2d, gamma, beta, nsamples: int, rows_per_sample: int, groups: int, eps: float, silu: bool,
+                frames: int = 1):
         x2d = x2d.to(BF16).contiguous()
         g32, b32 = gamma.detach().float().contiguous(), beta.detach().float().contiguous()
-        y = K.group_norm(x2d, nsamples, rows_per_sample, groups, eps, g32, b32, silu=silu)
+        if frames > 1 and not silu:
+            hw = rows_per_sample // frames
+            part = K.group_norm_frame_partials(x2d, nsamples * frames, hw, groups)
+            y = K.group_norm_apply_partials(x2d, nsamples, frames, hw, groups, eps, g32, b32, part, 1)
+        else:
+            y = K.group_norm(x2d, nsamples, rows_per_sample, groups, eps, g32, b32, silu=silu)
         ctx.save_for_backward(x2d, gamma, beta)
         ctx.cfg = (nsamples, rows_per_sample, groups, eps, silu)
         return y
@@ -348,7 +355,7 @@ class GroupNormFn(torch.autograd.Function):
         ns, rps, groups, eps, silu = ctx.cfg
         dx, dg, db = K.group_norm_bwd(x2d, g.to(BF16).contiguous(), ns, rps, groups, eps,
                                       gamma.detach().float().contiguous(), beta.detach().float().contiguous(), silu=silu)
-        return dx, dg.to(gamma.dtype), db.to(beta.dtype), None, None, None, None, None
+        return dx, dg.to(gamma.dtype), db.to(beta.dtype), None, None, None, None, None, None
 
 
 
@@ -467,7 +474,7 @@ def motion_module_train(mm, x2d, nclip: int, F: int, HW: int):
     clip, proj_in, [LN+PE -> fused q/k/v (+temporal LoRA) -> frame-axis attention -> to_out (+LoRA) -> +res] x2,
     LN -> GEGLU -> ff.2 -> +res, proj_out -> +x.  Tokens [(b*F + f)*HW + p, C] bf16."""
     C = x2d.shape[1]
-    h = GroupNormFn.apply(x2d, mm.norm.weight, mm.norm.bias, nclip, F * HW, mm.norm.num_groups, mm.norm.eps, False)
+    h = GroupNormFn.apply(x2d, mm.norm.weight, mm.norm.bias, nclip, F * HW, mm.norm.num_groups, mm.norm.eps, False, F)
     h = proj_train([mm.proj_in], h)
     for blk in mm.transformer_blocks:
         pe = blk.pos_embed.pe.detach().float().reshape(-1, C).contiguous()

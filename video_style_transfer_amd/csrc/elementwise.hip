@@ -705,7 +705,8 @@ extern "C" size_t vst_colsum_workspace_bytes(int M, int N) {
 }
 
 extern "C" int vst_colsum(const void* x, int ldx, int M, int N, float* y, void* workspace, void* stream) {
-  if (!x || !y || !workspace || M <= 0 || N <= 0 || N % 8 || (ldx & 7) || ldx < N) return VST_ERR_ARG;
+  if (!x || !y || !workspace || M <= 0 || N <= 0 || N % 8 || (ldx & 7) || ldx < N || ((uintptr_t)x & 15))
+    return VST_ERR_ARG;  // 16-B vector loads of 8-column chunks
   const ColsumPlan p = colsum_plan(M, N);
   hipStream_t s = (hipStream_t)stream;
   float* part1 = (float*)workspace;

@@ -654,12 +654,6 @@ static int gemm_p8_env() {
 // 9.1 ms per step, profiles/r2_ab_p8_all_k.txt).
 // VST_GEMM_P8 = 0 off, unset / 1 every shape with at least half a wave of 256x256 tiles.
 static int device_cus();
-static bool p8_sk_on();
-static bool p8_sk_shape(int M, int N, int K) {
-  const int tiles = ((M + 255) / 256) * ((N + 255) / 256), cus = device_cus();
-  return p8_sk_on() && tiles < cus && 2 * tiles >= cus && (K + 63) / 64 >= 4 &&
-         (long long)tiles * ((K + 63) / 64) < (1LL << 30) && cus * (int)sizeof(int) <= 4096;
-}
 static bool p8_auto(int M, int N, int K, bool geglu) {
   (void)geglu;
   const int e = gemm_p8_env();
@@ -678,7 +672,7 @@ static bool p8_bn192(int M, int N, bool geglu) {
     const char* e = getenv("VST_P8_BN");
     return e ? atoi(e) : 0;
   }();
-  if (geglu || env == 256 || p8_sk_on()) return false;
+  if (geglu || env == 256) return false;
   const int mb = (M + 255) / 256, cus = device_cus();
   const int r256 = (mb * ((N + 255) / 256) + cus - 1) / cus, r192 = (mb * ((N + 191) / 192) + cus - 1) / cus;
   return env == 192 || 0.8 * r192 < 0.97 * r256;
@@ -689,9 +683,7 @@ static bool p8_applies(int M, int N, int K1, bool two_src) {
   (void)M; (void)N;
   return !two_src || (K1 & 63) == 0;
 }
-// Workspace layout (caller-owned, zero-filled once): [split-K slabs | stream-K partial slots ...]
-// followed by kFlagBytes of stream-K flags at the very end (kept zero between launches).
-constexpr size_t kFlagBytes = 4096;
+// Workspace (caller-owned): the fp32 split-K slabs [splits][M][N].
 
 static int device_cus() {
   static int n = 0;
@@ -703,64 +695,10 @@ static int device_cus() {
   return n;
 }
 
-// Stream-K for the 256x256 ring (EPI 0): when the tile count leaves more than 20 % of the last
-// round's CUs idle (e.g. 160 or 384 tiles on 256 CUs), launch one workgroup per CU over equal
-// shares of the (tile, k-step) space instead.  All workgroups must be co-resident (1 per CU at
-// 160 KiB LDS), which a grid of exactly the CU count guarantees on an otherwise idle device.
-static bool plan_stream_k(int M, int N, int K, size_t ws_bytes, int& iters, int& grid) {
-  // Opt-in (VST_STREAMK=1): measured slower than the 192x256 data-parallel tile on this path —
-  // the persistent segment loop costs ~50 VGPRs on top of the 256x256 body and spills.
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("VST_STREAMK");
-    on = (e && atoi(e)) ? 1 : 0;
-  }
-  if (!on) return false;
-  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
-  const int nk = (K + 31) / 32;
-  const int cus = device_cus();
-  const int rounds = (tiles + cus - 1) / cus;
-  if ((double)tiles / ((double)rounds * cus) >= 0.8 || nk < 16 || cus > 1024) return false;
-  if (ws_bytes < (size_t)cus * 256 * 256 * sizeof(float) + kFlagBytes) return false;
-  const long long total = (long long)tiles * nk;
-  iters = (int)((total + cus - 1) / cus);
-  grid = cus;
-  return true;
-}
-
-// Stream-K for the 8-phase kernel (gemm_p8.hip): one partial round of 256x256 tiles (half or more of the CUs, fewer
-// tiles than CUs: the 16x16 level's M = 8192, N = 1280 grids) runs on one workgroup per CU over equal k-shares.
-// Opt-in (VST_P8_SK=1): measured slower in the denoise step (tools/p8_bench.sh: 8192x1280x1312 8.56 -> 11.1 ms per
-// step, 8192x1280x5120 8.69 (ring) -> 9.51 ms).  At K = 1312 a tile's operands are 1.3 MB while each split tile adds
-// ~0.8 MB of fp32 partial traffic (written + read back), and every share pays two pipeline fills for ~13 k-tiles.
-static bool p8_sk_on() {
-  static int v = -2;
-  if (v == -2) {
-    const char* e = getenv("VST_P8_SK");
-    v = e ? atoi(e) : 0;
-  }
-  return v != 0;
-}
-
-static void apply_p8_sk(GemmArgs& a, void* ws, size_t ws_bytes) {
-  const int cus = device_cus();
-  if (!ws || !p8_sk_shape(a.M, a.N, a.K)) return;
-  if (ws_bytes < (size_t)cus * 256 * 256 * sizeof(float) + kFlagBytes) return;
-  a.sk_grid = cus;
-  a.sk_ws = (float*)ws;
-  a.sk_flags = (int*)((char*)ws + ws_bytes - kFlagBytes);
-}
-
-static void apply_stream_k(GemmArgs& a, int tile, int splits, int epi, void* ws, size_t ws_bytes) {
-  if (tile != 3 || splits > 1 || epi != 0 || !ws) return;
-  int iters = 0, grid = 0;
-  if (!plan_stream_k(a.M, a.N, a.K, ws_bytes, iters, grid)) return;
-  a.sk_iters = iters;
-  a.sk_grid = grid;
-  a.sk_ws = (float*)ws;
-  a.sk_flags = (int*)((char*)ws + ws_bytes - kFlagBytes);
-}
-
+// Stream-K (one workgroup per CU over equal shares of the (tile, k-step) space, partial tiles summed by their
+// owner) was built for both the ring and the 8-phase kernel in rounds 1-3 and measured slower on every shape of this
+// path (8192x1280x1312: 8.56 -> 11.1 ms per step).  Its cross-workgroup hand-off also depended on
+// every workgroup being resident at once, which concurrent streams do not guarantee, so it was removed.
 
 static int gemm_ablate_env() {
   static int v = -1;
@@ -955,22 +893,13 @@ extern "C" const char* vst_gemm_kernel_name(int M, int N, int K, int kind, int t
   if (kind == 0 && (tile == 5 || (tile == 0 && N <= 64 && M >= 1024))) return "gemm_skinny";  // no-epilogue calls
   if (kind < 0 || kind > 3 || tile < 0 || tile > 9 || tile == 5 || splits < 0) return "";
   if (tile == 9) return kind == 0 ? "gemm_p8<256x192>" : "";
-  const int splits_in = splits;
   if (tile == 0 && kind <= 1 && p8_auto(M, N, K, kind == 1)) {
-    if (splits_in == 0 && kind == 0 && p8_bn192(M, N, false)) return "gemm_p8<256x192>";
+    if (splits == 0 && kind == 0 && p8_bn192(M, N, false)) return "gemm_p8<256x192>";
     tile = 8;
   }
-  choose(M, N, K, kind == 1, kind == 2, ws_bytes > kFlagBytes ? ws_bytes - kFlagBytes : 0, tile, splits);
-  if (tile == 8) {
-    const bool sk = splits_in != 1 && p8_sk_shape(M, N, K) &&
-                    ws_bytes >= (size_t)device_cus() * 256 * 256 * sizeof(float) + kFlagBytes;
-    if (sk) return kind == 1 ? "gemm_p8<256x256,geglu,streamk>" : "gemm_p8<256x256,streamk>";
-    return kind == 1 ? "gemm_p8<256x256,geglu>" : "gemm_p8<256x256>";
-  }
+  choose(M, N, K, kind == 1, kind == 2, ws_bytes, tile, splits);
+  if (tile == 8) return kind == 1 ? "gemm_p8<256x256,geglu>" : "gemm_p8<256x256>";
   if (splits > 1) return split_names[tile - 1];
-  int it = 0, gr = 0;
-  if (tile == 3 && kind != 1 && plan_stream_k(M, N, K, ws_bytes, it, gr))
-    return kind == 2 ? "gemm_ring<256x256,conv,streamk>" : "gemm_ring<256x256,streamk>";
   return names[tile - 1][kind == 2 ? 2 : kind];
 }
 
@@ -1011,17 +940,14 @@ extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int
   if (tile == 0 && !A2 && epilogue != 1 && rows_applies(M, N, K)) return launch_rows(a, (hipStream_t)stream);
   if (tile == 0 && skinny_ok && M >= 1024) tile = 5;  // LoRA down-projection: skinny kernel
   if (tile == 5) return run_gemm(a, 0, 0, 5, 1, (hipStream_t)stream);
-  const size_t slab_bytes = (workspace && ws_bytes > kFlagBytes) ? ws_bytes - kFlagBytes : 0;
-  const int splits_in = splits;  // tile 8: splits 1 = plain tiling, 0 = stream-K where it applies
+  const size_t slab_bytes = workspace ? ws_bytes : 0;
   if (tile == 0 && splits == 0 && p8_auto(M, N, K, epilogue == 1) && p8_applies(M, N, K1, A2 != nullptr))
     tile = p8_bn192(M, N, epilogue == 1) ? 9 : 8;
-  if (tile == 9) {  // the 8-phase kernel at 256x192 (no stream-K)
+  if (tile == 9) {  // the 8-phase kernel at 256x192
     a.p8_bn = 192;
     return run_gemm(a, 0, 0, 8, 1, (hipStream_t)stream);
   }
   choose(M, N, K, epilogue == 1, 0, slab_bytes, tile, splits);
-  if (slab_bytes) apply_stream_k(a, tile, splits, epilogue == 1 ? 1 : 0, workspace, ws_bytes);
-  if (tile == 8 && splits_in != 1) apply_p8_sk(a, workspace, ws_bytes);
   return run_gemm(a, 0, epilogue == 1, tile, splits, (hipStream_t)stream);
 }
 
@@ -1068,9 +994,8 @@ static int conv3x3_impl(const void* x1, int C1, const void* x2, int C2, int nimg
   a.r_bytes = R ? clamp_bytes(((size_t)(a.M - 1) * ldr + Cout) * 2) : 0;
   if ((ldc & 7) && Cout >= 8) return VST_ERR_ARG;
   if (!vec) { tile = 2; splits = 1; }
-  const size_t slab_bytes = (workspace && ws_bytes > kFlagBytes) ? ws_bytes - kFlagBytes : 0;
+  const size_t slab_bytes = workspace ? ws_bytes : 0;
   choose(a.M, a.N, a.K, 0, 1, slab_bytes, tile, splits);
-  if (slab_bytes && vec) apply_stream_k(a, tile, splits, 0, workspace, ws_bytes);
   return run_gemm(a, vec ? 1 : 2, 0, tile, splits, (hipStream_t)stream);
 }
 

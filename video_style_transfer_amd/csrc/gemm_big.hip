@@ -106,16 +106,10 @@ __device__ __forceinline__ void tile_coords(int t, int nbm, int nbn, int& bm, in
   bn = (t - gid * in_group) / gsize;
 }
 
-// One output tile's k-range [kt0, kt1): ring pipeline + epilogue.  Stream-K modes: sk_mode 0 =
-// whole tile (or a split-K slab, EPI 2); 1 = this k-range's fp32 partial goes to slot `sk_slot`
-// (accumulator register layout, 1 KiB coalesced per fragment and wave) and its flag is released;
-// 2 = the tile's head range: add the partials of slots sk_slot+1 .. sk_last (the later k-ranges,
-// which those workgroups computed FIRST in their own ranges, so they are normally ready), reset
-// their flags, then run the epilogue.
+// One output tile's k-range [kt0, kt1) (the whole K, or a split-K slab with EPI 2): ring pipeline + epilogue.
 template <class Cfg, int AMODE, int EPI>
 __device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const int m0, const int n0, const int kt0,
-                                          const int kt1, const int sk_mode, const int sk_slot, const int sk_last) {
-  constexpr int BM = Cfg::BM, BN = Cfg::BN;
+                                          const int kt1) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid / Cfg::WAVES_N, wc = wid - wr * Cfg::WAVES_N;
@@ -400,56 +394,6 @@ __device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const i
     return;
   }
 
-  // ---------------- stream-K partials ----------------
-  if constexpr (EPI == 0) {
-    // Partials cross XCDs: written through (sc1) and read with sc1 loads, flags stored / polled at
-    // agent scope — no L2-wide writeback or invalidate, which would also evict every other
-    // workgroup's A/W panels from the shared L2.
-    const auto rsk = make_rsrc(p.sk_ws, (uint32_t)((size_t)p.sk_grid * BM * BN * sizeof(float)));
-    if (sk_mode != 0 && (abl & 4)) {  // diagnostics: segmenting cost only (wrong results)
-      if (sk_mode == 1) return;
-    } else if (sk_mode == 1) {
-      const int base = sk_slot * (BM * BN * 4);
-#pragma unroll
-      for (int i = 0; i < Cfg::MI; ++i)
-#pragma unroll
-        for (int j = 0; j < Cfg::NJ; ++j) {
-          const f32x4 v = acc[i][j];
-          buf_store16_sc1(*reinterpret_cast<const u32x4*>(&v), rsk,
-                          base + (((wid * Cfg::MI + i) * Cfg::NJ + j) * 64 + lane) * 16);
-        }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's partial is in memory
-      __syncthreads();
-      if (tid == 0) __hip_atomic_store(p.sk_flags + sk_slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
-    else if (sk_mode == 2) {
-      for (int sl = sk_slot + 1; sl <= sk_last; ++sl) {
-        if (tid == 0) {
-          // bounded spin (~1 s): a missing producer must not hang the GPU
-          for (int spin = 0; spin < (1 << 23); ++spin) {
-            if (__hip_atomic_load(p.sk_flags + sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1) break;
-            __builtin_amdgcn_s_sleep(2);
-          }
-        }
-        __syncthreads();
-        const int base = sl * (BM * BN * 4);
-#pragma unroll
-        for (int i = 0; i < Cfg::MI; ++i) {
-          u32x4 v[Cfg::NJ];
-#pragma unroll
-          for (int j = 0; j < Cfg::NJ; ++j)
-            v[j] = buf_load16_sc1(rsk, base + (((wid * Cfg::MI + i) * Cfg::NJ + j) * 64 + lane) * 16);
-#pragma unroll
-          for (int j = 0; j < Cfg::NJ; ++j) acc[i][j] += *reinterpret_cast<const f32x4*>(&v[j]);
-          __builtin_amdgcn_sched_barrier(0);  // NJ loads in flight at a time: no accumulator spills
-        }
-        // the next launch's producers start after this kernel completes: resetting now is race-free
-        if (tid == 0) __hip_atomic_store(p.sk_flags + sl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
-
   // ---------------- epilogue ----------------
   // Split-K partials go straight from registers to the fp32 slab (16 B per lane).  Otherwise
   // bias (and GELU for EPI 3) is applied in registers, the whole BMxBN tile is staged ONCE in LDS as bf16 (the rounding
@@ -482,62 +426,39 @@ __device__ __forceinline__ void ring_tile(const GemmArgs& p, char* smem, const i
 }
 
 // Data-parallel launch: one tile per workgroup (split-K: blockIdx.z selects the k-range).
-// Stream-K launch (SK): one workgroup per CU; workgroup w (XCD-contiguous logical index) takes the
-// w-th equal share of the (tile, k-step) iteration space, so grids whose tile count leaves CUs idle
-// (160 or 384 tiles on 256 CUs) keep every CU busy; split tiles are combined through sk_ws.
-template <class Cfg, int AMODE, int EPI, bool SK>
+template <class Cfg, int AMODE, int EPI>
 __global__ __launch_bounds__(Cfg::THREADS, 1) void gemm_ring_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int BM = Cfg::BM, BN = Cfg::BN;
   const int nbn = (p.N + BN - 1) / BN, nbm = (p.M + BM - 1) / BM;
   const int nk_all = (p.K + RBK - 1) / RBK;
-  if constexpr (!SK) {
-    if (EPI != 2 && p.persist) {
-      // Persistent: gridDim.x workgroups (one per resident slot) walk the tiles.  Workgroup b runs on XCD
-      // b % 8 and takes that XCD's contiguous chunk of logical tiles in rounds, so co-resident tiles share
-      // L2 panels as in the one-tile-per-workgroup launch; the next tile's ring prologue follows the
-      // previous tile's epilogue stores without a workgroup relaunch (the stores drain under its DMA).
-      const int T = nbm * nbn, G = gridDim.x;
-      const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
-      const int per_xcd = (G - xcd + 7) / 8;
-      const int q = T >> 3, r = T & 7;
-      const int beg = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-      const int cnt = q + (xcd < r ? 1 : 0);
-      for (int j = loc; j < cnt; j += per_xcd) {
-        int bm, bn;
-        tile_coords(beg + j, nbm, nbn, bm, bn, p.group_m > 0 ? p.group_m : 8);
-        ring_tile<Cfg, AMODE, EPI>(p, smem, bm * BM, bn * BN, 0, nk_all, 0, 0, 0);
-        __syncthreads();  // the staged epilogue tile / ring LDS is reused by the next tile
-      }
-      return;
-    }
-    int bm, bn;
-    tile_coords(xcd_remap(blockIdx.x, nbn * nbm), nbm, nbn, bm, bn, p.group_m > 0 ? p.group_m : 8);
-    int kt0 = 0, kt1 = nk_all;
-    if (EPI == 2) {
-      kt0 = (int)((long long)nk_all * blockIdx.z / p.splits);
-      kt1 = (int)((long long)nk_all * (blockIdx.z + 1) / p.splits);
-    }
-    ring_tile<Cfg, AMODE, EPI>(p, smem, bm * BM, bn * BN, kt0, kt1, 0, 0, 0);
-  } else {
-    const int w = xcd_remap(blockIdx.x, gridDim.x);
-    const long long I = p.sk_iters;
-    const long long total = (long long)nbm * nbn * nk_all;
-    long long start = (long long)w * I;
-    const long long end = min(start + I, total);
-    while (start < end) {
-      const int t = (int)(start / nk_all);
-      const int kb = (int)(start - (long long)t * nk_all);
-      const int ke = (int)min((long long)nk_all, kb + (end - start));
-      const int mode = (kb == 0 && ke == nk_all) ? 0 : (kb == 0 ? 2 : 1);
-      const int last = (int)(((long long)(t + 1) * nk_all - 1) / I);  // workgroup holding the tile's last k-step
+  if (EPI != 2 && p.persist) {
+    // Persistent: gridDim.x workgroups (one per resident slot) walk the tiles.  Workgroup b runs on XCD
+    // b % 8 and takes that XCD's contiguous chunk of logical tiles in rounds, so co-resident tiles share
+    // L2 panels as in the one-tile-per-workgroup launch; the next tile's ring prologue follows the
+    // previous tile's epilogue stores without a workgroup relaunch (the stores drain under its DMA).
+    const int T = nbm * nbn, G = gridDim.x;
+    const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+    const int per_xcd = (G - xcd + 7) / 8;
+    const int q = T >> 3, r = T & 7;
+    const int beg = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    const int cnt = q + (xcd < r ? 1 : 0);
+    for (int j = loc; j < cnt; j += per_xcd) {
       int bm, bn;
-      tile_coords(t, nbm, nbn, bm, bn);
-      ring_tile<Cfg, AMODE, EPI>(p, smem, bm * BM, bn * BN, kb, ke, mode, w, last);
-      start += ke - kb;
-      __syncthreads();  // LDS (staged tile / ring) is reused by the next segment
+      tile_coords(beg + j, nbm, nbn, bm, bn, p.group_m > 0 ? p.group_m : 8);
+      ring_tile<Cfg, AMODE, EPI>(p, smem, bm * BM, bn * BN, 0, nk_all);
+      __syncthreads();  // the staged epilogue tile / ring LDS is reused by the next tile
     }
+    return;
   }
+  int bm, bn;
+  tile_coords(xcd_remap(blockIdx.x, nbn * nbm), nbm, nbn, bm, bn, p.group_m > 0 ? p.group_m : 8);
+  int kt0 = 0, kt1 = nk_all;
+  if (EPI == 2) {
+    kt0 = (int)((long long)nk_all * blockIdx.z / p.splits);
+    kt1 = (int)((long long)nk_all * (blockIdx.z + 1) / p.splits);
+  }
+  ring_tile<Cfg, AMODE, EPI>(p, smem, bm * BM, bn * BN, kt0, kt1);
 }
 
 // stages: as many as the LDS budget allows at the intended residency (lookahead S-2 tiles)
@@ -548,30 +469,27 @@ using Cfg128x64 = RingCfg<128, 64, 2, 2, 6>;    //  72 KiB, 2 WG/CU
 using Cfg256x160 = RingCfg<256, 160, 4, 2, 5>;  // 130 KiB, 1 WG/CU: N = 320/640/960/1280/1920/3840 without waste
 using Cfg192x256 = RingCfg<192, 256, 2, 4, 5>;  // 140 KiB, 1 WG/CU: 215 tiles at M = 8192, N = 1280
 
-template <class Cfg, int AMODE, int EPI, bool SK>
+template <class Cfg, int AMODE, int EPI>
 static int launch_ring_k(const GemmArgs& a, hipStream_t s, dim3 grid) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_ring_kernel<Cfg, AMODE, EPI, SK>,
+    (void)hipFuncSetAttribute((const void*)gemm_ring_kernel<Cfg, AMODE, EPI>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_ring_kernel<Cfg, AMODE, EPI, SK>), grid, dim3(Cfg::THREADS), Cfg::LDS, s, a);
+  hipLaunchKernelGGL((gemm_ring_kernel<Cfg, AMODE, EPI>), grid, dim3(Cfg::THREADS), Cfg::LDS, s, a);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 
 template <class Cfg, int AMODE, int EPI>
 static int launch_ring_t(const GemmArgs& a, hipStream_t s, int splits) {
   const int nwg = ((a.M + Cfg::BM - 1) / Cfg::BM) * ((a.N + Cfg::BN - 1) / Cfg::BN);
-  if constexpr (EPI == 0 && std::is_same_v<Cfg, Cfg256x256>) {  // stream-K (opt-in, see gemm.hip)
-    if (a.sk_iters > 0) return launch_ring_k<Cfg, AMODE, EPI, true>(a, s, dim3(a.sk_grid));
-  }
   if (EPI != 2 && a.persist > 0) {
     const int per_cu = Cfg::NWAVES == 8 ? 1 : 2;
     const int slots = a.persist * per_cu;
-    if (nwg > slots) return launch_ring_k<Cfg, AMODE, EPI, false>(a, s, dim3(slots, 1, 1));
+    if (nwg > slots) return launch_ring_k<Cfg, AMODE, EPI>(a, s, dim3(slots, 1, 1));
   }
-  return launch_ring_k<Cfg, AMODE, EPI, false>(a, s, dim3(nwg, 1, splits));
+  return launch_ring_k<Cfg, AMODE, EPI>(a, s, dim3(nwg, 1, splits));
 }
 
 template <class Cfg>

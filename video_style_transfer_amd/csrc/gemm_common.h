@@ -23,11 +23,6 @@ struct GemmArgs {
   int group_m;  // grouped tile order: row panels per group (0 = default 8; VST_GEMM_GROUP_M for tuning)
   int p8_bn;   // 8-phase kernel tile width: 0 / 256 or 192 (gemm_p8.hip)
   int ablate;  // diagnostics only (VST_GEMM_ABLATE): bit0 skip loop DMA, bit1 skip MFMA
-  // stream-K (ring GEMM, 256x256): k-steps per workgroup (0 = data-parallel), grid, partial slots
-  // [sk_grid][BM*BN] fp32 and their flags (zero between launches; consumers reset them)
-  int sk_iters, sk_grid;
-  float* sk_ws;
-  int* sk_flags;
   uint32_t a1_bytes, a2_bytes, w_bytes, r_bytes;
   // in-GEMM LoRA down-projection (gemm_p8.hip LORA, vst_gemm_lora): Acat [la_p][K] bf16 (row stride lda_la); the
   // output columns of group g = n / la_gn use u columns [g la_gr, (g + 1) la_gr), whose up-projection sits in W's

@@ -282,14 +282,6 @@ __device__ __forceinline__ void xattn_epilogue(const GemmArgs& p, char* smem, co
   }
 }
 
-// SK = stream-K: one workgroup per CU, each taking an equal share of the (tile, k-tile) iteration space, so grids of
-// 160 tiles (M = 8192, N = 1280: 62 % of the CUs under plain tiling) keep every CU busy.  A tile split between
-// workgroups is finished by its OWNER (the workgroup that runs its k-tile 0; that is always the owner's last
-// segment); the others (whose first segment starts mid-tile) store their fp32 accumulators in fragment order to
-// their partial slot, then raise their flag (agent-scope release).  The owner adds the partials in workgroup order
-// (deterministic), clears the flags for the next launch, and runs the epilogue.  Only owners wait, and only on
-// higher-numbered workgroups that wait on nobody, and the grid is at most one workgroup per CU: no cycle.
-//
 // LORA (vst_gemm_lora, UnZipLoRA / LoRA projections): the down-projection u = x . Acat^T is accumulated inside the
 // k-loop from the A fragments already in registers, so no separate pass over x produces it.  Each k-tile also
 // stages Acat's 16 u columns of this tile ([16][64] bf16, one extra DMA per wave issued with slot Amq0: waves 0-1
@@ -298,14 +290,13 @@ __device__ __forceinline__ void xattn_epilogue(const GemmArgs& p, char* smem, co
 // loop u is rounded to bf16 (the reference's rounding point of lora_layer's down output), exchanged through LDS and
 // multiplied by the tile's up-projection columns of W (K + ub0 ...) as one extra 16x16x32 step per accumulator —
 // the same operands, in the same order, as the [x | u] . [W | V]^T k-tile it replaces.
-template <int EPI, bool SK, int BN, bool LORA = false>
+template <int EPI, int BN, bool LORA = false>
 __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using Cfg = P8Cfg<BN>;
-  static_assert(!SK || BN == 256, "stream-K partial slots are 256 x 256");
   static_assert(EPI != 1 || BN == 256, "GEGLU needs 64-column [hidden | gate] blocks");
-  static_assert(!LORA || (!SK && EPI != 1), "in-GEMM LoRA: data-parallel tiles, linear epilogue");
-  static_assert(EPI != 4 || (!SK && BN == 192), "cross-attention epilogue: 192-column tiles (3 heads)");
+  static_assert(!LORA || EPI != 1, "in-GEMM LoRA: linear epilogue");
+  static_assert(EPI != 4 || BN == 192, "cross-attention epilogue: 192-column tiles (3 heads)");
   constexpr int LX = LORA ? 1 : 0;  // the Acat DMA in the vmcnt counts
   constexpr int SLOT = Cfg::SLOT, BUF = Cfg::BUF, RB1 = Cfg::RB1, NJ1 = Cfg::NJ1, NPB1 = Cfg::NPB1;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -549,172 +540,92 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   };
 #undef VST_P8_QUAD
 
-  if constexpr (!SK) {
-    int m0, n0;
-    VST_P8_STAMP(0)
-    tile_origin(xcd_remap(blockIdx.x, ntiles), m0, n0);
-    setup_tile(m0, n0);
-    run_segment(0, nk);
-    VST_P8_STAMP(2)
-    if constexpr (LORA) {
-      // u (bf16) -> LDS [256 rows][16 columns] (the drained ring), then acc += u . V^T over the 32-wide window
-      // (columns 16-31 zero: the [x | u] k-tile's second u half), V = W[n][K + ub0 ...]
-      char* U = smem;
+  int m0, n0;
+  VST_P8_STAMP(0)
+  tile_origin(xcd_remap(blockIdx.x, ntiles), m0, n0);
+  setup_tile(m0, n0);
+  run_segment(0, nk);
+  VST_P8_STAMP(2)
+  if constexpr (LORA) {
+    // u (bf16) -> LDS [256 rows][16 columns] (the drained ring), then acc += u . V^T over the 32-wide window
+    // (columns 16-31 zero: the [x | u] k-tile's second u half), V = W[n][K + ub0 ...]
+    char* U = smem;
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        u32x2 v;
-        v[0] = pack2bf(acc_u[q][0], acc_u[q][1]);
-        v[1] = pack2bf(acc_u[q][2], acc_u[q][3]);
-        *reinterpret_cast<u32x2*>(U + (wr * 128 + q * 64 + wc * 16 + fr) * 32 + fq * 8) = v;
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      const bf16x8 zero8 = {};
-      bf16x8 fv[Cfg::NJ];
-#pragma unroll
-      for (int j = 0; j < Cfg::NJ; ++j) {
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + Cfg::V_OFF + (wc * Cfg::WN + j * 16 + fr) * 32 + (fq & 1) * 16);
-        fv[j] = fq < 2 ? v : zero8;
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        bf16x8 fu = *reinterpret_cast<const bf16x8*>(U + (wr * 128 + i * 16 + fr) * 32 + (fq & 1) * 16);
-        fu = fq < 2 ? fu : zero8;
-#pragma unroll
-        for (int j = 0; j < Cfg::NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fv[j], fu, acc[i][j], 0, 0, 0);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // every wave's u reads done before the epilogue stages the tile over them
+    for (int q = 0; q < 2; ++q) {
+      u32x2 v;
+      v[0] = pack2bf(acc_u[q][0], acc_u[q][1]);
+      v[1] = pack2bf(acc_u[q][2], acc_u[q][3]);
+      *reinterpret_cast<u32x2*>(U + (wr * 128 + q * 64 + wc * 16 + fr) * 32 + fq * 8) = v;
     }
-    if constexpr (EPI == 4) xattn_epilogue<Cfg>(p, smem, m0, n0, acc, wr, wc);
-    else tile_epilogue<Cfg, EPI>(p, smem, m0, n0, acc, wr, wc);
-#ifdef VST_P8_TRACE
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-#endif
-    VST_P8_STAMP(3)
-  } else {
-    // Launched only with fewer tiles than workgroups, so a workgroup's share (< nk k-tiles) meets at most two
-    // tiles: first the tail of one (contributor, unless the share starts on a tile boundary), then the head of the
-    // next (owner).  Straight-line code: an outer segment loop keeps epilogue addressing live across the k-loop.
-    // Partial slot layout: [register r = 4 i + j][thread] f32x4 (fragment order, 16 B per lane, coalesced).
-    constexpr int PSLOT = 256 * 256;  // floats
-    // scalars (readfirstlane): divisions are VALU sequences, and a VGPR loop bound would make the whole k-loop's
-    // control and DMA addressing per-lane.  Shares: q or q + 1 k-tiles, start(v) = v q + min(v, r), no 64-bit divide.
-    const int G = gridDim.x;
-    const int w = xcd_remap(blockIdx.x, G);
-    const int T = ntiles * nk;  // host-checked < 2^31
-    const int q = T / G, r = T - q * G;
-    auto start_of = [&](int v) { return v * q + min(v, r); };
-    int g = __builtin_amdgcn_readfirstlane(start_of(w));
-    const int g1 = __builtin_amdgcn_readfirstlane(start_of(w + 1));
-    int m0, n0;
-    auto origin = [&](int tile) {
-      tile_origin(tile, m0, n0);
-      m0 = __builtin_amdgcn_readfirstlane(m0);
-      n0 = __builtin_amdgcn_readfirstlane(n0);
-    };
-    if (g < g1 && g % nk != 0) {  // contributor: k-tiles [kb, ke) of a tile owned by a lower workgroup
-      const int tile = __builtin_amdgcn_readfirstlane(g / nk);
-      const int kb = g - tile * nk;
-      const int ke = min(nk, kb + (g1 - g));
-      origin(tile);
-      setup_tile(m0, n0);
-      run_segment(kb, ke);
-      f32x4* slot = reinterpret_cast<f32x4*>(p.sk_ws + (size_t)w * PSLOT);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const bf16x8 zero8 = {};
+    bf16x8 fv[Cfg::NJ];
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) slot[(i * 4 + j) * 512 + tid] = acc[i][j];
-      // publish (MI355X_MICROARCH.md, inter-workgroup visibility, producer form): every storing wave waits for its
-      // own stores, the workgroup barrier, then ONE agent-scope release (L2 write-back) by lane 0, its completion
-      // waited for explicitly (the compiler may drop that wait), then the relaxed flag store
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(p.sk_flags + w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      g += ke - kb;
+    for (int j = 0; j < Cfg::NJ; ++j) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + Cfg::V_OFF + (wc * Cfg::WN + j * 16 + fr) * 32 + (fq & 1) * 16);
+      fv[j] = fq < 2 ? v : zero8;
     }
-    if (g < g1) {  // owner: k-tiles [0, ke) of this tile, then the later k-ranges from the next workgroups
-      int tl;      // laundered: nothing of the owner's addressing is computed before (and live across) its k-loop
-      tl = tid;
-      const int tile = __builtin_amdgcn_readfirstlane(g / nk), ke = g1 - g;
-      origin(tile);
-      setup_tile(m0, n0);
-      run_segment(0, ke);
-      const int te = (tile + 1) * nk;
-      for (int c = w + 1; c < G && start_of(c) < te; ++c) {
-        if (tl == 0) {
-          // relaxed poll (bounded, ~1 s: a missing contributor must not hang the GPU), then ONE agent acquire
-          // (invalidates this CU's L1) whose completion the barrier holds every wave behind
-          for (int spin = 0; spin < (1 << 23); ++spin) {
-            if (__hip_atomic_load(p.sk_flags + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
-            __builtin_amdgcn_s_sleep(2);
-          }
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
-        const f32x4* slot = reinterpret_cast<const f32x4*>(p.sk_ws + (size_t)c * PSLOT);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < 8; ++i) {
+      bf16x8 fu = *reinterpret_cast<const bf16x8*>(U + (wr * 128 + i * 16 + fr) * 32 + (fq & 1) * 16);
+      fu = fq < 2 ? fu : zero8;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] += slot[(i * 4 + j) * 512 + tl];
-          asm volatile("" ::: "memory");  // 4 loads in flight at a time: acc already holds 128 registers
-        }
-        if (tl == 0) __hip_atomic_store(p.sk_flags + c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      tile_epilogue<Cfg, EPI>(p, smem, m0, n0, acc, wr, wc, tl);
+      for (int j = 0; j < Cfg::NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fv[j], fu, acc[i][j], 0, 0, 0);
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's u reads done before the epilogue stages the tile over them
   }
+  if constexpr (EPI == 4) xattn_epilogue<Cfg>(p, smem, m0, n0, acc, wr, wc);
+  else tile_epilogue<Cfg, EPI>(p, smem, m0, n0, acc, wr, wc);
+#ifdef VST_P8_TRACE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+#endif
+  VST_P8_STAMP(3)
 }
 
-template <int EPI, bool SK, int BN, bool LORA = false>
+template <int EPI, int BN, bool LORA = false>
 static int launch_p8_epi(const GemmArgs& a, hipStream_t s) {
   static bool attr = false;
   constexpr int lds = EPI == 4 ? 160 * 1024 : (LORA ? P8Cfg<BN>::LDS_LORA : P8Cfg<BN>::LDS);
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_p8_kernel<EPI, SK, BN, LORA>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)gemm_p8_kernel<EPI, BN, LORA>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               lds);
     attr = true;
   }
-  const int nwg = SK ? a.sk_grid : ((a.M + 255) / 256) * ((a.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_p8_kernel<EPI, SK, BN, LORA>), dim3(nwg), dim3(512), lds, s, a);
+  const int nwg = ((a.M + 255) / 256) * ((a.N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_p8_kernel<EPI, BN, LORA>), dim3(nwg), dim3(512), lds, s, a);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 
 // in-GEMM LoRA down-projection (a.la set): epilogue 0 (bias / residual), bn 256 or 192
 int launch_gemm_p8_lora(const GemmArgs& a, int bn, hipStream_t s) {
-  if (!a.la || a.sk_grid > 0) return VST_ERR_ARG;
-  return bn == 192 ? launch_p8_epi<0, false, 192, true>(a, s) : launch_p8_epi<0, false, 256, true>(a, s);
+  if (!a.la) return VST_ERR_ARG;
+  return bn == 192 ? launch_p8_epi<0, 192, true>(a, s) : launch_p8_epi<0, 256, true>(a, s);
 }
 
 // cross-attention epilogue (a.xa_k set), 256x192 tiles, with or without the in-GEMM LoRA
 int launch_gemm_p8_xattn(const GemmArgs& a, hipStream_t s) {
-  if (!a.xa_k || !a.xa_v || a.sk_grid > 0) return VST_ERR_ARG;
-  return a.la ? launch_p8_epi<4, false, 192, true>(a, s) : launch_p8_epi<4, false, 192, false>(a, s);
+  if (!a.xa_k || !a.xa_v) return VST_ERR_ARG;
+  return a.la ? launch_p8_epi<4, 192, true>(a, s) : launch_p8_epi<4, 192, false>(a, s);
 }
 
-// epi: 0 bias / row bias / residual, 1 GEGLU, 3 bias + GELU; bn: 256 or 192 (not with GEGLU or stream-K)
+// epi: 0 bias / row bias / residual, 1 GEGLU, 3 bias + GELU; bn: 256 or 192 (not with GEGLU)
 int launch_gemm_p8(const GemmArgs& a, int epi, int bn, hipStream_t s) {
   if (a.A2 && (a.K1 & 63)) return VST_ERR_ARG;  // a 64-deep k-tile must not straddle the two A sources
-  const bool sk = a.sk_grid > 0 && a.sk_ws && a.sk_flags;
   if (bn == 192) {
-    if (sk) return VST_ERR_ARG;
     switch (epi) {
-      case 0: return launch_p8_epi<0, false, 192>(a, s);
-      case 3: return launch_p8_epi<3, false, 192>(a, s);
+      case 0: return launch_p8_epi<0, 192>(a, s);
+      case 3: return launch_p8_epi<3, 192>(a, s);
       default: return VST_ERR_ARG;
     }
   }
   if (bn != 256) return VST_ERR_ARG;
   switch (epi) {
-    case 0: return sk ? launch_p8_epi<0, true, 256>(a, s) : launch_p8_epi<0, false, 256>(a, s);
-    case 1: return sk ? launch_p8_epi<1, true, 256>(a, s) : launch_p8_epi<1, false, 256>(a, s);
-    case 3: return sk ? launch_p8_epi<3, true, 256>(a, s) : launch_p8_epi<3, false, 256>(a, s);
+    case 0: return launch_p8_epi<0, 256>(a, s);
+    case 1: return launch_p8_epi<1, 256>(a, s);
+    case 3: return launch_p8_epi<3, 256>(a, s);
     default: return VST_ERR_ARG;
   }
 }

@@ -334,16 +334,25 @@ __global__ __launch_bounds__(512) void gn_apply_kernel(const bf16_t* __restrict_
   }
 }
 
-// Frame-sharded motion GroupNorm (statistics over all frames of a clip, frames spread over
-// ranks): merge this rank's chunk partials into per-(sample, group) double (sum, sumsq), which the
-// host all-reduces across ranks, then finalize from the reduced sums.
-__global__ __launch_bounds__(64) void gn_sums_kernel(const float* __restrict__ part, int nchunk, int groups,
-                                                     double* __restrict__ sums) {
-  const int s = blockIdx.x / groups, gi = blockIdx.x - s * groups;
+// Motion-module GroupNorm (statistics over every frame of a clip), frame-sharded or not.  The statistics are
+// built from per-FRAME chunk partials (gn_stats_kernel with one sample per frame, chunking that depends only on
+// the frame's row count), so a rank holding some frames of a clip produces exactly the partials the unsharded
+// forward produces for those frames.  The finalize merges the clip's F x nck partials in one fixed order, read
+// from the rank-major layout [P][clips][F/P][nck][G][2] an all-gather leaves (P = 1: the unsharded layout), so the
+// sharded and unsharded statistics are the same bits whatever P is.
+__global__ __launch_bounds__(64) void gn_finalize_parts_kernel(const float* __restrict__ part, int P, int nclips,
+                                                               int Fl, int nck, int groups, int Cg, double count,
+                                                               float eps, const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta, float* __restrict__ scale,
+                                                               float* __restrict__ shift, int C) {
+  const int b = blockIdx.x / groups, gi = blockIdx.x - b * groups;
   const int lane = threadIdx.x;
+  const int per_clip = P * Fl * nck;  // partials of one clip, in (global frame, chunk) order
   double a = 0.0, q = 0.0;
-  for (int c = lane; c < nchunk; c += 64) {
-    const float* p = part + (((size_t)s * nchunk + c) * groups + gi) * 2;
+  for (int c = lane; c < per_clip; c += 64) {
+    const int f = c / nck, k = c - f * nck;
+    const int r = f / Fl, fl = f - r * Fl;
+    const float* p = part + (((((size_t)r * nclips + b) * Fl + fl) * nck + k) * groups + gi) * 2;
     a += p[0];
     q += p[1];
   }
@@ -352,26 +361,13 @@ __global__ __launch_bounds__(64) void gn_sums_kernel(const float* __restrict__ p
     a += __shfl_xor(a, o);
     q += __shfl_xor(q, o);
   }
-  if (lane == 0) {
-    sums[(size_t)blockIdx.x * 2] = a;
-    sums[(size_t)blockIdx.x * 2 + 1] = q;
-  }
-}
-
-__global__ __launch_bounds__(64) void gn_finalize_sums_kernel(const double* __restrict__ sums, double count,
-                                                              int groups, int Cg, float eps,
-                                                              const float* __restrict__ gamma,
-                                                              const float* __restrict__ beta,
-                                                              float* __restrict__ scale, float* __restrict__ shift,
-                                                              int C) {
-  const int s = blockIdx.x / groups, gi = blockIdx.x - s * groups;
-  const double mean = sums[(size_t)blockIdx.x * 2] / count;
-  const double var = fmax(sums[(size_t)blockIdx.x * 2 + 1] / count - mean * mean, 0.0);
+  const double mean = a / count;
+  const double var = fmax(q / count - mean * mean, 0.0);
   const float rstd = (float)(1.0 / sqrt(var + (double)eps));
-  for (int c = gi * Cg + threadIdx.x; c < (gi + 1) * Cg; c += 64) {
+  for (int c = gi * Cg + lane; c < (gi + 1) * Cg; c += 64) {
     const float sc = rstd * gamma[c];
-    scale[(size_t)s * C + c] = sc;
-    shift[(size_t)s * C + c] = beta[c] - (float)mean * sc;
+    scale[(size_t)b * C + c] = sc;
+    shift[(size_t)b * C + c] = beta[c] - (float)mean * sc;
   }
 }
 
@@ -789,7 +785,15 @@ __global__ __launch_bounds__(256) void layernorm_bwd_reduce_kernel(const float* 
 
 using namespace vst;
 
-// rows per workgroup: >= ~256 workgroups (swept 256..4096 with tools/norm_bench.py), 8..256 rows each
+// rows per workgroup.  Forward GroupNorms: a function of the sample's (frame's) row count only -- never of how many
+// samples share the launch -- so a frame's statistics are the same bits in a batch of any size (the frame-sharded
+// forward runs 1/P of the frames per rank, tests/test_frame_shard.py asserts equality); rows / 8 gives >= 8 chunks
+// per frame, >= 256 workgroups at the denoise step's 32 frames (the same chunking the old total-rows rule picked
+// there: 32 / 128 / 256 rows at 16x16 / 32x32 / 64x64).  Backward (vst_groupnorm_bwd, per-clip samples of the
+// training step): >= ~256 workgroups over the whole launch (swept 256..4096 with tools/norm_bench.py).
+static inline int gn_rpc_rows(int rows_per_sample) {
+  return std::max(8, std::min(256, (rows_per_sample + 7) / 8));
+}
 static inline int gn_rpc(int nsamples, int rows_per_sample) {
   static const long long target = [] {
     const char* e = getenv("VST_GN_TARGET");  // tuning only (tools/norm_bench.py)
@@ -802,13 +806,20 @@ static inline int gn_nchunk(int nsamples, int rows_per_sample) {
   const int rpc = gn_rpc(nsamples, rows_per_sample);
   return (rows_per_sample + rpc - 1) / rpc;
 }
+static inline int gn_nchunk_rows(int rows_per_sample) {
+  const int rpc = gn_rpc_rows(rows_per_sample);
+  return (rows_per_sample + rpc - 1) / rpc;
+}
 static inline size_t gn_part_floats(int nsamples, int rows_per_sample, int groups) {
   const int nchunk = gn_nchunk(nsamples, rows_per_sample);
   return ((size_t)nsamples * nchunk * groups * 2 + 3) & ~(size_t)3;  // keep scale/shift 16-B aligned
 }
+static inline size_t gn_part_floats_rows(int nsamples, int rows_per_sample, int groups) {
+  return ((size_t)nsamples * gn_nchunk_rows(rows_per_sample) * groups * 2 + 3) & ~(size_t)3;
+}
 
 extern "C" size_t vst_groupnorm_workspace_bytes(int nsamples, int rows_per_sample, int groups, int C) {
-  return (gn_part_floats(nsamples, rows_per_sample, groups) + (size_t)2 * nsamples * C) * sizeof(float);
+  return (gn_part_floats_rows(nsamples, rows_per_sample, groups) + (size_t)2 * nsamples * C) * sizeof(float);
 }
 
 extern "C" int vst_groupnorm(const void* x1, int ld1, int C1, const void* x2, int ld2, int C2, int nsamples,
@@ -821,10 +832,10 @@ extern "C" int vst_groupnorm(const void* x1, int ld1, int C1, const void* x2, in
   if (C > 4096) return VST_ERR_ARG;
   if (!x2) C2 = 0;
   hipStream_t s = (hipStream_t)stream;
-  const int rpc = gn_rpc(nsamples, rows_per_sample);
-  const int nchunk = gn_nchunk(nsamples, rows_per_sample);
+  const int rpc = gn_rpc_rows(rows_per_sample);
+  const int nchunk = gn_nchunk_rows(rows_per_sample);
   float* part = (float*)workspace;
-  float* scale = part + gn_part_floats(nsamples, rows_per_sample, groups);
+  float* scale = part + gn_part_floats_rows(nsamples, rows_per_sample, groups);
   float* shift = scale + (size_t)nsamples * C;
   const int CH = C / 8;
   const int rps = gn_rps(C);
@@ -847,44 +858,44 @@ static int gn_check(const void* x1, int ld1, int C1, const void* x2, int ld2, in
   return VST_OK;
 }
 
-extern "C" int vst_groupnorm_sums(const void* x1, int ld1, int C1, const void* x2, int ld2, int C2, int nsamples,
-                                  int rows_per_sample, int groups, double* sums, void* workspace, void* stream) {
-  if (gn_check(x1, ld1, C1, x2, ld2, C2, nsamples, rows_per_sample, groups) || !sums || !workspace)
-    return VST_ERR_ARG;
-  if (!x2) C2 = 0;
-  const int C = C1 + C2;
+extern "C" int vst_groupnorm_frame_chunks(int rows_per_frame) {
+  return rows_per_frame > 0 ? gn_nchunk_rows(rows_per_frame) : 0;
+}
+
+extern "C" int vst_groupnorm_frame_partials(const void* x1, int ld1, int C1, int nframes, int rows_per_frame,
+                                            int groups, float* part, void* stream) {
+  if (gn_check(x1, ld1, C1, nullptr, 0, 0, nframes, rows_per_frame, groups) || !part) return VST_ERR_ARG;
+  const int C = C1;
   hipStream_t s = (hipStream_t)stream;
-  const int rpc = gn_rpc(nsamples, rows_per_sample);
-  const int nchunk = gn_nchunk(nsamples, rows_per_sample);
-  const int CH = C / 8;
   const int rps = gn_rps(C);
   const size_t lds = (size_t)2 * rps * C * sizeof(float);
-  float* part = (float*)workspace;
-  hipLaunchKernelGGL(gn_stats_kernel, dim3(nchunk, nsamples), dim3(rps * CH), lds, s, (const bf16_t*)x1, ld1, C1,
-                     (const bf16_t*)x2, ld2, C2, rows_per_sample, rpc, groups, part);
-  hipLaunchKernelGGL(gn_sums_kernel, dim3(nsamples * groups), dim3(64), 0, s, part, nchunk, groups, sums);
+  hipLaunchKernelGGL(gn_stats_kernel, dim3(gn_nchunk_rows(rows_per_frame), nframes), dim3(rps * (C / 8)), lds, s,
+                     (const bf16_t*)x1, ld1, C1, (const bf16_t*)nullptr, 0, 0, rows_per_frame,
+                     gn_rpc_rows(rows_per_frame), groups, part);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 
-extern "C" int vst_groupnorm_apply_sums(const void* x1, int ld1, int C1, const void* x2, int ld2, int C2,
-                                        int nsamples, int rows_per_sample, int groups, const double* sums,
-                                        double count, float eps, const float* gamma, const float* beta, int silu_act,
-                                        void* y, int ldy, void* workspace, void* stream) {
-  if (gn_check(x1, ld1, C1, x2, ld2, C2, nsamples, rows_per_sample, groups) || !sums || !workspace || !y ||
-      !gamma || !beta || (ldy & 7) || !(count > 0.0))
+extern "C" int vst_groupnorm_apply_partials(const void* x1, int ld1, int C1, int nclips, int frames_local,
+                                            int rows_per_frame, int groups, const float* part, int nranks, float eps,
+                                            const float* gamma, const float* beta, int silu_act, void* y, int ldy,
+                                            float* scale_shift, void* stream) {
+  if (gn_check(x1, ld1, C1, nullptr, 0, 0, nclips * frames_local, rows_per_frame, groups) || nclips <= 0 ||
+      frames_local <= 0 || nranks <= 0 || !part || !y || !gamma || !beta || !scale_shift || (ldy & 7) ||
+      ((uintptr_t)scale_shift & 15) || (nclips * C1) % 4)
     return VST_ERR_ARG;
-  if (!x2) C2 = 0;
-  const int C = C1 + C2;
+  const int C = C1;
   hipStream_t s = (hipStream_t)stream;
-  float* scale = (float*)workspace + gn_part_floats(nsamples, rows_per_sample, groups);
-  float* shift = scale + (size_t)nsamples * C;
-  hipLaunchKernelGGL(gn_finalize_sums_kernel, dim3(nsamples * groups), dim3(64), 0, s, sums, count, groups,
-                     C / groups, eps, gamma, beta, scale, shift, C);
-  const int rpc = gn_rpc(nsamples, rows_per_sample);
-  const int nchunk = gn_nchunk(nsamples, rows_per_sample);
-  hipLaunchKernelGGL(gn_apply_kernel, dim3(nchunk, nsamples), dim3(gn_rps(C) * (C / 8)), 0, s, (const bf16_t*)x1,
-                     ld1, C1, (const bf16_t*)x2, ld2, C2, rows_per_sample, rpc, scale, shift, silu_act, (bf16_t*)y,
-                     ldy);
+  float* scale = scale_shift;
+  float* shift = scale + (size_t)nclips * C;
+  const int nck = gn_nchunk_rows(rows_per_frame);
+  const double count = (double)nranks * frames_local * rows_per_frame * (C / groups);
+  hipLaunchKernelGGL(gn_finalize_parts_kernel, dim3(nclips * groups), dim3(64), 0, s, part, nranks, nclips,
+                     frames_local, nck, groups, C / groups, count, eps, gamma, beta, scale, shift, C);
+  const int rows_per_clip = frames_local * rows_per_frame;
+  const int rpc = gn_rpc_rows(rows_per_frame);
+  hipLaunchKernelGGL(gn_apply_kernel, dim3((rows_per_clip + rpc - 1) / rpc, nclips), dim3(gn_rps(C) * (C / 8)), 0, s,
+                     (const bf16_t*)x1, ld1, C1, (const bf16_t*)nullptr, 0, 0, rows_per_clip, rpc, scale, shift,
+                     silu_act, (bf16_t*)y, ldy);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 

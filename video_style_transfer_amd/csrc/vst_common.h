@@ -26,14 +26,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint3
 __device__ __forceinline__ u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, int off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
 }
-// sc1 (device-coherent) forms: write-through stores / L2-bypassing loads for data handed between
-// workgroups on different XCDs without an L2-wide writeback (buffer_wbl2) or invalidate.
-__device__ __forceinline__ void buf_store16_sc1(u32x4 v, __amdgpu_buffer_rsrc_t r, int off) {
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
-}
-__device__ __forceinline__ u32x4 buf_load16_sc1(__amdgpu_buffer_rsrc_t r, int off) {
-  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
-}
 __device__ __forceinline__ u32x2 buf_load8(__amdgpu_buffer_rsrc_t r, int off) {
   return __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
 }

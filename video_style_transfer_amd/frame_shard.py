@@ -5,9 +5,12 @@ attention needs every frame of a clip at each pixel, and whose GroupNorm takes i
 whole clip (diffusers AnimateDiffTransformer3D, built at animatediff/utils.py:31).
 
 With P ranks each holding F/P contiguous frames of every clip, a motion module runs as:
-  1. GroupNorm statistics: per-(clip, group) fp64 (sum, sumsq) over this rank's frames
-     -> all-reduce (2*B*32 doubles) -> every rank normalises its own frames with the clip-wide
-     statistics, then applies proj_in (per token, frame-local);
+  1. GroupNorm statistics: fp32 (sum, sumsq) chunk partials of each of this rank's frames
+     -> all-gather (B*F/P frames x 8 chunks x 32 groups x 2 floats per rank) -> every rank merges the
+     clip's partials in one fixed frame order (fp64) and normalises its own frames, then applies proj_in
+     (per token, frame-local).  The unsharded forward merges the same per-frame partials in the same
+     order, so the statistics -- and with them the whole sharded forward -- are bit-identical to the
+     unsharded one;
   2. frame shard -> pixel shard: one all-to-all hands rank q the pixel slab q (H*W/P pixels) of every
      frame. Each rank now holds all F frames for H*W/P pixels. That is exactly the data the
      frame-axis attention needs. The whole transformer block runs unchanged on it (LN, q/k/v, temporal
@@ -69,6 +72,19 @@ class FrameShard:
         else:
             dist.all_reduce(t, group=self.group)
         return t
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """Every rank's equal-shaped `t` stacked rank-major: [world, *t.shape]."""
+        out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        if self.world == 1:
+            out[0].copy_(t)
+        elif self.backend != "nccl":  # gloo: list all-gather through host memory
+            parts = [torch.empty(t.shape, dtype=t.dtype) for _ in range(self.world)]
+            dist.all_gather(parts, t.cpu().contiguous(), group=self.group)
+            out.copy_(torch.stack(parts))
+        else:
+            dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        return out
 
     def _all_to_all(self, out: torch.Tensor, inp: torch.Tensor):
         if self._staged(inp):

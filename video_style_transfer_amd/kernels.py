@@ -68,13 +68,12 @@ def gemm_kernel_name(M, N, K, kind):
     name = _lib.load().vst_gemm_kernel_name(M, N, K, kind, GEMM_POLICY["tile"], GEMM_POLICY["splits"], _WS_BYTES)
     return name.decode() if name else None
 _WS = {}
-_WS_BYTES = 80 << 20  # split-K slabs / stream-K partial slots (256 x 256 KiB) + 4 KiB of flags
+_WS_BYTES = 80 << 20  # fp32 split-K slabs
 
 
 def _workspace(device):
-    """GEMM workspace per (device, stream) (allocated once, reused stream-ordered): fp32 split-K slabs /
-    stream-K partials, and stream-K flags in its last 4 KiB, which must start (and stay) zero.  One per stream,
-    so GEMMs running concurrently on two streams (the CFG branches, pipeline.py) never share slabs."""
+    """GEMM workspace per (device, stream) (allocated once, reused stream-ordered): the fp32 split-K slabs.  One per
+    stream, so GEMMs queued on two streams never share slabs."""
     key = (device, _stream())
     ws = _WS.get(key)
     if ws is None:
@@ -400,46 +399,46 @@ def group_norm(x1, nsamples, rows_per_sample, groups, eps, gamma, beta, *, silu=
     return out
 
 
-def _gn_ws(x1, nsamples, rows_per_sample, groups, C):
-    ws_bytes = _lib.load().vst_groupnorm_workspace_bytes(nsamples, rows_per_sample, groups, C)
-    return torch.empty((ws_bytes + 3) // 4, dtype=F32, device=x1.device)
-
-
-def group_norm_sums(x1, nsamples, rows_per_sample, groups, *, x2=None, out=None):
-    """Per-(sample, group) fp64 (sum, sumsq) over this rank's rows -> [nsamples*groups*2] (frame-sharded
-    motion GroupNorm: the host all-reduces these across ranks)."""
-    _dev(x1, BF16, "x1")
-    C = x1.shape[1] + (0 if x2 is None else x2.shape[1])
-    if x2 is not None:
-        _dev(x2, BF16, "x2")
-    if x1.shape[0] != nsamples * rows_per_sample:
-        raise _lib.VstError("group_norm_sums: rows != nsamples*rows_per_sample")
+def group_norm_frame_partials(x, nframes, rows_per_frame, groups, *, out=None):
+    """fp32 (sum, sumsq) chunk partials of every frame, [nframes, chunks, groups, 2] (vst_groupnorm_frame_partials):
+    a frame's partials depend on that frame only, so the frame-sharded motion GroupNorm all-gathers them."""
+    _dev(x, BF16, "x")
+    C = x.shape[1]
+    if x.shape[0] != nframes * rows_per_frame:
+        raise _lib.VstError("group_norm_frame_partials: rows != nframes*rows_per_frame")
+    nck = int(_lib.load().vst_groupnorm_frame_chunks(rows_per_frame))
     if out is None:
-        out = torch.empty(nsamples * groups * 2, dtype=torch.float64, device=x1.device)
-    ws = _gn_ws(x1, nsamples, rows_per_sample, groups, C)
-    with _Rec("groupnorm", 0.0, 2.0 * x1.shape[0] * C):
-        _lib.call("vst_groupnorm_sums", _p(x1), _ld(x1), x1.shape[1], _p(x2), 0 if x2 is None else _ld(x2),
-                  0 if x2 is None else x2.shape[1], nsamples, rows_per_sample, groups, _p(out), _p(ws), _stream())
+        out = torch.empty((nframes, nck, groups, 2), dtype=F32, device=x.device)
+    if out.dtype != F32 or not out.is_cuda or not out.is_contiguous() or out.numel() != nframes * nck * groups * 2:
+        raise _lib.VstError("group_norm_frame_partials: out must be contiguous fp32 [nframes, chunks, groups, 2]")
+    with _Rec("groupnorm", 0.0, 2.0 * x.shape[0] * C):
+        _lib.call("vst_groupnorm_frame_partials", _p(x), _ld(x), C, nframes, rows_per_frame, groups, _p(out),
+                  _stream())
     return out
 
 
-def group_norm_apply_sums(x1, nsamples, rows_per_sample, groups, eps, gamma, beta, sums, count, *, silu=False,
-                          x2=None, out=None):
-    """GroupNorm of this rank's rows with statistics from (all-reduced) `sums`; `count` = elements per
-    (sample, group) over the whole clip."""
-    _dev(x1, BF16, "x1")
-    C = x1.shape[1] + (0 if x2 is None else x2.shape[1])
-    if x2 is not None:
-        _dev(x2, BF16, "x2")
-    if sums.dtype != torch.float64 or not sums.is_cuda or sums.numel() != nsamples * groups * 2:
-        raise _lib.VstError("group_norm_apply_sums: sums must be fp64 [nsamples*groups*2] on device")
+def group_norm_apply_partials(x, nclips, frames_local, rows_per_frame, groups, eps, gamma, beta, part, nranks, *,
+                              silu=False, out=None):
+    """GroupNorm of this rank's rows (clips x frames_local frames) with statistics over all nranks * frames_local
+    frames of each clip, merged in one fixed order from `part` = [nranks, nclips, frames_local, chunks, groups, 2]
+    (the all-gather of every rank's group_norm_frame_partials; nranks = 1: the whole clip is here)."""
+    _dev(x, BF16, "x")
+    C = x.shape[1]
+    nck = int(_lib.load().vst_groupnorm_frame_chunks(rows_per_frame))
+    if x.shape[0] != nclips * frames_local * rows_per_frame:
+        raise _lib.VstError("group_norm_apply_partials: rows != nclips*frames_local*rows_per_frame")
+    if part.dtype != F32 or not part.is_cuda or not part.is_contiguous() or \
+            part.numel() != nranks * nclips * frames_local * nck * groups * 2:
+        raise _lib.VstError("group_norm_apply_partials: part must be contiguous fp32 "
+                            "[nranks, nclips, frames_local, chunks, groups, 2] on device")
     if out is None:
-        out = torch.empty((x1.shape[0], C), dtype=BF16, device=x1.device)
-    ws = _gn_ws(x1, nsamples, rows_per_sample, groups, C)
-    with _Rec("groupnorm", 0.0, 2.0 * 2 * x1.shape[0] * C):
-        _lib.call("vst_groupnorm_apply_sums", _p(x1), _ld(x1), x1.shape[1], _p(x2), 0 if x2 is None else _ld(x2),
-                  0 if x2 is None else x2.shape[1], nsamples, rows_per_sample, groups, _p(sums), float(count),
-                  float(eps), _p(gamma), _p(beta), 1 if silu else 0, _p(out), _ld(out), _p(ws), _stream())
+        out = torch.empty((x.shape[0], C), dtype=BF16, device=x.device)
+    _dev(out, BF16, "out")
+    ss = torch.empty(2 * nclips * C, dtype=F32, device=x.device)
+    with _Rec("groupnorm", 0.0, 2.0 * 2 * x.shape[0] * C):
+        _lib.call("vst_groupnorm_apply_partials", _p(x), _ld(x), C, nclips, frames_local, rows_per_frame, groups,
+                  _p(part), nranks, float(eps), _p(gamma), _p(beta), 1 if silu else 0, _p(out), _ld(out), _p(ss),
+                  _stream())
     return out
 
 
@@ -579,11 +578,21 @@ def group_norm_bwd(x, g, nsamples, rows_per_sample, groups, eps, gamma, beta, *,
 
 
 def colsum(x, out=None):
-    """fp32 [N] column sums of a bf16 [M, N] row-major view (bias gradients), deterministic (vst_colsum)."""
+    """fp32 [N] column sums of a bf16 [M, N] row-major view (bias gradients), deterministic (vst_colsum).  The kernel
+    reads 16-B chunks of 8 columns: a view whose width, row stride or base is not 8-column aligned is first copied
+    into a zero-padded [M, ceil8(N)] buffer (the padding columns sum to zero and are dropped)."""
     _dev(x, BF16, "x")
     M, N = x.shape
     if out is None:
         out = torch.empty(N, dtype=F32, device=x.device)
+    if N % 8 or _ld(x) % 8 or x.data_ptr() % 16:
+        n8 = (N + 7) // 8 * 8
+        xp = torch.zeros((M, n8), dtype=BF16, device=x.device)
+        K_copy = xp[:, :N]
+        K_copy.copy_(x)
+        full = colsum(xp)
+        out.copy_(full[:N])
+        return out
     ws = torch.empty((_lib.load().vst_colsum_workspace_bytes(M, N) + 3) // 4, dtype=F32, device=x.device)
     with _Rec("colsum", 0.0, 2.0 * M * N):
         _lib.call("vst_colsum", _p(x), _ld(x), M, N, _p(out), _p(ws), _stream())

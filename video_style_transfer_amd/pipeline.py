@@ -29,15 +29,12 @@ class AnimateDiffDenoiser:
     def __init__(self, unet: UNetMotionModel, num_frames: int, height: int, width: int, *,
                  num_inference_steps: int = 50, guidance_scale: float = 7.5, device=None,
                  scheduler: Optional[EulerDiscreteScheduler] = None, use_graph: bool = True, shard=None,
-                 num_clips: int = 1, cfg_streams: Optional[bool] = None):
+                 num_clips: int = 1):
         """`num_clips` clips are denoised together (the reference loop is one clip, B=1).
         `shard` (frame_shard.FrameShard): this process denoises frames [f0, f0 + F/P) of every clip and
         exchanges with the other ranks inside every motion module.
-        `cfg_streams` (opt-in; env VST_CFG_STREAMS=1): the uncond and cond branches run as two B=1 UNet forwards
-        on two HIP streams forked and joined inside the captured step, so one branch's launch gaps, GEMM fills /
-        epilogues and HBM-bound kernels could overlap the other branch's MFMA work (the branches share nothing
-        until the combine).  Measured slower on MI355X: 76.6 vs 72.8 ms per step, same box
-        (profiles/r3_ab_cfg_streams.txt), so the default is the batched B=2 forward on one stream."""
+        The CFG branches always run as ONE batched B=2 forward on one stream (running them as two B=1 chains on two
+        forked streams measured slower, 76.6 vs 72.8 ms per step, profiles/r3_ab_cfg_streams.txt; removed)."""
         self.unet = unet
         self.nclips = num_clips
         self.shard = shard
@@ -63,11 +60,6 @@ class AnimateDiffDenoiser:
         self.sigmas = self.scheduler.sigmas.to(dev, torch.float32).contiguous()
         self.enc = None
         self.graph = None
-        if cfg_streams is None:
-            import os
-            cfg_streams = os.environ.get("VST_CFG_STREAMS", "0") == "1"
-        self.cfg_streams = bool(cfg_streams) and self.cfg and shard is None
-        self._side = torch.cuda.Stream(device=self.device) if self.cfg_streams else None
 
     def set_prompt_embeds(self, cond_embeds, cond_pooled, uncond_embeds=None, uncond_pooled=None):
         """(1 or num_clips, L, D) text states and (1 or num_clips, P) pooled embeds per branch
@@ -86,8 +78,6 @@ class AnimateDiffDenoiser:
             enc, pooled = cond_embeds, cond_pooled
         self.enc = enc.to(dev, BF16).contiguous()
         self.pooled = pooled.to(dev, BF16).contiguous()
-        # persistent per-branch views (the text K/V cache is keyed on the tensor object)
-        self.enc_branch = (self.enc[:n], self.enc[n:]) if self.cfg else None
         # SDXL time ids (inference_animatediff.py:81-85)
         tid = torch.tensor([self.height, self.width, 0, 0, self.height, self.width], dtype=torch.float32)
         self.time_ids = tid.unsqueeze(0).repeat(self.ncopy * n, 1).to(dev).contiguous()
@@ -97,21 +87,7 @@ class AnimateDiffDenoiser:
         B = self.ncopy * self.nclips
         K.pack_latents(self.lat, self.x, sigmas=self.sigmas, step_idx=self.step_idx, ncopy=self.ncopy)
         emb = self.unet.embed(self.timesteps, self.pooled, self.time_ids, B, step_idx=self.step_idx)
-        if self.cfg_streams:
-            n, rows = self.nclips, self.nclips * self.F * self.h * self.w
-            main = torch.cuda.current_stream(self.device)
-            side = self._side
-            side.wait_stream(main)
-            with torch.cuda.stream(side):  # cond branch
-                noise_c = self.unet.forward_tokens(self.x[rows:], n, self.F, self.h, self.w, emb[n:],
-                                                   self.enc_branch[1])
-            noise_u = self.unet.forward_tokens(self.x[:rows], n, self.F, self.h, self.w, emb[:n],
-                                               self.enc_branch[0])
-            main.wait_stream(side)
-            noise_c.record_stream(main)
-            noise = torch.cat([noise_u, noise_c], 0)
-        else:
-            noise = self.unet.forward_tokens(self.x, B, self.F, self.h, self.w, emb, self.enc, shard=self.shard)
+        noise = self.unet.forward_tokens(self.x, B, self.F, self.h, self.w, emb, self.enc, shard=self.shard)
         K.euler_cfg_step(noise, self.lat, self.sigmas, self.step_idx, guidance=self.guidance, ncopy=self.ncopy)
         K.step_advance(self.step_idx, self.num_steps)
 

@@ -282,21 +282,22 @@ class MotionModule(nn.Module):
     def run(self, x, nimg, H, W, ctx):
         HW = H * W
         shard = ctx.shard
-        if shard is None or shard.world == 1:
-            h = self.norm.run(x, nimg // ctx.F, ctx.F * HW)  # statistics over every frame of a clip
-            h = self.proj_in.run(h)
+        B, G = nimg // ctx.F, self.norm.num_groups
+        # GroupNorm statistics over every frame of a clip, from per-frame partials merged in one fixed frame order:
+        # the same bits whether this process holds the whole clip or a frame shard of it
+        part = K.group_norm_frame_partials(x, nimg, HW, G)
+        P = 1 if shard is None else shard.world
+        if P > 1:
+            part = shard.all_gather(part)
+        h = K.group_norm_apply_partials(x, B, ctx.F, HW, G, self.norm.eps, f32(self.norm.weight), f32(self.norm.bias),
+                                        part, P)
+        h = self.proj_in.run(h)
+        if P == 1:
             for blk in self.transformer_blocks:
                 h = blk.run(h, nimg, HW, ctx)
             return self.proj_out.run(h, residual=x)
-        # frames of each clip spread over ranks (frame_shard.py): clip-wide GN statistics by
-        # all-reduce, frame-axis work on a pixel shard holding every frame
-        Fl, P = ctx.F, shard.world
-        B, G, C = nimg // Fl, self.norm.num_groups, x.shape[1]
-        sums = K.group_norm_sums(x, B, Fl * HW, G)
-        shard.all_reduce_(sums)
-        h = K.group_norm_apply_sums(x, B, Fl * HW, G, self.norm.eps, f32(self.norm.weight), f32(self.norm.bias),
-                                    sums, float(Fl * P * HW * (C // G)))
-        h = self.proj_in.run(h)
+        # frames of each clip spread over ranks (frame_shard.py): frame-axis work on a pixel shard holding every frame
+        Fl = ctx.F
         h = shard.to_pixels(h, B, Fl, HW)
         tctx = dataclasses.replace(ctx, F=Fl * P)
         for blk in self.transformer_blocks:
