@@ -116,12 +116,32 @@ def pmc_traffic(symbol):
     return None, "no PMC profile of this build of libvst_hip.so"
 
 
+def _gpu_busy(ms):
+    """Keep the stream busy for ~`ms` (torch.cuda._sleep, calibrated once), so the host can enqueue a whole
+    instrumented step behind it: the step's launches then run back to back as in the graph replay, and an event
+    interval measures its kernel, not the host's enqueue gap before it (tiny kernels were inflated 2-3x by those)."""
+    global _SLEEP_CYC_PER_MS
+    if _SLEEP_CYC_PER_MS is None:
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(1000)  # warm-up
+        a.record()
+        torch.cuda._sleep(10_000_000)
+        b.record()
+        torch.cuda.synchronize()
+        _SLEEP_CYC_PER_MS = 10_000_000 / max(a.elapsed_time(b), 1e-3)
+    torch.cuda._sleep(int(ms * _SLEEP_CYC_PER_MS))
+
+
+_SLEEP_CYC_PER_MS = None
+
+
 def roofline(den):
-    """One instrumented eager step: HIP events around every launch on its stream.  The CFG branches run one after
-    the other here (B=2 on one stream): per-kernel times of two concurrent streams would overlap."""
+    """One instrumented eager step: HIP events around every launch on its stream, enqueued behind a ~0.4 s busy
+    kernel so the launches execute back to back (their sum is then comparable with the replayed step)."""
     from video_style_transfer_amd import kernels as K
     den.step_idx.zero_()
     torch.cuda.synchronize()
+    _gpu_busy(400.0)
     K.profile_launches(True)
     den._step()
     rec = K.collect_launches()
@@ -233,7 +253,7 @@ def cpu_baseline(args, cfg):
     50-step CFG loop = frames / (2 * steps * t_forward)."""
     from oracle.unet import unet_forward
     from video_style_transfer_amd.weights import synthetic_state_dict
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = _cpu_threads()
     torch.set_num_threads(threads)
     sd = synthetic_state_dict(cfg, args.seed, args.lora_rank or None)
     fr, h = args.cpu_sample_frames, args.size // 8
@@ -248,7 +268,7 @@ def cpu_baseline(args, cfg):
         dt = time.perf_counter() - t0
     del sd
     fps = fr / (2 * args.num_inference_steps * dt)
-    return {"value": fps, "unit": "frames/s", "cores": threads, "kind": "port", "cpu": _cpu_model(),
+    return {"value": fps, "unit": "frames/s", "cores": threads, "kind": "port", "cpu": _cpu_model(), **_cpu_share(),
             "sample": f"1 UNet forward (one CFG branch) of a {fr}-frame {args.size}x{args.size} clip, fp32, "
                       f"{dt:.2f}s, extrapolated x{2 * args.num_inference_steps} forwards"}
 
@@ -258,7 +278,7 @@ def train_cpu_baseline(args, cfg):
     (`cpu_sample_frames` frames at the bench resolution), extrapolated to training frames/s."""
     from oracle.unet import unet_forward
     from video_style_transfer_amd.weights import synthetic_state_dict
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = _cpu_threads()
     torch.set_num_threads(threads)
     sd = synthetic_state_dict(cfg, args.seed, args.lora_rank or None)
     for k, v in sd.items():
@@ -274,9 +294,22 @@ def train_cpu_baseline(args, cfg):
     ((pred - torch.randn_like(pred)) ** 2).mean().backward()
     dt = time.perf_counter() - t0
     del sd
-    return {"value": fr / dt, "unit": "frames/s", "cores": threads, "kind": "port", "cpu": _cpu_model(),
+    return {"value": fr / dt, "unit": "frames/s", "cores": threads, "kind": "port", "cpu": _cpu_model(), **_cpu_share(),
             "sample": f"fp32 oracle forward + backward (motion-module parameters trainable) of a {fr}-frame "
                       f"{args.size}x{args.size} clip: {dt:.2f}s"}
+
+
+def _cpu_threads():
+    """Host threads for the CPU baseline: this GPU's share of the box's cores.  The GPU box gives each GPU a 16-core
+    share and exports OMP_NUM_THREADS=16 for it (the machine's other cores belong to the other GPUs' jobs); elsewhere
+    every core this process may run on."""
+    env = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    return env or len(os.sched_getaffinity(0))
+
+
+def _cpu_share():
+    return {"host_cpus": os.cpu_count(), "cpus_allowed": len(os.sched_getaffinity(0)),
+            "threads_note": "OMP_NUM_THREADS (this GPU's host-core share on the box) threads"}
 
 
 def _cpu_model():
@@ -450,9 +483,11 @@ def bench_train(args, world, rank, local, dev):
     lr_now = float(opt.param_groups[0]["lr"])
     rl = table = step_rl = None
     if not args.no_roofline:
-        # one instrumented eager step (HIP events around every launch on its stream)
-        K.profile_launches(True)
+        # one instrumented eager step (HIP events around every launch on its stream), enqueued behind a busy kernel
         lat_e = lat if vae is None else encode_frames(vae, frames, vgen)
+        torch.cuda.synchronize()
+        _gpu_busy(1500.0)
+        K.profile_launches(True)
         if window:  # one whole window, so the optimizer / clip launches are counted once
             step.window(lat_e, enc, pooled)
         else:

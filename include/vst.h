@@ -52,11 +52,14 @@ size_t vst_gemm_workspace_bytes(int M, int N, int K);
  * LoRACompatibleLinear.forward, unziplora_unet/lora_linear.py:74-81).  Returns 3
  * (VST_ERR_UNSUPPORTED) when the shape is not on the 8-phase kernel or a tile would need u columns
  * outside one 16-aligned block; vst_gemm_lora_supported answers that without a launch (0, or the
- * tile width 256 / 192 it uses). */
+ * tile width 256 / 192 / 320 it uses; 320-wide tiles are 128 rows high). */
 int vst_gemm_lora(const void* x, int ldx, const void* Acat, int ld_acat, int P, int group_n, int group_r,
                   const void* W, int ldw, int M, int N, int K, const float* bias, const void* R, int ldr,
                   void* C, int ldc, void* stream);
 int vst_gemm_lora_supported(int M, int N, int K, int P, int group_n, int group_r);
+/* Test / A-B knob: force the 8-phase kernel's tile width (256, 192 or 320 where legal; 0 = automatic policy) for
+ * every later GEMM of this process; returns the previous setting.  Not on the product path. */
+int vst_p8_force_bn(int bn);
 
 /* attn2 of a BasicTransformerBlock as ONE launch: the q projection (vst_gemm_lora when Acat != NULL, else
  * [x].[W]^T) with the cross-attention over the text tokens as its epilogue,

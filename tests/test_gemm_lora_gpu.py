@@ -137,3 +137,36 @@ def test_run_ops_uses_in_gemm_lora(cuda, K):
     assert rec[0][1] == "gemm_p8<256x192,lora>"
     u = (x.float() @ A.float().t()).to(torch.bfloat16)
     check(out, K.linear(x, W, b, x2=u), 1e-3, 4e-3, "run_ops in-GEMM vs two-pass")
+
+
+@pytest.mark.parametrize("M,Kd,nproj,n_per,r_per,P,use_bias,use_res", [
+    (8192, 1280, 1, 1280, 16, 32, True, True),     # to_out at 16x16 on 128x320 tiles (one full round)
+    (32768, 640, 3, 640, 16, 64, False, False),    # the 32x32 q/k/v: 256-wide tiles straddle q/k, 320-wide do not
+    (8292, 1000, 1, 1280, 16, 32, True, True),     # M tail (8292 = 64 x 128 + 100), K tail
+    (131072, 320, 1, 320, 16, 32, True, False),
+])
+def test_gemm_lora_128x320(cuda, K, M, Kd, nproj, n_per, r_per, P, use_bias, use_res):
+    """vst_gemm_lora on the 128x320 tiles (forced with vst_p8_force_bn): against fp32 torch and the two-pass path,
+    and bit for bit equal to the 256-row tiles where those support the shape (same k order for x.W^T and for u)."""
+    g = torch.Generator().manual_seed(M + Kd + nproj)
+    x, A, W = _operands(M, Kd, nproj, n_per, r_per, P, g, cuda)
+    N = W.shape[0]
+    b = (torch.randn(N, generator=g) * 0.1).to(cuda) if use_bias else None
+    r = rnd(M, N, gen=g).to(cuda) if use_res else None
+    with K.p8_tile_width(320):
+        assert K.gemm_lora_tile(M, N, Kd, P, n_per, r_per) == 320
+        out = K.linear_lora(x, W, A, n_per, r_per, b, residual=r)
+    u = (x.float() @ A.float().t()).to(torch.bfloat16)
+    ref = x.float() @ W[:, :Kd].float().t() + u.float() @ W[:, Kd:].float().t()
+    if b is not None:
+        ref = ref + b
+    if r is not None:
+        ref = ref.to(torch.bfloat16).float() + r.float()
+    check(out, ref, 5e-3, 1e-2, f"gemm_lora 128x320 {M}x{N}x{Kd}+{P} vs fp32")
+    if Kd % 64 == 0:
+        two = K.linear(x, W, b, x2=u, residual=r)
+        check(out, two, 1e-3, 4e-3, f"gemm_lora 128x320 {M}x{N}x{Kd}+{P} vs two-pass")
+    for bn in (192, 256):
+        with K.p8_tile_width(bn):
+            if K.gemm_lora_tile(M, N, Kd, P, n_per, r_per) == bn:
+                assert torch.equal(out, K.linear_lora(x, W, A, n_per, r_per, b, residual=r)), bn

@@ -87,17 +87,20 @@ def test_gemm_underfilled_grids(cuda, K, M, N, Kd, K2):
 
 
 @pytest.mark.parametrize("M,N,K1,K2,geglu", [(8192, 1280, 1280, 32, False), (2000, 640, 320, 0, False),
-                                             (4096, 2560, 640, 64, True), (1024, 320, 2048, 0, False)])
+                                             (4096, 2560, 640, 64, True), (1024, 320, 2048, 0, False),
+                                             (8200, 1920, 1344, 0, False), (131072, 320, 320, 0, False)])
 def test_gemm_8phase_bitwise_equals_ring(cuda, K, M, N, K1, K2, geglu):
-    """The 8-phase 256x256x64 kernel (gemm_p8.hip, tile 8) accumulates every output over k in the same MFMA order as
-    the ring kernel (tile 3, no split): identical bits, tails in M / N / K (LoRA columns) included."""
+    """The 8-phase kernel (gemm_p8.hip: 256x256 tile 8, 256x192 tile 9, 128x320 tile 10) accumulates every output
+    over k in the same MFMA order as the ring kernel (tile 3, no split): identical bits, tails in M / N / K (LoRA
+    columns) included."""
     g = torch.Generator().manual_seed(M + N + K1)
     x, x2 = rnd(M, K1, gen=g).to(cuda), (rnd(M, K2, gen=g).to(cuda) if K2 else None)
     w = rnd(N, K1 + K2, scale=(K1 + K2) ** -0.5, gen=g).to(cuda)
     b = torch.randn(N, generator=g).to(cuda)
     r = None if geglu else rnd(M, N, gen=g).to(cuda)
     outs = []
-    for tile in ((3, 8) if geglu else (3, 8, 9)):  # tile 9: the 8-phase kernel at 256x192 (no GEGLU)
+    # tile 9: the 8-phase kernel at 256x192, tile 10 at 128x320 (no GEGLU; N a multiple of 320)
+    for tile in ((3, 8) if geglu else (3, 8, 9) + ((10,) if N % 320 == 0 else ())):
         K.GEMM_POLICY.update(tile=tile, splits=1)
         try:
             outs.append(K.linear(x, w, b, x2=x2, residual=r, geglu=geglu))
@@ -105,6 +108,31 @@ def test_gemm_8phase_bitwise_equals_ring(cuda, K, M, N, K1, K2, geglu):
             K.GEMM_POLICY.update(tile=0, splits=0)
     for o in outs[1:]:
         assert torch.equal(outs[0], o)
+
+
+@pytest.mark.parametrize("M,N,K1,K2,act", [(8192, 1280, 1280, 32, None), (32768, 640, 640, 32, None),
+                                           (1000, 320, 192, 0, "gelu"), (8292, 3840, 1280, 64, None)])
+def test_gemm_8phase_128x320_vs_torch(cuda, K, M, N, K1, K2, act):
+    """The 128x320 tiles of the 8-phase kernel (tile 10: 4 x 2 waves of 64 x 80) against fp32 torch, with an M tail
+    (8292 = 64 x 128 + 100), the two-source A (LoRA columns) and the GELU epilogue."""
+    g = torch.Generator().manual_seed(M + N + 3)
+    x, x2 = rnd(M, K1, gen=g).to(cuda), (rnd(M, K2, gen=g).to(cuda) if K2 else None)
+    w = rnd(N, K1 + K2, scale=(K1 + K2) ** -0.5, gen=g).to(cuda)
+    b = torch.randn(N, generator=g).to(cuda)
+    r = None if act else rnd(M, N, gen=g).to(cuda)
+    K.GEMM_POLICY.update(tile=10, splits=1)
+    try:
+        assert K.gemm_kernel_name(M, N, K1 + K2, 0) == "gemm_p8<128x320>"
+        out = K.linear(x, w, b, x2=x2, residual=r, act=act)
+    finally:
+        K.GEMM_POLICY.update(tile=0, splits=0)
+    xx = x.float() if x2 is None else torch.cat([x, x2], 1).float()
+    ref = xx @ w.float().t() + b
+    if act:
+        ref = torch.nn.functional.gelu(ref)
+    if r is not None:
+        ref = ref.to(torch.bfloat16).float() + r.float()
+    check(out, ref, name=f"gemm_p8<128x320> {M}x{N}x{K1 + K2}")
 
 
 @pytest.mark.parametrize("M,N,K1,K2,act", [(8192, 1280, 1280, 32, None), (32768, 640, 640, 32, None),

@@ -18,18 +18,25 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CHILD = r"""
-import os, sys, torch, torch.distributed as dist
+import os, sys, time
+t0 = time.time()
+def log(m):
+    print(f"[rccl child {time.time() - t0:6.1f}s] {m}", flush=True)
+import torch, torch.distributed as dist
 sys.path.insert(0, os.environ["VST_ROOT"])
+log("torch imported")
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
 assert str(dist.get_backend()).lower() == "nccl"
+log("nccl process group up")
 n = 1 << 20
 a = torch.zeros(n, device=dev); b = torch.zeros(n, device=dev); c = torch.zeros(3, 5, device=dev)
 ga = torch.empty(1, 3, 5, device=dev); ta = torch.empty(n, device=dev)
 for _ in range(2):  # warm-up on a side stream (communicator setup outside the capture)
     dist.all_reduce(a); dist.all_to_all_single(ta, b); dist.all_gather_into_tensor(ga, c)
 torch.cuda.synchronize()
+log("eager collectives done")
 g = torch.cuda.CUDAGraph()
 s = torch.cuda.Stream()
 s.wait_stream(torch.cuda.current_stream())
@@ -39,6 +46,7 @@ with torch.cuda.stream(s):
         dist.all_to_all_single(ta, b); ta.mul_(3.0)
         dist.all_gather_into_tensor(ga, c)
 torch.cuda.current_stream().wait_stream(s)
+log("captured")
 for it in range(3):
     x = torch.randn(n, device=dev); y = torch.randn(n, device=dev); z = torch.randn(3, 5, device=dev)
     a.copy_(x); b.copy_(y); c.copy_(z)
@@ -75,7 +83,12 @@ def test_rccl_world1_collectives_in_hip_graph():
     if torch.cuda.device_count() == 0:
         pytest.skip("no HIP device")
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), VST_ROOT=ROOT,
-               HSA_ENABLE_IPC_MODE_LEGACY="0")
-    r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
-    print(r.stdout[-2000:], r.stderr[-3000:])
-    assert r.returncode == 0 and "rccl capture ok" in r.stdout, r.stderr[-3000:]
+               HSA_ENABLE_IPC_MODE_LEGACY="0", NCCL_DEBUG=os.environ.get("NCCL_DEBUG", "INFO"))
+    # the child's output streams straight through (a first import on a fresh box can take a minute)
+    out = os.path.join(ROOT, "gpurun_out", "rccl_child.log")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    with open(out, "w") as f:
+        r = subprocess.run([sys.executable, "-u", "-c", CHILD], env=env, stdout=f, stderr=subprocess.STDOUT, timeout=150)
+    text = open(out).read()
+    print(text[-4000:])
+    assert r.returncode == 0 and "rccl capture ok" in text, text[-3000:]

@@ -667,16 +667,64 @@ static bool p8_auto(int M, int N, int K, bool geglu) {
 // 1.5, N = 320 a 192 + 128 split instead of 256 + 64.  A 256x192 tile costs ~0.8 of a 256x256 one (its fill and
 // epilogue do not shrink with it), so it is taken when ceil(tiles192 / CUs) * 0.8 beats ceil(tiles256 / CUs).
 // VST_P8_BN=256 keeps every shape on 256x256 (A/B).
-static bool p8_bn192(int M, int N, bool geglu) {
-  static const int env = [] {
+// Forced 8-phase tile width (256 / 192 / 320, 0 = the policy below): VST_P8_BN, or vst_p8_force_bn (tests, A/B).
+static int g_p8_force_bn = -1;
+static int p8_forced_bn() {
+  if (g_p8_force_bn < 0) {
     const char* e = getenv("VST_P8_BN");
-    return e ? atoi(e) : 0;
-  }();
-  if (geglu || env == 256) return false;
+    g_p8_force_bn = e ? atoi(e) : 0;
+  }
+  return g_p8_force_bn;
+}
+
+static bool p8_bn192(int M, int N, bool geglu) {
+  const int env = p8_forced_bn();
+  if (geglu || env == 256 || env == 320) return false;
   const int mb = (M + 255) / 256, cus = device_cus();
   const int r256 = (mb * ((N + 255) / 256) + cus - 1) / cus, r192 = (mb * ((N + 191) / 192) + cus - 1) / cus;
   return env == 192 || 0.8 * r192 < 0.97 * r256;
 }
+
+// 128x320 tiles of the 8-phase kernel (tile code 10): every SDXL width (320 / 640 / 1280 / 1920 / 3840) splits into
+// 320-column tiles without padding, and M = 8192 gives exactly one full round (256 tiles on 256 CUs) where 256x192
+// gives 224.  A 128x320 tile is 0.625 of a 256x256 one in work.  VST_P8_320 = 1 takes it wherever its round count
+// times 0.7 beats the 256 / 192 choice; VST_P8_BN = 320 wherever it is legal (A/B).
+static bool p8_320_on() {
+  static const int on = [] {
+    const char* e = getenv("VST_P8_320");
+    return e ? atoi(e) : 0;
+  }();
+  return on != 0;
+}
+
+static bool p8_bn320(int M, int N, bool geglu) {
+  const int env = p8_forced_bn();
+  if (geglu || N % 320) return false;
+  if (env == 320) return true;
+  if (!p8_320_on() || env == 256 || env == 192) return false;
+  const int cus = device_cus();
+  const int mb = (M + 255) / 256;
+  const int r256 = (mb * ((N + 255) / 256) + cus - 1) / cus, r192 = (mb * ((N + 191) / 192) + cus - 1) / cus;
+  const int r320 = (((M + 127) / 128) * (N / 320) + cus - 1) / cus;
+  const double best = p8_bn192(M, N, false) ? 0.8 * r192 : r256;
+  return 0.7 * r320 < 0.97 * best;
+}
+
+static int p8_bn(int M, int N, bool geglu) {
+  return p8_bn320(M, N, geglu) ? 320 : p8_bn192(M, N, geglu) ? 192 : 256;
+}
+
+}  // namespace vst
+
+// Force the 8-phase kernel's tile width for every later GEMM of this process (256 / 192 / 320 where legal; 0 = the
+// automatic policy); returns the previous setting.  For tests and A/B runs.
+extern "C" int vst_p8_force_bn(int bn) {
+  const int prev = vst::p8_forced_bn();
+  vst::g_p8_force_bn = (bn == 256 || bn == 192 || bn == 320) ? bn : 0;
+  return prev;
+}
+
+namespace vst {
 
 // tile code 8: AMODE 0, no split-K, a 64-aligned A source split, 256x256 tiles
 static bool p8_applies(int M, int N, int K1, bool two_src) {
@@ -738,7 +786,7 @@ static int run_gemm(GemmArgs& a, int amode, int geglu, int tile, int splits, hip
   if (tile == 8) {
     if (amode != 0 || splits > 1) return VST_ERR_ARG;
     a.splits = 1;
-    return launch_gemm_p8(a, geglu ? 1 : (a.act ? 3 : 0), a.p8_bn == 192 ? 192 : 256, s);
+    return launch_gemm_p8(a, geglu ? 1 : (a.act ? 3 : 0), a.p8_bn == 192 || a.p8_bn == 320 ? a.p8_bn : 256, s);
   }
   if (amode == 2) {  // scalar-gather conv (conv_in): register-staged kernel, no split
     a.splits = 1;
@@ -777,20 +825,28 @@ static bool lora_ingemm_env() {
   return v != 0;
 }
 
-// 0 = not supported (the host falls back to u = x.Acat^T + vst_gemm_ex), else the 8-phase tile width (256 / 192).
-// Every tile's output columns must need u columns inside one 16-aligned block of 16.
-static int lora_ingemm_bn(int M, int N, int K, int P, int gn, int gr) {
+// 0 = not supported (the host falls back to u = x.Acat^T + vst_gemm_ex), else the 8-phase tile width (256 / 192 /
+// 320).  Every tile's output columns must need u columns inside one 16-aligned block of 16.  When the policy's width
+// straddles two projections (the 32x32 q/k/v: C = 640 on 256-wide tiles) and 128x320 tiles are enabled, those are
+// taken: every SDXL projection width is a multiple of 320.
+static bool lora_tiles_ok(int N, int P, int gn, int gr, int bn) {
+  for (int n0 = 0; n0 < N; n0 += bn) {
+    const int g0 = n0 / gn, g1 = (std::min(n0 + bn, N) - 1) / gn;
+    const int lo = (g0 * gr) & ~15, hi = (g1 + 1) * gr;
+    if (hi > lo + 16 || lo + 16 > P) return false;
+  }
+  return true;
+}
+
+static int lora_ingemm_bn(int M, int N, int K, int P, int gn, int gr, int force_bn = 0) {
   if (!lora_ingemm_env() || M <= 0 || N <= 0 || K < 128 || (K & 7) || P <= 0 || (P & 15) || P > 256 || gn <= 0 ||
       gr <= 0 || N % gn || (N / gn) * gr > P)
     return 0;
   if (!p8_auto(M, N, K, false)) return 0;
-  const int bn = p8_bn192(M, N, false) ? 192 : 256;
-  for (int n0 = 0; n0 < N; n0 += bn) {
-    const int g0 = n0 / gn, g1 = (std::min(n0 + bn, N) - 1) / gn;
-    const int lo = (g0 * gr) & ~15, hi = (g1 + 1) * gr;
-    if (hi > lo + 16 || lo + 16 > P) return 0;
-  }
-  return bn;
+  const int bn = force_bn ? force_bn : p8_bn(M, N, false);
+  if (lora_tiles_ok(N, P, gn, gr, bn)) return bn;
+  if (!force_bn && p8_320_on() && N % 320 == 0 && lora_tiles_ok(N, P, gn, gr, 320)) return 320;
+  return 0;
 }
 
 extern "C" int vst_gemm_lora_supported(int M, int N, int K, int P, int group_n, int group_r) {
@@ -837,7 +893,7 @@ static bool xattn_ok(int M, int N, int K, const void* Acat, int P, int gn, int g
       Nk > 80)
     return false;
   if (!p8_auto(M, N, K, false) || !p8_bn192(M, N, false)) return false;
-  return !Acat || lora_ingemm_bn(M, N, K, P, gn, gr) == 192;
+  return !Acat || lora_ingemm_bn(M, N, K, P, gn, gr, 192) == 192;
 }
 
 extern "C" int vst_gemm_cross_attention_supported(int M, int N, int K, int lora, int P, int group_n, int group_r,
@@ -891,9 +947,11 @@ extern "C" const char* vst_gemm_kernel_name(int M, int N, int K, int kind, int t
   if (kind == 3) return "gemm_kernel<conv_in>";
   if (kind == 0 && tile == 0 && rows_applies(M, N, K)) return "gemm_rows";
   if (kind == 0 && (tile == 5 || (tile == 0 && N <= 64 && M >= 1024))) return "gemm_skinny";  // no-epilogue calls
-  if (kind < 0 || kind > 3 || tile < 0 || tile > 9 || tile == 5 || splits < 0) return "";
+  if (kind < 0 || kind > 3 || tile < 0 || tile > 10 || tile == 5 || splits < 0) return "";
   if (tile == 9) return kind == 0 ? "gemm_p8<256x192>" : "";
+  if (tile == 10) return kind == 0 ? "gemm_p8<128x320>" : "";
   if (tile == 0 && kind <= 1 && p8_auto(M, N, K, kind == 1)) {
+    if (splits == 0 && kind == 0 && p8_bn(M, N, false) == 320) return "gemm_p8<128x320>";
     if (splits == 0 && kind == 0 && p8_bn192(M, N, false)) return "gemm_p8<256x192>";
     tile = 8;
   }
@@ -919,9 +977,10 @@ extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int
   if (epilogue == 2 && (R || row_bias)) return VST_ERR_ARG;  // GELU: bias only
   if (R && (ldr & 7)) return VST_ERR_ARG;
   if (row_bias && row_bias_div <= 0) return VST_ERR_ARG;
-  if (tile < 0 || tile > 9 || splits < 0) return VST_ERR_ARG;
-  if ((tile == 8 || tile == 9) && !p8_applies(M, N, K1, A2 != nullptr)) return VST_ERR_ARG;
-  if (tile == 9 && epilogue == 1) return VST_ERR_ARG;  // GEGLU needs the 256-wide tiles
+  if (tile < 0 || tile > 10 || splits < 0) return VST_ERR_ARG;
+  if ((tile == 8 || tile == 9 || tile == 10) && !p8_applies(M, N, K1, A2 != nullptr)) return VST_ERR_ARG;
+  if ((tile == 9 || tile == 10) && epilogue == 1) return VST_ERR_ARG;  // GEGLU needs the 256-wide tiles
+  if (tile == 10 && N % 320) return VST_ERR_ARG;
   const bool skinny_ok = N <= 64 && !A2 && !bias && !row_bias && !R && epilogue == 0;
   if (tile == 5 && !skinny_ok) return VST_ERR_ARG;
   GemmArgs a{};
@@ -942,9 +1001,9 @@ extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int
   if (tile == 5) return run_gemm(a, 0, 0, 5, 1, (hipStream_t)stream);
   const size_t slab_bytes = workspace ? ws_bytes : 0;
   if (tile == 0 && splits == 0 && p8_auto(M, N, K, epilogue == 1) && p8_applies(M, N, K1, A2 != nullptr))
-    tile = p8_bn192(M, N, epilogue == 1) ? 9 : 8;
-  if (tile == 9) {  // the 8-phase kernel at 256x192
-    a.p8_bn = 192;
+    tile = p8_bn(M, N, epilogue == 1) == 320 ? 10 : p8_bn192(M, N, epilogue == 1) ? 9 : 8;
+  if (tile == 9 || tile == 10) {  // the 8-phase kernel at 256x192 / 128x320
+    a.p8_bn = tile == 9 ? 192 : 320;
     return run_gemm(a, 0, 0, 8, 1, (hipStream_t)stream);
   }
   choose(M, N, K, epilogue == 1, 0, slab_bytes, tile, splits);

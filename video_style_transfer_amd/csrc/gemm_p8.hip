@@ -30,25 +30,33 @@
 
 namespace vst {
 
-// BN = 256 (wave tile 128 x 64) or 192 (128 x 48: the N = 1280 / 640 / 320 grids in fewer-padded, fuller rounds).
-// Slot Bnq0 holds the first 32 columns of every wave column, Bnq1 the remaining WN - 32 (32 or 16).
-template <int BN_>
-struct P8Cfg {  // the epilogue's view of the tile (same wave tiling as RingCfg<256, BN, 2, 4, S>)
-  static constexpr int BM = 256, BN = BN_, WAVES_M = 2, WAVES_N = 4, NWAVES = 8, THREADS = 512;
-  static constexpr int WM = 128, WN = BN / 4, MI = 8, NJ = WN / 16;
-  static constexpr int RB1 = WN - 32;               // Bnq1 rows per wave column
-  static constexpr int NJ1 = RB1 / 16;              // Bnq1 fragments per wave
-  static constexpr int NPB1 = 4 * RB1 / 64;         // Bnq1 1-KiB pieces per wave (2 or 1)
-  static constexpr int SLOT = 128 * 64 * 2;         // 16 KiB: Amq0, Amq1, Bnq0
-  static constexpr int SLOT_B1 = 4 * RB1 * 128;     // Bnq1
-  static constexpr int BUF = 3 * SLOT + SLOT_B1;
+// BM x BN tiles, 8 waves as 2 (M) x 4 (N), wave tile WM x WN = BM/2 x BN/4:
+//   256 x 256 (128 x 64), 256 x 192 (128 x 48: the N = 1280 / 640 / 320 grids in fewer-padded, fuller rounds), and
+//   128 x 320 (64 x 80: every SDXL width is a multiple of 320, so N = 320 / 640 / 1280 / 1920 / 3840 split without
+//   padding and M = 8192 gives exactly one full round of 256 tiles on 256 CUs).
+// Slot A0 / A1 hold the first / second half of every wave row's WM rows; slot B0 the first 32 columns of every wave
+// column, B1 the remaining WN - 32 (32, 16 or 48).
+template <int BN_, int BM_ = 256>
+struct P8Cfg {  // the epilogue's view of the tile (same wave tiling as RingCfg<BM, BN, 2, 4, S>)
+  static constexpr int BM = BM_, BN = BN_, WAVES_M = 2, WAVES_N = 4, NWAVES = 8, THREADS = 512;
+  static constexpr int WM = BM / 2, WN = BN / 4, MI = WM / 16, NJ = WN / 16;
+  static constexpr int HALF = WM / 2;               // rows of a wave row in one A slot
+  static constexpr int MQR = HALF / 16;             // 16-row blocks per A quadrant (4 or 2)
+  static constexpr int NPA = BM / 128;              // A slot 1-KiB pieces per wave (2 or 1)
+  static constexpr int RB1 = WN - 32;               // B1 rows per wave column
+  static constexpr int NJ1 = RB1 / 16;              // B1 fragments per wave
+  static constexpr int NPB1 = 4 * RB1 / 64;         // B1 1-KiB pieces per wave (2, 1 or 3)
+  static constexpr int SLOT_A = BM / 2 * 128;       // A0, A1
+  static constexpr int SLOT_B0 = 128 * 128;         // B0: 4 wave columns x 32 rows
+  static constexpr int SLOT_B1 = 4 * RB1 * 128;     // B1
+  static constexpr int BUF = 2 * SLOT_A + SLOT_B0 + SLOT_B1;
   static constexpr int EPI_BYTES = BM * (BN * 2 + 16);
   static constexpr int LDS = 2 * BUF > EPI_BYTES ? 2 * BUF : EPI_BYTES;
   // LORA: two 2-KiB Acat slots ([16 u columns][64 k] per k-tile) + 1 KiB sink for the waves without a piece, then
   // the tile's up-projection columns V [BN rows][16] (32-B rows), staged once in the prologue
-  static constexpr int LORA_OFF = 2 * BUF, V_OFF = 2 * BUF + 5 * 1024, LORA_END = V_OFF + 256 * 32;
+  static constexpr int LORA_OFF = 2 * BUF, V_OFF = 2 * BUF + 5 * 1024, LORA_END = V_OFF + BN * 32;
   static constexpr int LDS_LORA = LORA_END > EPI_BYTES ? LORA_END : EPI_BYTES;
-  static_assert(BN == 256 || BN == 192, "tile width");
+  static_assert((BM == 256 && (BN == 256 || BN == 192)) || (BM == 128 && BN == 320), "tile shape");
   static_assert(LDS <= 160 * 1024 && LDS_LORA <= 160 * 1024, "LDS budget");
 };
 
@@ -290,26 +298,29 @@ __device__ __forceinline__ void xattn_epilogue(const GemmArgs& p, char* smem, co
 // loop u is rounded to bf16 (the reference's rounding point of lora_layer's down output), exchanged through LDS and
 // multiplied by the tile's up-projection columns of W (K + ub0 ...) as one extra 16x16x32 step per accumulator —
 // the same operands, in the same order, as the [x | u] . [W | V]^T k-tile it replaces.
-template <int EPI, int BN, bool LORA = false>
+template <int EPI, int BN, bool LORA = false, int PH = 3, int BM = 256>
 __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  using Cfg = P8Cfg<BN>;
+  using Cfg = P8Cfg<BN, BM>;
   static_assert(EPI != 1 || BN == 256, "GEGLU needs 64-column [hidden | gate] blocks");
   static_assert(!LORA || EPI != 1, "in-GEMM LoRA: linear epilogue");
-  static_assert(EPI != 4 || BN == 192, "cross-attention epilogue: 192-column tiles (3 heads)");
+  static_assert(EPI != 4 || (BN == 192 && BM == 256), "cross-attention epilogue: 256 x 192 tiles (3 heads)");
   constexpr int LX = LORA ? 1 : 0;  // the Acat DMA in the vmcnt counts
-  constexpr int SLOT = Cfg::SLOT, BUF = Cfg::BUF, RB1 = Cfg::RB1, NJ1 = Cfg::NJ1, NPB1 = Cfg::NPB1;
+  constexpr int BUF = Cfg::BUF, RB1 = Cfg::RB1, NJ1 = Cfg::NJ1, NPB1 = Cfg::NPB1, NPA = Cfg::NPA;
+  constexpr int HALF = Cfg::HALF, MQR = Cfg::MQR;
+  // slot offsets inside a buffer: A0, A1, B0, B1
+  auto slot_off = [](int s_) { return s_ < 2 ? s_ * Cfg::SLOT_A : (s_ == 2 ? 2 * Cfg::SLOT_A : 2 * Cfg::SLOT_A + Cfg::SLOT_B0); };
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid >> 2, wc = wid & 3;
   const int fr = lane & 15, fq = lane >> 4;
-  const int nbm = (p.M + 255) / 256, nbn = (p.N + BN - 1) / BN;
+  const int nbm = (p.M + BM - 1) / BM, nbn = (p.N + BN - 1) / BN;
   const int ntiles = nbm * nbn;
   auto tile_origin = [&](int t, int& m0, int& n0) {
     const int GROUP_M = 8, in_group = GROUP_M * nbn;
     const int gid = t / in_group, first_m = gid * GROUP_M;
     const int gsize = min(nbm - first_m, GROUP_M);
-    m0 = (first_m + (t - gid * in_group) % gsize) * 256;
+    m0 = (first_m + (t - gid * in_group) % gsize) * BM;
     n0 = ((t - gid * in_group) / gsize) * BN;
   };
   const auto ra1 = make_rsrc(p.A1, p.a1_bytes);
@@ -327,7 +338,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
 
   // ---- per-lane DMA descriptors: slot s in {Amq0, Amq1, Bnq0, Bnq1}; 1-KiB piece q = PB + PS*pc of a slot holds slot
   //      rows 8q .. 8q+7 (row 8q + (lane >> 3)); this lane moves chunk c = (lane & 7) ^ ((row >> 1) & 7) of that row.
-  constexpr int NPC = 2, PS = 8;
+  constexpr int NPC = NPB1 > 2 ? NPB1 : 2, PS = 8;  // pieces per wave of the largest slot (B0: 2, B1: up to 3)
   const int PB = wid;
   uint32_t base1[4][NPC], base2[2][NPC];
   int c8[4][NPC];
@@ -352,27 +363,27 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
         const int c = (lane & 7) ^ ((r >> 1) & 7);
         c8[s][pc] = c * 8;
         if (s < 2) {
-          const int m = m0 + (r >> 6) * 128 + s * 64 + (r & 63);
+          const int m = m0 + (r / HALF) * Cfg::WM + s * HALF + (r % HALF);
           base1[s][pc] = m < p.M ? (uint32_t)(m * p.lda1 + c * 8) * 2u : (uint32_t)kOOB;
           base2[s][pc] = m < p.M ? (uint32_t)(m * p.lda2 + c * 8) * 2u : (uint32_t)kOOB;
         } else {
           const int rb = s == 2 ? 32 : RB1;
           const int n = n0 + (r / rb) * Cfg::WN + (s - 2) * 32 + (r % rb);
-          base1[s][pc] = (n < p.N && (s == 2 || pc < NPB1)) ? (uint32_t)(n * p.ldw + c * 8) * 2u : (uint32_t)kOOB;
+          base1[s][pc] = (n < p.N && (s == 2 ? pc < 2 : pc < NPB1)) ? (uint32_t)(n * p.ldw + c * 8) * 2u : (uint32_t)kOOB;
         }
       }
   };
   // slot s of k-tile kt into buffer (kt & 1); kt >= kend: out-of-range offsets (zeros), keeps vmcnt counts uniform
   auto dma_slot = [&](int s, int kt, int kend) {
     if ((abl & 1) && kt > 1) return;
-    char* dst = smem + (kt & 1) * BUF + s * SLOT + PB * 1024;
+    char* dst = smem + (kt & 1) * BUF + slot_off(s) + PB * 1024;
     const int k0 = kt * 64;
     const bool live = kt < kend && !((abl & 32) && kt > 1);
     if (s < 2) {
       const bool second = k0 >= p.K1;
       const uint32_t kb = (uint32_t)(second ? k0 - p.K1 : k0) * 2u;
 #pragma unroll
-      for (int pc = 0; pc < NPC; ++pc) {
+      for (int pc = 0; pc < NPA; ++pc) {
         const bool kin = live && (!ktail || k0 + c8[s][pc] < p.K);
         const int off = kin ? (int)((second ? base2[s][pc] : base1[s][pc]) + kb) : kOOB;
         p8_dma16(second ? ra2 : ra1, dst + pc * PS * 1024, off);
@@ -380,7 +391,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     } else {
       const uint32_t kb = (uint32_t)k0 * 2u;
 #pragma unroll
-      for (int pc = 0; pc < (s == 3 ? NPB1 : NPC); ++pc) {
+      for (int pc = 0; pc < (s == 3 ? NPB1 : 2); ++pc) {
         const bool kin = live && (!ktail || k0 + c8[s][pc] < p.K);
         p8_dma16(rw, dst + pc * PS * 1024, kin ? (int)(base1[s][pc] + kb) : kOOB);
       }
@@ -390,17 +401,17 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   // slot s of a k-tile that is live and fully inside K (every k-tile but the last two of a segment): no checks
   auto dma_fast = [&](int s, int kt) {
     if ((abl & 1) && kt > 1) return;
-    char* dst = smem + (kt & 1) * BUF + s * SLOT + PB * 1024;
+    char* dst = smem + (kt & 1) * BUF + slot_off(s) + PB * 1024;
     const int k0 = kt * 64;
     if (s < 2) {
       const bool second = k0 >= p.K1;
       const uint32_t kb = (uint32_t)(second ? k0 - p.K1 : k0) * 2u;
 #pragma unroll
-      for (int pc = 0; pc < NPC; ++pc)
+      for (int pc = 0; pc < NPA; ++pc)
         p8_dma16(second ? ra2 : ra1, dst + pc * PS * 1024, (int)((second ? base2[s][pc] : base1[s][pc]) + kb));
     } else {
 #pragma unroll
-      for (int pc = 0; pc < (s == 3 ? NPB1 : NPC); ++pc)
+      for (int pc = 0; pc < (s == 3 ? NPB1 : 2); ++pc)
         p8_dma16(rw, dst + pc * PS * 1024, (int)(base1[s][pc] + (uint32_t)k0 * 2u));
     }
   };
@@ -415,32 +426,34 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     }
   };
 
-  f32x4 acc[8][Cfg::NJ];
+  f32x4 acc[Cfg::MI][Cfg::NJ];
   f32x4 acc_u[2];   // LORA: u of row block wc of row quadrants 0 / 1 (this wave's row half)
   bf16x8 fl[2];     // LORA: Acat fragments of the current k-tile (16 u columns x 2 k-halves)
   bf16x8 fu[2];     // LORA: A fragments of row block wc of the current row quadrant (a copy of fa[wc], read
                     // separately so the u MFMAs index no register array by the runtime wc)
-  bf16x8 fa[4][2];         // A fragments of the current row quadrant (mq): 4 x 16 rows x 2 k-halves
-  bf16x8 fb0[2][2], fb1[2][2];  // W fragments of column quadrants nq0 / nq1
+  bf16x8 fa[MQR][2];       // A fragments of the current row quadrant (mq): MQR x 16 rows x 2 k-halves
+  bf16x8 fb0[2][2], fb1[NJ1 > 2 ? NJ1 : 2][2];  // W fragments of column quadrants nq0 / nq1
 #ifdef VST_P8_TRACE
-  for (int i = 0; i < 4; ++i) for (int h = 0; h < 2; ++h) fa[i][h] = bf16x8{};
-  for (int j = 0; j < 2; ++j) for (int h = 0; h < 2; ++h) fb0[j][h] = fb1[j][h] = bf16x8{};
+  for (int i = 0; i < MQR; ++i) for (int h = 0; h < 2; ++h) fa[i][h] = bf16x8{};
+  for (int j = 0; j < 2; ++j) for (int h = 0; h < 2; ++h) fb0[j][h] = bf16x8{};
+  for (int j = 0; j < NJ1; ++j) for (int h = 0; h < 2; ++h) fb1[j][h] = bf16x8{};
 #endif
   auto read_a = [&](int buf, int mq) {
     if (abl & 16) return;
-    const char* S = smem + buf * BUF + mq * SLOT;
+    const char* S = smem + buf * BUF + slot_off(mq);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MQR; ++i)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) fa[i][h] = *reinterpret_cast<const bf16x8*>(S + p8_off(wr * 64 + i * 16 + fr, h * 4 + fq));
-    if constexpr (LORA) {
+      for (int h = 0; h < 2; ++h) fa[i][h] = *reinterpret_cast<const bf16x8*>(S + p8_off(wr * HALF + i * 16 + fr, h * 4 + fq));
+    if constexpr (LORA) {  // row block wc of the quadrant (MQR < 4: waves wc >= MQR repeat a block, their u unused)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) fu[h] = *reinterpret_cast<const bf16x8*>(S + p8_off(wr * 64 + wc * 16 + fr, h * 4 + fq));
+      for (int h = 0; h < 2; ++h)
+        fu[h] = *reinterpret_cast<const bf16x8*>(S + p8_off(wr * HALF + (wc % MQR) * 16 + fr, h * 4 + fq));
     }
   };
-  auto read_b = [&](int buf, int nq, bf16x8 (&fb)[2][2]) {
+  auto read_b = [&](int buf, int nq, auto& fb) {
     if (abl & 16) return;
-    const char* S = smem + buf * BUF + (2 + nq) * SLOT;
+    const char* S = smem + buf * BUF + slot_off(2 + nq);
     const int rb = nq == 0 ? 32 : RB1;
 #pragma unroll
     for (int j = 0; j < (nq == 0 ? 2 : NJ1); ++j)
@@ -460,15 +473,15 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   };
 #define VST_P8_QUAD(MQ, NQ, FB)                                                                        \
   if (!(abl & 2)) {                                                                                  \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < ((NQ) == 0 ? 2 : NJ1); ++j) \
-        _Pragma("unroll") for (int h = 0; h < 2; ++h) acc[(MQ) * 4 + i][(NQ) * 2 + j] =              \
-        __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j][h], fa[i][h], acc[(MQ) * 4 + i][(NQ) * 2 + j], 0, 0, 0); \
+    _Pragma("unroll") for (int i = 0; i < MQR; ++i) _Pragma("unroll") for (int j = 0; j < ((NQ) == 0 ? 2 : NJ1); ++j) \
+        _Pragma("unroll") for (int h = 0; h < 2; ++h) acc[(MQ) * MQR + i][(NQ) * 2 + j] =              \
+        __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j][h], fa[i][h], acc[(MQ) * MQR + i][(NQ) * 2 + j], 0, 0, 0); \
   }
 
   // k-tiles [kb, ke) of the current tile into acc (zeroed here); ends with the LDS drained and free for reuse
   auto run_segment = [&](int kb, int ke) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < Cfg::MI; ++i)
 #pragma unroll
       for (int j = 0; j < Cfg::NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     acc_u[0] = acc_u[1] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -483,11 +496,17 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       const bool ok = row < BN && n < p.N;
       p8_dma16(make_rsrc(p.Wt, p.wtail_bytes), smem + Cfg::V_OFF + wid * 1024,
                ok ? (int)(((uint32_t)n * p.ldw + p.K + ub0 + 8 * (lane & 1)) * 2u) : kOOB);
+      if constexpr (BN > 256) {  // rows 256 .. BN - 1 (waves 0-1; older than every slot DMA like the first piece)
+        const int row2 = 256 + row, n2 = n0_tile + row2;
+        if (wid < 2)
+          p8_dma16(make_rsrc(p.Wt, p.wtail_bytes), smem + Cfg::V_OFF + (8 + wid) * 1024,
+                   row2 < BN && n2 < p.N ? (int)(((uint32_t)n2 * p.ldw + p.K + ub0 + 8 * (lane & 1)) * 2u) : kOOB);
+      }
     }
     dma_slot(0, kb, ke); dma_lora(kb, ke, true); dma_slot(2, kb, ke); dma_slot(3, kb, ke);
     dma_slot(1, kb, ke); dma_slot(3, kb + 1, ke); dma_slot(0, kb + 1, ke); dma_lora(kb + 1, ke, true);
     dma_slot(2, kb + 1, ke);
-    p8_vmwait<6 + NPB1 + LX>();  // Amq0, (Acat,) Bnq0, Bnq1 of kb landed
+    p8_vmwait<2 * NPA + 2 + NPB1 + LX>();  // A0, (Acat,) B0, B1 of kb landed
     p8_barrier();
     VST_P8_STAMP(1)
     read_b(kb & 1, 1, fb1);
@@ -503,7 +522,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       read_a(buf, 0);
       read_b(buf, 0, fb0);
       read_l(buf);
-      if (!(abl & 4)) p8_vmwait<4 + NPB1 + LX>();  // Amq1(t) landed
+      if (!(abl & 4)) p8_vmwait<NPA + 2 + NPB1 + LX>();  // A1(t) landed
       dma(1, t + 1);
       p8_barrier();
       lora_mfma(acc_u[0], 0);
@@ -513,7 +532,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       p8_barrier();
       // I1
       read_a(buf, 1);
-      if (!(abl & 4)) p8_vmwait<6 + LX>();  // Bnq1(t+1) landed
+      if (!(abl & 4)) p8_vmwait<2 * NPA + 2 + LX>();  // B1(t+1) landed
       dma(3, t + 2);
       p8_barrier();
       lora_mfma(acc_u[1], 0);
@@ -522,7 +541,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       p8_barrier();
       // I2
       read_b(buf ^ 1, 1, fb1);
-      if (!(abl & 4)) p8_vmwait<2 + NPB1>();  // Amq0(t+1), Bnq0(t+1) landed
+      if (!(abl & 4)) p8_vmwait<NPA + NPB1>();  // A0(t+1), B0(t+1) landed
       dma(0, t + 2);
       dma_lora(t + 2, ke, !FAST);
       dma(2, t + 2);
@@ -538,13 +557,91 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the trailing zero DMAs land before LDS reuse
     p8_barrier();
   };
+  // PH = 2: two barrier intervals of 32 MFMAs per k-tile (24 at BN = 192), so every load segment of one wave group
+  // runs beside a full-length MFMA segment of the other, and each wave's DMAs split evenly over the two (the 3-interval
+  // schedule pairs its 4-DMA interval with a 16-MFMA one):
+  //   J0(t) = {read A0(t), B0(t), B1(t), Acat(t); wait A1(t); issue B1(t+1), A1(t+1)} | Q(0,0) + Q(0,1)
+  //   J1(t) = {read A1(t);                        wait A0/B0/B1(t+1); issue A0(t+2) (+Acat), B0(t+2)} | Q(1,1) + Q(1,0)
+  // Every load segment ends with its LDS reads retired (lgkmcnt(0)) before its barrier, so a slot read in interval X is
+  // refilled from interval X + 1 on (WAR); a slot waited for in interval X is read in X + 1 (RAW, both groups' waits
+  // precede the barrier the later reader passes).  Same k order per accumulator as PH = 3: bitwise-equal results.
+  auto run_segment2 = [&](int kb, int ke) {
+#pragma unroll
+    for (int i = 0; i < Cfg::MI; ++i)
+#pragma unroll
+      for (int j = 0; j < Cfg::NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc_u[0] = acc_u[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (LORA) {  // V [BN][16] of this tile (older than every slot DMA: the first wait below covers it)
+      const int row = wid * 32 + (lane >> 1), n = n0_tile + row;
+      const bool ok = row < BN && n < p.N;
+      p8_dma16(make_rsrc(p.Wt, p.wtail_bytes), smem + Cfg::V_OFF + wid * 1024,
+               ok ? (int)(((uint32_t)n * p.ldw + p.K + ub0 + 8 * (lane & 1)) * 2u) : kOOB);
+      if constexpr (BN > 256) {  // rows 256 .. BN - 1 (waves 0-1; older than every slot DMA like the first piece)
+        const int row2 = 256 + row, n2 = n0_tile + row2;
+        if (wid < 2)
+          p8_dma16(make_rsrc(p.Wt, p.wtail_bytes), smem + Cfg::V_OFF + (8 + wid) * 1024,
+                   row2 < BN && n2 < p.N ? (int)(((uint32_t)n2 * p.ldw + p.K + ub0 + 8 * (lane & 1)) * 2u) : kOOB);
+      }
+    }
+    dma_slot(0, kb, ke); dma_lora(kb, ke, true); dma_slot(2, kb, ke); dma_slot(3, kb, ke);
+    dma_slot(1, kb, ke);
+    dma_slot(0, kb + 1, ke); dma_lora(kb + 1, ke, true); dma_slot(2, kb + 1, ke);
+    p8_vmwait<2 * NPA + 2 + LX>();  // A0, (Acat,) B0, B1 of kb landed; A1(kb), A0/B0(kb + 1) in flight
+    p8_barrier();
+    VST_P8_STAMP(1)
+    if (late) p8_barrier();
+    if (late) __builtin_amdgcn_s_setprio(1);
+    auto ktile2 = [&](int t, auto fast_tag) {
+      constexpr bool FAST = decltype(fast_tag)::value;
+      auto dma = [&](int s_, int kt) {
+        if constexpr (FAST) dma_fast(s_, kt); else dma_slot(s_, kt, ke);
+      };
+      const int buf = t & 1;
+      // J0
+      read_a(buf, 0);
+      read_b(buf, 0, fb0);
+      read_b(buf, 1, fb1);
+      read_l(buf);
+      if (!(abl & 4)) p8_vmwait<NPA + 2 + LX>();  // A1(t) landed
+      dma(3, t + 1);
+      dma(1, t + 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      p8_barrier();
+      lora_mfma(acc_u[0], 0);
+      VST_P8_QUAD(0, 0, fb0)
+      VST_P8_QUAD(0, 1, fb1)
+      lora_mfma(acc_u[0], 1);
+      p8_barrier();
+      // J1
+      read_a(buf, 1);
+      if (!(abl & 4)) p8_vmwait<NPA>();  // A0, (Acat,) B0, B1 of t + 1 landed
+      dma(0, t + 2);
+      dma_lora(t + 2, ke, !FAST);
+      dma(2, t + 2);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      p8_barrier();
+      lora_mfma(acc_u[1], 0);
+      VST_P8_QUAD(1, 1, fb1)
+      VST_P8_QUAD(1, 0, fb0)
+      lora_mfma(acc_u[1], 1);
+      p8_barrier();
+    };
+    int t = kb;
+    const int ke_fast = ke - 2 - (ktail ? 1 : 0);
+    for (; t < ke_fast; ++t) ktile2(t, std::true_type{});
+    for (; t < ke; ++t) ktile2(t, std::false_type{});
+    if (!late) p8_barrier();
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the trailing zero DMAs land before LDS reuse
+    p8_barrier();
+  };
 #undef VST_P8_QUAD
 
   int m0, n0;
   VST_P8_STAMP(0)
   tile_origin(xcd_remap(blockIdx.x, ntiles), m0, n0);
   setup_tile(m0, n0);
-  run_segment(0, nk);
+  if constexpr (PH == 2) run_segment2(0, nk);
+  else run_segment(0, nk);
   VST_P8_STAMP(2)
   if constexpr (LORA) {
     // u (bf16) -> LDS [256 rows][16 columns] (the drained ring), then acc += u . V^T over the 32-wide window
@@ -555,7 +652,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       u32x2 v;
       v[0] = pack2bf(acc_u[q][0], acc_u[q][1]);
       v[1] = pack2bf(acc_u[q][2], acc_u[q][3]);
-      *reinterpret_cast<u32x2*>(U + (wr * 128 + q * 64 + wc * 16 + fr) * 32 + fq * 8) = v;
+      if (wc < MQR) *reinterpret_cast<u32x2*>(U + (wr * Cfg::WM + q * HALF + wc * 16 + fr) * 32 + fq * 8) = v;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -567,8 +664,8 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       fv[j] = fq < 2 ? v : zero8;
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      bf16x8 fu = *reinterpret_cast<const bf16x8*>(U + (wr * 128 + i * 16 + fr) * 32 + (fq & 1) * 16);
+    for (int i = 0; i < Cfg::MI; ++i) {
+      bf16x8 fu = *reinterpret_cast<const bf16x8*>(U + (wr * Cfg::WM + i * 16 + fr) * 32 + (fq & 1) * 16);
       fu = fq < 2 ? fu : zero8;
 #pragma unroll
       for (int j = 0; j < Cfg::NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fv[j], fu, acc[i][j], 0, 0, 0);
@@ -585,23 +682,41 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   VST_P8_STAMP(3)
 }
 
-template <int EPI, int BN, bool LORA = false>
-static int launch_p8_epi(const GemmArgs& a, hipStream_t s) {
+// VST_P8_PH = 2 / 3: the k-loop schedule (A/B; see run_segment2)
+static int p8_ph_env() {
+  static const int v = [] {
+    const char* e = getenv("VST_P8_PH");
+    return e ? atoi(e) : 3;
+  }();
+  return v;
+}
+
+template <int EPI, int BN, bool LORA, int PH, int BM>
+static int launch_p8_ph(const GemmArgs& a, hipStream_t s) {
   static bool attr = false;
-  constexpr int lds = EPI == 4 ? 160 * 1024 : (LORA ? P8Cfg<BN>::LDS_LORA : P8Cfg<BN>::LDS);
+  using Cfg = P8Cfg<BN, BM>;
+  constexpr int lds = EPI == 4 ? 160 * 1024 : (LORA ? Cfg::LDS_LORA : Cfg::LDS);
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_p8_kernel<EPI, BN, LORA>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              lds);
+    (void)hipFuncSetAttribute((const void*)gemm_p8_kernel<EPI, BN, LORA, PH, BM>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  const int nwg = ((a.M + 255) / 256) * ((a.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_p8_kernel<EPI, BN, LORA>), dim3(nwg), dim3(512), lds, s, a);
+  const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_p8_kernel<EPI, BN, LORA, PH, BM>), dim3(nwg), dim3(512), lds, s, a);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+}
+
+// BN = 320 runs 128-row tiles (P8Cfg)
+template <int EPI, int BN, bool LORA = false>
+static int launch_p8_epi(const GemmArgs& a, hipStream_t s) {
+  constexpr int BM = BN == 320 ? 128 : 256;
+  return p8_ph_env() == 2 ? launch_p8_ph<EPI, BN, LORA, 2, BM>(a, s) : launch_p8_ph<EPI, BN, LORA, 3, BM>(a, s);
 }
 
 // in-GEMM LoRA down-projection (a.la set): epilogue 0 (bias / residual), bn 256 or 192
 int launch_gemm_p8_lora(const GemmArgs& a, int bn, hipStream_t s) {
   if (!a.la) return VST_ERR_ARG;
+  if (bn == 320) return launch_p8_epi<0, 320, true>(a, s);
   return bn == 192 ? launch_p8_epi<0, 192, true>(a, s) : launch_p8_epi<0, 256, true>(a, s);
 }
 
@@ -611,13 +726,13 @@ int launch_gemm_p8_xattn(const GemmArgs& a, hipStream_t s) {
   return a.la ? launch_p8_epi<4, 192, true>(a, s) : launch_p8_epi<4, 192, false>(a, s);
 }
 
-// epi: 0 bias / row bias / residual, 1 GEGLU, 3 bias + GELU; bn: 256 or 192 (not with GEGLU)
+// epi: 0 bias / row bias / residual, 1 GEGLU, 3 bias + GELU; bn: 256, 192 or 320 (128-row tiles; not with GEGLU)
 int launch_gemm_p8(const GemmArgs& a, int epi, int bn, hipStream_t s) {
   if (a.A2 && (a.K1 & 63)) return VST_ERR_ARG;  // a 64-deep k-tile must not straddle the two A sources
-  if (bn == 192) {
+  if (bn == 192 || bn == 320) {
     switch (epi) {
-      case 0: return launch_p8_epi<0, 192>(a, s);
-      case 3: return launch_p8_epi<3, 192>(a, s);
+      case 0: return bn == 192 ? launch_p8_epi<0, 192>(a, s) : launch_p8_epi<0, 320>(a, s);
+      case 3: return bn == 192 ? launch_p8_epi<3, 192>(a, s) : launch_p8_epi<3, 320>(a, s);
       default: return VST_ERR_ARG;
     }
   }

@@ -150,6 +150,25 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
 _LORA_BN = {}
 
 
+class p8_tile_width:
+    """Context manager forcing the 8-phase GEMM's tile width (256 / 192 / 320 where legal; 0 = the library's
+    policy) for the GEMMs launched inside it (vst_p8_force_bn); tests and A/B runs only."""
+
+    def __init__(self, bn):
+        self.bn = int(bn)
+
+    def __enter__(self):
+        self.prev = int(_lib.load().vst_p8_force_bn(self.bn))
+        _LORA_BN.clear()
+        _XATTN_OK.clear()
+        return self
+
+    def __exit__(self, *a):
+        _lib.load().vst_p8_force_bn(self.prev)
+        _LORA_BN.clear()
+        _XATTN_OK.clear()
+
+
 def gemm_lora_tile(M, N, K, P, group_n, group_r):
     """Tile width (256 / 192) of the in-GEMM LoRA projection (vst_gemm_lora) for this shape, 0 = not supported
     (the caller then runs the down-projection as its own pass).  Host-side policy only; no launch."""
@@ -191,7 +210,8 @@ def linear_lora(x: torch.Tensor, w: torch.Tensor, a: torch.Tensor, group_n: int,
     # algorithmic work: base + up-projection (as the unfused "gemm_lora" counts it) + the down-projection once
     flops = 2.0 * M * N * (K + r) + 2.0 * M * K * r
     nbytes = 2.0 * (M * K + N * (K + r) + r * K + M * N * (2 if residual is not None else 1))
-    with _Rec("gemm_lora", flops, nbytes, lambda: f"gemm_p8<256x{bn},lora>", (M, N, K + P)):
+    sym = f"gemm_p8<128x{bn},lora>" if bn == 320 else f"gemm_p8<256x{bn},lora>"
+    with _Rec("gemm_lora", flops, nbytes, lambda: sym, (M, N, K + P)):
         _lib.call("vst_gemm_lora", _p(x), _ld(x), _p(a), _ld(a), P, group_n, group_r, _p(w), _ld(w), M, N, K,
                   _p(bias), _p(residual), 0 if residual is None else _ld(residual), _p(out), _ld(out), _stream())
     return out
