@@ -290,3 +290,52 @@ def test_frame_shard_sdxl_768_32_frames_cfg_pair_four_ranks_one_gpu():
     for rank, status, info in res:
         print(f"[shard] configs[3] CFG pair rank {rank}: {status} {info}")
         assert status == "ok", f"rank {rank}: {info}"
+
+
+def _gpu_worker_piecewise(rank, world, port, q):
+    """Piecewise capture of the frame-sharded denoise step (frame_shard.PiecewiseGraph: HIP graphs split at the
+    collectives, which run between the replays): 3 replayed steps == 3 eager steps, bit for bit."""
+    try:
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        _init(rank, world, port)
+        from test_parity_gpu import _setup
+        from video_style_transfer_amd.frame_shard import FrameShard, PiecewiseGraph
+        from video_style_transfer_amd.pipeline import AnimateDiffDenoiser
+        from video_style_transfer_amd.utils import build_unet
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        cfg, sd, lat, enc, pooled, tids = _setup("tiny", 8, 16, seed=6, B=2)
+        unet = build_unet(cfg, state_dict=sd, device=dev)
+        sh = FrameShard()
+        den = AnimateDiffDenoiser(unet, 8, 128, 128, num_inference_steps=10, device=dev, shard=sh, num_clips=1,
+                                  use_graph=False)
+        den.set_prompt_embeds(enc[1:2], pooled[1:2], enc[0:1], pooled[0:1])
+        lat0 = den.init_latents(seed=3)
+        eager = den.run_steps(3).clone()
+        den.set_latents(lat0)
+        den.use_graph = True
+        den.capture()
+        assert isinstance(den.graph, PiecewiseGraph) and den.graph.num_graphs > 1
+        den.set_latents(lat0)
+        graph = den.run_steps(3).clone()
+        same = torch.equal(eager, graph)
+        q.put((rank, "ok" if same else "fail", f"piecewise graph ({den.graph.num_graphs} graphs, "
+                                               f"{len(den.graph.items) - den.graph.num_graphs} collectives) == eager: "
+                                               f"{same}, max |diff| {(eager - graph).abs().max().item():.3e}"))
+    except BaseException:  # noqa: BLE001
+        import traceback
+        q.put((rank, "fail", traceback.format_exc()[-2000:]))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_frame_shard_piecewise_graph_two_ranks_one_gpu():
+    if torch.cuda.device_count() == 0:
+        pytest.skip("no HIP device")
+    res = _spawn(_gpu_worker_piecewise, 2)
+    for rank, status, info in res:
+        print(f"[shard] piecewise rank {rank}: {status} {info}")
+        assert status == "ok", f"rank {rank}: {info}"

@@ -34,16 +34,20 @@ def test_build_ops_groups_unziplora_projections(C):
 
 
 def test_lora_in_gemm_policy_at_sdxl_shapes():
-    """16x16 level (M = 8192 CFG-batched tokens): q/k/v, attn2 q and to_out all absorb the down-projection; 32x32
-    (M = 32768): to_out does, q/k/v does not (256-wide tiles straddle the q/k boundary at C = 640)."""
+    """Every SDXL projection absorbs the down-projection: 16x16 level (M = 8192 CFG-batched tokens) q/k/v, attn2 q and
+    to_out; 32x32 (M = 32768) to_out and q/k/v (on 128x320 tiles: 256-wide ones straddle the q/k boundary at C = 640).
+    The decision depends on the shape, not on M: a frame-sharded rank with 1/P of the rows takes the same path."""
+    from video_style_transfer_amd import kernels as K
     from video_style_transfer_amd.lora_linear import build_ops, lora_in_gemm
     a16, a32 = _attn(1280, cross=False), _attn(640, cross=False)
-    assert lora_in_gemm(build_ops([a16.to_q, a16.to_k, a16.to_v], 1.0), 8192)
-    assert lora_in_gemm(build_ops([a16.to_q], 1.0), 8192)
-    assert lora_in_gemm(build_ops([a16.to_out[0]], 1.0), 8192)
-    assert lora_in_gemm(build_ops([a32.to_out[0]], 1.0), 32768)
-    assert not lora_in_gemm(build_ops([a32.to_q, a32.to_k, a32.to_v], 1.0), 32768)
-    assert not lora_in_gemm(build_ops([a16.to_out[0]], 1.0), 512)  # too few tiles for the 8-phase kernel
+    for m in (8192, 1024, 512):
+        assert lora_in_gemm(build_ops([a16.to_q, a16.to_k, a16.to_v], 1.0), m)
+        assert lora_in_gemm(build_ops([a16.to_q], 1.0), m)
+        assert lora_in_gemm(build_ops([a16.to_out[0]], 1.0), m)
+    for m in (32768, 4096):
+        assert lora_in_gemm(build_ops([a32.to_out[0]], 1.0), m)
+        qkv = build_ops([a32.to_q, a32.to_k, a32.to_v], 1.0)
+        assert lora_in_gemm(qkv, m) and K.gemm_lora_tile(m, qkv.n, qkv.k1, qkv.a.shape[0], qkv.gn, qkv.gr) == 320
 
 
 def test_cross_attention_fusion_policy():
@@ -55,6 +59,7 @@ def test_cross_attention_fusion_policy():
         attn = _attn(C, cross=True)
         ops = build_ops([attn.to_q], 1.0)
         assert AP._cross_fusable(ops, 32 * Nq, Nq, 77)
+        assert AP._cross_fusable(ops, 4 * Nq, Nq, 77)  # shape-only: a frame shard fuses where the whole clip does
         assert not AP._cross_fusable(ops, 32 * 320, 320, 77)
     plain = AP.Attention(1280, 2048, 20, 64)
     assert AP._cross_fusable(build_ops([plain.to_q], 1.0), 8192, 256, 77)

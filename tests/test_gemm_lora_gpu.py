@@ -101,17 +101,21 @@ def test_gemm_lora_u_only(cuda, K):
 
 
 def test_gemm_lora_unsupported_falls_back(cuda, K):
-    """A tile that would need two u blocks (q/k boundary inside a 256-wide tile at C = 640) is refused (status 3)
-    and run_ops takes the two-pass path with the same result as the explicit two-pass call."""
+    """A shape where every tile width would put two u blocks in one tile (q/k/v of width 600: 192-, 256-wide tiles
+    straddle a projection boundary, and 600 is not a multiple of 320) is refused (status 3) and run_ops takes the
+    two-pass path with the same result as the explicit two-pass call.  The decision depends on the shape only, not on
+    M (a frame-sharded rank must take the unsharded forward's path)."""
     from video_style_transfer_amd import _lib
     from video_style_transfer_amd.lora_linear import ProjOps, lora_in_gemm, run_ops
     g = torch.Generator().manual_seed(9)
     M, Kd = 32768, 640
-    x, A, W = _operands(M, Kd, 3, 640, 16, 64, g, cuda)
-    assert K.gemm_lora_tile(M, 1920, Kd, 64, 640, 16) == 0
+    x, A, W = _operands(M, Kd, 3, 600, 16, 64, g, cuda)
+    for m in (M, 4096, 300):
+        assert K.gemm_lora_tile(m, 1800, Kd, 64, 600, 16) == 0
+    assert K.gemm_lora_tile(32768, 1920, Kd, 64, 640, 16) == K.gemm_lora_tile(2048, 1920, Kd, 64, 640, 16) == 320
     with pytest.raises(_lib.VstError):
-        K.linear_lora(x, W, A, 640, 16)
-    ops = ProjOps(W, A, None, Kd, 1920, 48, 640, 16)
+        K.linear_lora(x, W, A, 600, 16)
+    ops = ProjOps(W, A, None, Kd, 1800, 48, 600, 16)
     assert not lora_in_gemm(ops, M)
     out = run_ops(x, ops)
     u = K.linear(x, A, kind="gemm_lora_down")

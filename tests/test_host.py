@@ -42,16 +42,19 @@ def test_bad_arguments_rejected_without_gpu():
 
 def test_gemm_lora_policy_without_gpu():
     """vst_gemm_lora_supported (host policy, no launch): the SDXL UnZipLoRA r=8 projections run the down-projection
-    inside the 8-phase GEMM; a tile that straddles two u blocks, or a rank wider than one block, is refused."""
+    inside the 8-phase GEMM, whatever M is (the decision is shape-only, so a frame-sharded rank takes the unsharded
+    forward's path); a shape where every tile width straddles two u blocks, or a rank wider than one block, is
+    refused."""
     from video_style_transfer_amd import _lib
     lib = _lib.load()
     q = lib.vst_gemm_lora_supported
     assert q(8192, 1280, 1280, 32, 1280, 16) == 192   # to_out / attn2 q at 16x16
     assert q(8192, 3840, 1280, 64, 1280, 16) == 256   # attn1 q/k/v at 16x16
     assert q(32768, 640, 640, 32, 640, 16) == 192     # to_out at 32x32
-    assert q(32768, 1920, 640, 64, 640, 16) == 0      # q/k boundary inside a 256-wide tile
+    assert q(32768, 1920, 640, 64, 640, 16) == 320    # q/k boundary inside a 256-wide tile: 128x320 tiles
+    assert q(32768, 1800, 640, 64, 600, 16) == 0      # every width straddles (600 wide, not a multiple of 320)
     assert q(8192, 1280, 1280, 32, 1280, 32) == 0     # r = 16 UnZipLoRA: 32 u columns per projection
-    assert q(1024, 1280, 1280, 32, 1280, 16) == 0     # grid too small for the 8-phase kernel
+    assert q(1024, 1280, 1280, 32, 1280, 16) == 192   # small grids too (shape-only decision)
     # attn2 as one launch (q projection + text cross-attention epilogue): 256-row tiles inside a frame, <= 80 keys
     xq = lib.vst_gemm_cross_attention_supported
     assert xq(8192, 1280, 1280, 1, 32, 1280, 16, 256, 77) == 1    # 16x16 level, UnZipLoRA r=8
@@ -60,7 +63,7 @@ def test_gemm_lora_policy_without_gpu():
     assert xq(8192, 1280, 1280, 1, 32, 1280, 16, 320, 77) == 0    # tiles would straddle frames
     assert xq(8192, 1280, 1280, 1, 32, 1280, 16, 256, 81) == 0    # more keys than the LDS holds
     # a refused shape returns status 3 from the launch entry as well, before touching the pointers
-    assert lib.vst_gemm_lora(1, 1280, 1, 640, 64, 640, 16, 1, 704, 32768, 1920, 640, None, None, 0, 1, 1920,
+    assert lib.vst_gemm_lora(1, 1280, 1, 640, 64, 600, 16, 1, 704, 32768, 1800, 640, None, None, 0, 1, 1800,
                              None) == 3
 
 

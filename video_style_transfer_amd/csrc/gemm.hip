@@ -826,9 +826,12 @@ static bool lora_ingemm_env() {
 }
 
 // 0 = not supported (the host falls back to u = x.Acat^T + vst_gemm_ex), else the 8-phase tile width (256 / 192 /
-// 320).  Every tile's output columns must need u columns inside one 16-aligned block of 16.  When the policy's width
-// straddles two projections (the 32x32 q/k/v: C = 640 on 256-wide tiles) and 128x320 tiles are enabled, those are
-// taken: every SDXL projection width is a multiple of 320.
+// 320).  Every tile's output columns must need u columns inside one 16-aligned block of 16.  Whether the in-GEMM
+// path is taken depends on the SHAPE only (N, K, the projection groups), never on M: it runs whenever some tile width
+// keeps every tile inside one u block (the policy's width first, then 192, 256, 320 -- every SDXL width is a multiple
+// of 320, so the 32x32 q/k/v, which straddles q/k on 256-wide tiles, runs on 128x320 tiles).  So a frame-sharded rank
+// (fewer rows) takes the same path as the unsharded forward, and the two agree bit for bit: the tile width itself
+// does not change any output bit (same k order).
 static bool lora_tiles_ok(int N, int P, int gn, int gr, int bn) {
   for (int n0 = 0; n0 < N; n0 += bn) {
     const int g0 = n0 / gn, g1 = (std::min(n0 + bn, N) - 1) / gn;
@@ -842,10 +845,10 @@ static int lora_ingemm_bn(int M, int N, int K, int P, int gn, int gr, int force_
   if (!lora_ingemm_env() || M <= 0 || N <= 0 || K < 128 || (K & 7) || P <= 0 || (P & 15) || P > 256 || gn <= 0 ||
       gr <= 0 || N % gn || (N / gn) * gr > P)
     return 0;
-  if (!p8_auto(M, N, K, false)) return 0;
-  const int bn = force_bn ? force_bn : p8_bn(M, N, false);
-  if (lora_tiles_ok(N, P, gn, gr, bn)) return bn;
-  if (!force_bn && p8_320_on() && N % 320 == 0 && lora_tiles_ok(N, P, gn, gr, 320)) return 320;
+  if (force_bn) return lora_tiles_ok(N, P, gn, gr, force_bn) && (force_bn != 320 || N % 320 == 0) ? force_bn : 0;
+  const int cand[4] = {p8_bn(M, N, false), 192, 256, 320};
+  for (int bn : cand)
+    if ((bn != 320 || N % 320 == 0) && lora_tiles_ok(N, P, gn, gr, bn)) return bn;
   return 0;
 }
 
@@ -888,11 +891,11 @@ static bool xattn_env() {
   return v != 0;
 }
 
+// Shape-only decision (not M: a frame-sharded rank fuses exactly where the unsharded forward does).
 static bool xattn_ok(int M, int N, int K, const void* Acat, int P, int gn, int gr, int Nq, int Nk) {
   if (!xattn_env() || M <= 0 || N <= 0 || N % 64 || K < 128 || (K & 7) || Nq <= 0 || Nq % 256 || M % Nq || Nk < 1 ||
       Nk > 80)
     return false;
-  if (!p8_auto(M, N, K, false) || !p8_bn192(M, N, false)) return false;
   return !Acat || lora_ingemm_bn(M, N, K, P, gn, gr, 192) == 192;
 }
 

@@ -682,11 +682,13 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   VST_P8_STAMP(3)
 }
 
-// VST_P8_PH = 2 / 3: the k-loop schedule (A/B; see run_segment2)
+// The k-loop schedule: 2 (two 32-MFMA intervals per k-tile, run_segment2; default) or 3 (three intervals,
+// run_segment; VST_P8_PH=3).  Measured (tools/p8_ph_ab.py, profiles/r4_p8_ph_ab.txt): 2-5 % faster in isolation on
+// the step's GEMM shapes, -0.4 ms per denoise step in two alternations; outputs bit-identical.
 static int p8_ph_env() {
   static const int v = [] {
     const char* e = getenv("VST_P8_PH");
-    return e ? atoi(e) : 3;
+    return e ? atoi(e) : 2;
   }();
   return v;
 }

@@ -20,10 +20,11 @@ Per module and rank this moves 2 x (P-1)/P of the rank's activation over xGMI. T
 an all-gather of the clip before the attention (the north-star formulation), and no motion-module
 work is duplicated across ranks.
 
-The layout permutations around the all-to-all are one HIP kernel each (vst_permute_rows). With the
-nccl (= RCCL) backend the collectives run on the current stream and are captured in the step's HIP
-graph. The gloo backend (CPU transport; used by tests to run several ranks on one GPU or on CPU) stages
-through host memory and cannot be graph-captured.
+The layout permutations around the all-to-all are one HIP kernel each (vst_permute_rows).  A step is captured
+PIECEWISE (PiecewiseGraph): the kernels between two collectives form one HIP graph, and the collectives run between
+the graph replays on the same stream.  So no collective is ever inside a captured graph (RCCL's own graph capture is
+not relied on), and the gloo backend (CPU transport, host staging; used by tests to run several ranks on one GPU or on
+CPU) gets the same captured step as nccl (= RCCL).
 """
 from __future__ import annotations
 
@@ -37,6 +38,63 @@ from . import kernels as K
 Permute = Callable[[torch.Tensor, Sequence[int], Sequence[int]], torch.Tensor]
 
 
+class PiecewiseGraph:
+    """A HIP-graph capture split at the collectives: capture() runs `fn` once under capture; every collective that
+    FrameShard issues meanwhile closes the current graph, is recorded as a host call, and a new graph opens after it.
+    replay() replays graph, collective, graph, ... in capture order on the current stream.  All pieces share one
+    memory pool (replayed in capture order, as torch requires for pool sharing)."""
+
+    def __init__(self):
+        self.items = []
+        self.pool = None
+        self._g = None
+
+    def _begin(self):
+        self._g = torch.cuda.CUDAGraph()
+        # thread-local: the process group's watchdog thread may query events of earlier (eager) collectives
+        self._g.capture_begin(pool=self.pool, capture_error_mode="thread_local")
+
+    def _end(self):
+        self._g.capture_end()
+        if self.pool is None:
+            self.pool = self._g.pool()
+        self.items.append(self._g)
+        self._g = None
+
+    def collective(self, fn):
+        """Called by FrameShard in place of issuing a collective while capturing."""
+        self._end()
+        self.items.append(fn)
+        self._begin()
+
+    def capture(self, fn, shards, stream):
+        """Capture fn() on `stream` (a side stream, as torch capture requires) with `shards` in piecewise mode."""
+        for sh in shards:
+            sh._pw = self
+        try:
+            torch.cuda.synchronize()
+            with torch.cuda.stream(stream):
+                self._begin()
+                fn()
+                self._end()
+            torch.cuda.current_stream().wait_stream(stream)
+        finally:
+            for sh in shards:
+                sh._pw = None
+        return self
+
+    @property
+    def num_graphs(self):
+        return sum(1 for it in self.items if isinstance(it, torch.cuda.CUDAGraph))
+
+    def replay(self):
+        for it in self.items:
+            if isinstance(it, torch.cuda.CUDAGraph):
+                it.replay()
+            else:
+                it()
+
+
 class FrameShard:
     def __init__(self, group=None, permute: Optional[Permute] = None):
         if not dist.is_initialized():
@@ -46,10 +104,18 @@ class FrameShard:
         self.rank = dist.get_rank(group)
         self.backend = str(dist.get_backend(group)).lower()
         self._permute = permute or K.permute_rows
+        self._pw = None  # PiecewiseGraph while a step is being captured
 
     @property
     def graph_capturable(self) -> bool:
-        return self.backend == "nccl"
+        """Piecewise capture works on every backend (the collectives stay outside the graphs)."""
+        return True
+
+    def _issue(self, fn):
+        if self._pw is not None:
+            self._pw.collective(fn)
+        else:
+            fn()
 
     def local_frames(self, F: int):
         """(frames per rank, first global frame of this rank)."""
@@ -65,12 +131,15 @@ class FrameShard:
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.world == 1:
             return t
-        if self._staged(t):
-            h = t.cpu()
-            dist.all_reduce(h, group=self.group)
-            t.copy_(h)
-        else:
-            dist.all_reduce(t, group=self.group)
+
+        def op():
+            if self._staged(t):
+                h = t.cpu()
+                dist.all_reduce(h, group=self.group)
+                t.copy_(h)
+            else:
+                dist.all_reduce(t, group=self.group)
+        self._issue(op)
         return t
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
@@ -78,21 +147,28 @@ class FrameShard:
         out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
         if self.world == 1:
             out[0].copy_(t)
-        elif self.backend != "nccl":  # gloo: list all-gather through host memory
-            parts = [torch.empty(t.shape, dtype=t.dtype) for _ in range(self.world)]
-            dist.all_gather(parts, t.cpu().contiguous(), group=self.group)
-            out.copy_(torch.stack(parts))
-        else:
-            dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+            return out
+        src = t.contiguous()
+
+        def op():
+            if self.backend != "nccl":  # gloo: list all-gather through host memory
+                parts = [torch.empty(src.shape, dtype=src.dtype) for _ in range(self.world)]
+                dist.all_gather(parts, src.cpu(), group=self.group)
+                out.copy_(torch.stack(parts))
+            else:
+                dist.all_gather_into_tensor(out, src, group=self.group)
+        self._issue(op)
         return out
 
     def _all_to_all(self, out: torch.Tensor, inp: torch.Tensor):
-        if self._staged(inp):
-            ho = torch.empty(out.shape, dtype=out.dtype)
-            dist.all_to_all_single(ho, inp.cpu(), group=self.group)
-            out.copy_(ho)
-        else:
-            dist.all_to_all_single(out, inp, group=self.group)
+        def op():
+            if self._staged(inp):
+                ho = torch.empty(out.shape, dtype=out.dtype)
+                dist.all_to_all_single(ho, inp.cpu(), group=self.group)
+                out.copy_(ho)
+            else:
+                dist.all_to_all_single(out, inp, group=self.group)
+        self._issue(op)
 
     # ---- layout exchange ------------------------------------------------------------------
     def to_pixels(self, h: torch.Tensor, B: int, Fl: int, HW: int) -> torch.Tensor:

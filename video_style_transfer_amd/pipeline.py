@@ -92,7 +92,9 @@ class AnimateDiffDenoiser:
         K.step_advance(self.step_idx, self.num_steps)
 
     def capture(self):
-        """Warm up (fills every derived-weight cache), then capture one step into a HIP graph."""
+        """Warm up (fills every derived-weight cache), then capture one step into a HIP graph.  Frame-sharded over
+        several ranks: piecewise (frame_shard.PiecewiseGraph), the graphs split at the collectives, which run between
+        them."""
         saved = self.lat.clone()
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
@@ -100,10 +102,14 @@ class AnimateDiffDenoiser:
             self.step_idx.zero_()
             self._step()
         torch.cuda.current_stream(self.device).wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._step()
-        self.graph = g
+        if self.shard is not None and self.shard.world > 1:
+            from .frame_shard import PiecewiseGraph
+            self.graph = PiecewiseGraph().capture(self._step, [self.shard], s)
+        else:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._step()
+            self.graph = g
         self.lat.copy_(saved)
         self.step_idx.zero_()
 
@@ -127,8 +133,6 @@ class AnimateDiffDenoiser:
 
     def run_steps(self, n: Optional[int] = None):
         n = self.num_steps if n is None else n
-        if self.shard is not None and not self.shard.graph_capturable:
-            self.use_graph = False
         if self.use_graph and self.graph is None:
             self.capture()
         for _ in range(n):
