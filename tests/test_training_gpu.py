@@ -523,10 +523,19 @@ def test_unet_training_step_grads_vs_oracle(cuda, config):
           f"worst {yorder[-1]:.2e}")
     for k, v in sorted(kinds.items(), key=lambda kv: -kv[1]):
         print(f"[train] {config}   worst per kind {k:40s} {v:.2e}")
-    # every gradient within 5e-2 of fp32, or no further than 1.5x the reference's own bf16-autocast gradient is
-    bad = {n: (e, yerr[n]) for n, e in errs.items() if e >= max(5e-2, 1.5 * yerr[n])}
+    # Gates (round 4): the error DISTRIBUTION over all trainable tensors at the reference's own bf16-autocast one --
+    # median and 95th percentile within 1.25x of the autocast gradients' (or 3e-2 / 6e-2 absolute) -- and every
+    # tensor within 2x its autocast error (or 5e-2).  Why not round 3's per-tensor 1.5x: the yardstick is not
+    # reproducible (torch's bf16-autocast GEMMs on the GPU: its SDXL median measured 4.78e-2, 4.88e-2, 5.04e-2 and
+    # 5.54e-2 in four runs of this test on the same inputs), and an ulp-level change of the forward moves the HIP
+    # gradients' median by the same ~10 % (in-GEMM vs two-pass UnZipLoRA down-projection, numerically equivalent to
+    # 1e-3: 5.46e-2 vs 4.97e-2); per tensor, two such noisy estimates differ by more than 1.5x somewhere among 480
+    # (9.1e-2 vs 5.9e-2 on one tensor).  Recorded in DESIGN.md §5 and profiles/r4_train_grads_ab.txt.
+    bad = {n: (e, yerr[n]) for n, e in errs.items() if e >= max(5e-2, 2.0 * yerr[n])}
     assert not bad, bad
-    assert errs[order[len(order) // 2]] <= max(3e-2, 1.5 * yorder[len(yorder) // 2])
+    med, ymed = errs[order[len(order) // 2]], yorder[len(yorder) // 2]
+    p95, yp95 = errs[order[int(0.95 * (len(order) - 1))]], yorder[int(0.95 * (len(yorder) - 1))]
+    assert med <= max(3e-2, 1.25 * ymed) and p95 <= max(6e-2, 1.25 * yp95), (med, ymed, p95, yp95)
 
 
 @pytest.mark.parametrize("M,N,ld,c0", [(512, 512, 512, 0), (65536, 1280, 1280, 0), (1000, 64, 72, 0), (3, 8, 8, 0),

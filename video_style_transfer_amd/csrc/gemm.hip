@@ -954,8 +954,8 @@ extern "C" const char* vst_gemm_kernel_name(int M, int N, int K, int kind, int t
   if (tile == 9) return kind == 0 ? "gemm_p8<256x192>" : "";
   if (tile == 10) return kind == 0 ? "gemm_p8<128x320>" : "";
   if (tile == 0 && kind <= 1 && p8_auto(M, N, K, kind == 1)) {
-    if (splits == 0 && kind == 0 && p8_bn(M, N, false) == 320) return "gemm_p8<128x320>";
-    if (splits == 0 && kind == 0 && p8_bn192(M, N, false)) return "gemm_p8<256x192>";
+    if (splits <= 1 && kind == 0 && p8_bn(M, N, false) == 320) return "gemm_p8<128x320>";
+    if (splits <= 1 && kind == 0 && p8_bn192(M, N, false)) return "gemm_p8<256x192>";
     tile = 8;
   }
   choose(M, N, K, kind == 1, kind == 2, ws_bytes, tile, splits);
@@ -1003,7 +1003,9 @@ extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int
   if (tile == 0 && skinny_ok && M >= 1024) tile = 5;  // LoRA down-projection: skinny kernel
   if (tile == 5) return run_gemm(a, 0, 0, 5, 1, (hipStream_t)stream);
   const size_t slab_bytes = workspace ? ws_bytes : 0;
-  if (tile == 0 && splits == 0 && p8_auto(M, N, K, epilogue == 1) && p8_applies(M, N, K1, A2 != nullptr))
+  // splits 1 = no split-K (a row's bits then never depend on M: the denoise forward's row-invariant policy); the
+  // 8-phase kernel, which never splits, is chosen the same way under 0 and 1
+  if (tile == 0 && splits <= 1 && p8_auto(M, N, K, epilogue == 1) && p8_applies(M, N, K1, A2 != nullptr))
     tile = p8_bn(M, N, epilogue == 1) == 320 ? 10 : p8_bn192(M, N, epilogue == 1) ? 9 : 8;
   if (tile == 9 || tile == 10) {  // the 8-phase kernel at 256x192 / 128x320
     a.p8_bn = tile == 9 ? 192 : 320;

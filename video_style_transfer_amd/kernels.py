@@ -60,12 +60,33 @@ class _Rec:
 
 
 GEMM_POLICY = {"tile": 0, "splits": 0}  # 0 = library heuristic (tuning / tests may force)
+_ROW_INVARIANT = [0]
+
+
+class row_invariant:
+    """Inside: GEMMs and convs run without split-K (splits = 1 unless GEMM_POLICY forces a count), so every output
+    row's bits depend on that row's inputs only, never on how many rows the launch has.  The denoise forward runs
+    under it (UNetMotionModel.forward_tokens): a frame-sharded rank then computes exactly the unsharded forward's
+    bits for its frames.  (Split-K only ever applied to grids under half a wave of tiles; the forward's token GEMMs
+    at the step's shapes never split anyway.)"""
+
+    def __enter__(self):
+        _ROW_INVARIANT[0] += 1
+        return self
+
+    def __exit__(self, *a):
+        _ROW_INVARIANT[0] -= 1
+
+
+def _splits():
+    s = GEMM_POLICY["splits"]
+    return s if s or not _ROW_INVARIANT[0] else 1
 
 
 def gemm_kernel_name(M, N, K, kind):
     """Kernel the library launches for a GEMM / conv of this size (kind: 0 linear, 1 GEGLU, 2 conv,
     3 scalar-gather conv) under the current GEMM_POLICY."""
-    name = _lib.load().vst_gemm_kernel_name(M, N, K, kind, GEMM_POLICY["tile"], GEMM_POLICY["splits"], _WS_BYTES)
+    name = _lib.load().vst_gemm_kernel_name(M, N, K, kind, GEMM_POLICY["tile"], _splits(), _WS_BYTES)
     return name.decode() if name else None
 _WS = {}
 _WS_BYTES = 80 << 20  # fp32 split-K slabs
@@ -143,7 +164,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
         _lib.call("vst_gemm_ex", _p(x), _ld(x), _p(x2), 0 if x2 is None else _ld(x2), K1, _p(w), _ld(w), M, N, K,
                   _p(bias), _p(row_bias), row_bias_div, N if row_bias is not None else 0, _p(residual),
                   0 if residual is None else _ld(residual), _p(out), _ld(out), 1 if geglu else (2 if act else 0),
-                  GEMM_POLICY["tile"], GEMM_POLICY["splits"], _p(ws), _WS_BYTES, _stream())
+                  GEMM_POLICY["tile"], _splits(), _p(ws), _WS_BYTES, _stream())
     return out
 
 
@@ -317,7 +338,7 @@ def conv3x3(x1: torch.Tensor, nimg: int, H: int, W: int, w: torch.Tensor, bias: 
         ws = _workspace(x1.device)
         _lib.call("vst_conv3x3_ex", _p(x1), C1, _p(x2), C2, nimg, H, W, stride, 1 if upsample else 0, _p(w), Cout,
                   _p(bias), _p(row_bias), row_bias_div, 0 if row_bias is None else _ld(row_bias), _p(residual), 0 if residual is None else _ld(residual),
-                  _p(out), _ld(out) if Cout >= 8 else Cout, GEMM_POLICY["tile"], GEMM_POLICY["splits"], _p(ws),
+                  _p(out), _ld(out) if Cout >= 8 else Cout, GEMM_POLICY["tile"], _splits(), _p(ws),
                   _WS_BYTES, _stream())
     return out
 

@@ -529,19 +529,20 @@ class UNetMotionModel(nn.Module):
     def forward_tokens(self, x, B, F, h, w, emb_silu, enc, cross_kwargs=None, shard=None):
         """x: [B*F*h*w, in_channels] bf16 -> noise prediction [B*F*h*w, out_channels] bf16.
         With `shard` (frame_shard.FrameShard), F is this rank's frames of each clip."""
-        ctx = FwdCtx(B, F, emb_silu, enc, cross_kwargs or {}, shard, self.batched_temb(emb_silu))
-        nimg = B * F
-        H, W = h, w
-        x = self.conv_in.run(x, nimg, H, W)
-        skips = [(x, H, W)]
-        for blk in self.down_blocks:
-            x, H, W, outs = blk.run(x, nimg, H, W, ctx)
-            skips.extend(outs)
-        x = self.mid_block.run(x, nimg, H, W, ctx)
-        for blk in self.up_blocks:
-            x, H, W = blk.run(x, nimg, H, W, ctx, skips)
-        x = self.conv_norm_out.run(x, nimg, H * W, silu=True)
-        return self.conv_out.run(x, nimg, H, W)
+        with K.row_invariant():  # no split-K: a row's bits do not depend on the launch's row count (frame shards)
+            ctx = FwdCtx(B, F, emb_silu, enc, cross_kwargs or {}, shard, self.batched_temb(emb_silu))
+            nimg = B * F
+            H, W = h, w
+            x = self.conv_in.run(x, nimg, H, W)
+            skips = [(x, H, W)]
+            for blk in self.down_blocks:
+                x, H, W, outs = blk.run(x, nimg, H, W, ctx)
+                skips.extend(outs)
+            x = self.mid_block.run(x, nimg, H, W, ctx)
+            for blk in self.up_blocks:
+                x, H, W = blk.run(x, nimg, H, W, ctx, skips)
+            x = self.conv_norm_out.run(x, nimg, H * W, silu=True)
+            return self.conv_out.run(x, nimg, H, W)
 
     def forward(self, sample, timestep, encoder_hidden_states, timestep_cond=None, attention_mask=None,
                 cross_attention_kwargs=None, added_cond_kwargs=None, return_dict=True, frame_shard=None, **kwargs):
