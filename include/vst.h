@@ -60,6 +60,9 @@ int vst_gemm_lora_supported(int M, int N, int K, int P, int group_n, int group_r
 /* Test / A-B knob: force the 8-phase kernel's tile width (256, 192 or 320 where legal; 0 = automatic policy) for
  * every later GEMM of this process; returns the previous setting.  Not on the product path. */
 int vst_p8_force_bn(int bn);
+/* Test / A-B knob: 3x3 convs whose channel sources are multiples of 64 run on the 8-phase kernel (1) or the ring
+ * kernel (0) for every later conv of this process (default: VST_P8_CONV, else 0); returns the previous setting. */
+int vst_p8_conv(int on);
 
 /* attn2 of a BasicTransformerBlock as ONE launch: the q projection (vst_gemm_lora when Acat != NULL, else
  * [x].[W]^T) with the cross-attention over the text tokens as its epilogue,

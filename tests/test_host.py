@@ -184,7 +184,9 @@ def test_gemm_kernel_policy_host_only():
     assert name(2, 13760, 1280, 0) == "gemm_rows"               # batched time_emb_proj of every resnet
     assert name(9, 1280, 1280, 0).endswith("splitk>")           # M > 8: split-K tiles
     assert name(131072, 320, 2880, 2).endswith("conv>")
-    assert name(131072, 4, 2880, 2) == "gemm_ring<128x64,conv>"  # conv_out
+    assert name(131072, 4, 2880, 2) == "gemm_ring<128x64,conv>"  # conv_out: Cout not a multiple of 64
+    assert name(8192, 1280, 11520, 2) == "gemm_p8<128x320,conv>"  # 16^2 resnet conv: implicit im2col, 8-phase
+    assert name(32768, 640, 5760, 2) == "gemm_p8<128x320,conv>"
 
 
 def test_text_encoder_surface_cpu():

@@ -294,6 +294,38 @@ def test_conv3x3(cuda, K, n, Ci, Co, H, W, stride, up):
     check(out, to_nhwc(ref), name="conv")
 
 
+@pytest.mark.parametrize("n,C1,C2,Co,H,W,stride,up", [
+    (8, 320, 0, 320, 64, 64, 1, False),     # 64x64 level, Cout 320: 128x320 tiles
+    (16, 640, 320, 640, 32, 32, 1, False),  # up path: skip concat, Cout 640
+    (16, 320, 0, 640, 64, 64, 2, False),    # downsample (stride 2)
+    (16, 640, 0, 640, 16, 16, 1, True),     # upsample (nearest 2x)
+    (32, 1280, 0, 1280, 16, 16, 1, False),  # 16x16 level, Cout 1280: 256-row tiles
+])
+def test_conv3x3_8phase_bitwise_equals_ring(cuda, K, n, C1, C2, Co, H, W, stride, up):
+    """3x3 convs on the 8-phase kernel (vst_p8_conv: implicit im2col into its A slots, a (tap, channel) cursor per slot)
+    against the ring kernel's conv bit for bit (same k order), and against fp32 torch; temb row bias and residual."""
+    g = torch.Generator().manual_seed(n + C1 + Co + stride)
+    x1 = rnd(n, C1, H, W, gen=g)
+    x2 = rnd(n, C2, H, W, gen=g) if C2 else None
+    Ci = C1 + C2
+    w = rnd(Co, Ci, 3, 3, scale=(9 * Ci) ** -0.5, gen=g)
+    b = torch.randn(Co, generator=g) * 0.1
+    OH, OW = (2 * H, 2 * W) if up else ((H + 1) // 2, (W + 1) // 2) if stride == 2 else (H, W)
+    temb = torch.randn(n, Co, generator=g)
+    r = rnd(n, Co, OH, OW, gen=g)
+    args = (to_nhwc(x1).to(cuda), n, H, W, wflat(w).to(cuda), b.to(cuda))
+    kw = dict(x2=None if x2 is None else to_nhwc(x2).to(cuda), stride=stride, upsample=up, row_bias=temb.to(cuda),
+              row_bias_div=OH * OW, residual=to_nhwc(r).to(cuda))
+    ring = K.conv3x3(*args, **kw)
+    with K.p8_conv(True):
+        assert "gemm_p8" in K.gemm_kernel_name(n * OH * OW, Co, 9 * Ci, 2)
+        p8 = K.conv3x3(*args, **kw)
+    assert torch.equal(p8, ring)
+    xx = x1.float() if x2 is None else torch.cat([x1, x2], 1).float()
+    ref = conv_ref(xx, w.float(), b, stride, up).to(torch.bfloat16).float() + temb[:, :, None, None] + r.float()
+    check(p8, to_nhwc(ref), name="conv p8")
+
+
 @pytest.mark.parametrize("M,N,Kd", [(2, 1280, 320), (2, 1280, 2816), (2, 13760, 1280), (1, 8, 8), (3, 104, 40),
                                     (5, 640, 1288), (8, 336, 4096)])
 @pytest.mark.parametrize("epi", ["bias", "residual", "gelu", "rowbias"])

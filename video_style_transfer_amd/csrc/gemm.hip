@@ -636,6 +636,7 @@ int launch_gemm_ring(const GemmArgs& a, int amode, int epi, int tile, int splits
 int launch_gemm_p8(const GemmArgs& a, int epi, int bn, hipStream_t s);
 int launch_gemm_p8_lora(const GemmArgs& a, int bn, hipStream_t s);
 int launch_gemm_p8_xattn(const GemmArgs& a, hipStream_t s);
+int launch_gemm_p8_conv(const GemmArgs& a, int bn, hipStream_t s);
 
 // 8-phase 256x256x64 kernel (gemm_p8.hip) for plain / LoRA-augmented projections and GEGLU (see p8_auto).
 static int gemm_p8_env() {
@@ -710,6 +711,15 @@ static bool p8_bn320(int M, int N, bool geglu) {
   return 0.7 * r320 < 0.97 * best;
 }
 
+static int g_p8_conv = -1;  // VST_P8_CONV, or vst_p8_conv (tests, A/B)
+static bool p8_conv_env() {
+  if (g_p8_conv < 0) {
+    const char* e = getenv("VST_P8_CONV");
+    g_p8_conv = e ? atoi(e) : 1;
+  }
+  return g_p8_conv != 0;
+}
+
 static int p8_bn(int M, int N, bool geglu) {
   return p8_bn320(M, N, geglu) ? 320 : p8_bn192(M, N, geglu) ? 192 : 256;
 }
@@ -721,6 +731,14 @@ static int p8_bn(int M, int N, bool geglu) {
 extern "C" int vst_p8_force_bn(int bn) {
   const int prev = vst::p8_forced_bn();
   vst::g_p8_force_bn = (bn == 256 || bn == 192 || bn == 320) ? bn : 0;
+  return prev;
+}
+
+// Route 3x3 convs with 64-multiple channel sources to the 8-phase kernel (1) or the ring kernel (0) for every later
+// conv of this process; returns the previous setting.  For tests and A/B runs.
+extern "C" int vst_p8_conv(int on) {
+  const int prev = vst::p8_conv_env() ? 1 : 0;
+  vst::g_p8_conv = on ? 1 : 0;
   return prev;
 }
 
@@ -948,6 +966,10 @@ extern "C" const char* vst_gemm_kernel_name(int M, int N, int K, int kind, int t
                                        "gemm_ring<256x256,splitk>", "gemm_ring<256x128,splitk>", "",
                                        "gemm_ring<256x160,splitk>", "gemm_ring<192x256,splitk>"};
   if (kind == 3) return "gemm_kernel<conv_in>";
+  if (kind == 2 && tile == 0 && splits <= 1 && p8_conv_env() && K % 576 == 0 && N % 64 == 0 &&
+      p8_auto(M, N, K, false))
+    return N % 320 == 0 ? "gemm_p8<128x320,conv>" : p8_bn(M, N, false) == 192 ? "gemm_p8<256x192,conv>"
+                                                                                 : "gemm_p8<256x256,conv>";
   if (kind == 0 && tile == 0 && rows_applies(M, N, K)) return "gemm_rows";
   if (kind == 0 && (tile == 5 || (tile == 0 && N <= 64 && M >= 1024))) return "gemm_skinny";  // no-epilogue calls
   if (kind < 0 || kind > 3 || tile < 0 || tile > 10 || tile == 5 || splits < 0) return "";
@@ -1058,6 +1080,15 @@ static int conv3x3_impl(const void* x1, int C1, const void* x2, int C2, int nimg
   a.r_bytes = R ? clamp_bytes(((size_t)(a.M - 1) * ldr + Cout) * 2) : 0;
   if ((ldc & 7) && Cout >= 8) return VST_ERR_ARG;
   if (!vec) { tile = 2; splits = 1; }
+  // 3x3 convs with both sources a multiple of 64 channels run on the 8-phase kernel (implicit im2col; 128x320 tiles
+  // where Cout is a multiple of 320, else the projection policy's width); VST_P8_CONV=0 restores the ring kernel
+  if (vec && tile == 0 && splits <= 1 && p8_conv_env() && !(C1 & 63) && !((x2 ? C2 : 0) & 63) && !(a.N & 63) &&
+      p8_auto(a.M, a.N, a.K, false)) {
+    a.splits = 1;
+    a.ablate = 0;
+    a.group_m = gemm_group_env();
+    return launch_gemm_p8_conv(a, a.N % 320 == 0 ? 320 : p8_bn(a.M, a.N, false), (hipStream_t)stream);
+  }
   const size_t slab_bytes = workspace ? ws_bytes : 0;
   choose(a.M, a.N, a.K, 0, 1, slab_bytes, tile, splits);
   return run_gemm(a, vec ? 1 : 2, 0, tile, splits, (hipStream_t)stream);

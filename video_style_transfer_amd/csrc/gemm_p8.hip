@@ -298,10 +298,16 @@ __device__ __forceinline__ void xattn_epilogue(const GemmArgs& p, char* smem, co
 // loop u is rounded to bf16 (the reference's rounding point of lora_layer's down output), exchanged through LDS and
 // multiplied by the tile's up-projection columns of W (K + ub0 ...) as one extra 16x16x32 step per accumulator —
 // the same operands, in the same order, as the [x | u] . [W | V]^T k-tile it replaces.
-template <int EPI, int BN, bool LORA = false, int PH = 3, int BM = 256>
+// CONV: the A operand is the implicit im2col of an NHWC 3x3 conv (pad 1; stride 2, nearest-2x upsample, the VAE's
+// (0,1,0,1) padding; x2 = the up path's skip concat), K ordered (tap, channel) with Ctot = C1 + C2 a multiple of 64,
+// so a 64-deep k-tile is one tap of one source.  Each A slot's DMAs are issued for consecutive k-tiles, so a (tap,
+// channel) cursor per slot advances by 64 per issue and its pieces' row bases are recomputed only when the tap or the
+// source changes (padding rows read out of range: zeros).  Same k order as the ring kernel's conv: same bits.
+template <int EPI, int BN, bool LORA = false, int PH = 3, int BM = 256, bool CONV = false>
 __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using Cfg = P8Cfg<BN, BM>;
+  static_assert(!CONV || (!LORA && EPI == 0), "conv: plain epilogue");
   static_assert(EPI != 1 || BN == 256, "GEGLU needs 64-column [hidden | gate] blocks");
   static_assert(!LORA || EPI != 1, "in-GEMM LoRA: linear epilogue");
   static_assert(EPI != 4 || (BN == 192 && BM == 256), "cross-attention epilogue: 256 x 192 tiles (3 heads)");
@@ -342,6 +348,11 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   const int PB = wid;
   uint32_t base1[4][NPC], base2[2][NPC];
   int c8[4][NPC];
+  // CONV: output pixel (image, oy, ox) of each A piece's row; per-slot (tap, channel) cursor and source
+  int cv_img[2][NPA], cv_oy[2][NPA], cv_ox[2][NPA];
+  int cv_tap[2] = {0, 0}, cv_ci[2] = {0, 0}, cv_ci0[2] = {0, 0};
+  bool cv_second[2] = {false, false}, cv_rebase[2] = {true, true};
+  const int Ctot = p.C1 + p.C2;
   const auto rl = make_rsrc(LORA ? p.la : p.Wt, LORA ? p.la_bytes : 0u);
   int ub0 = 0, lc8 = 0;          // LORA: the tile's first u column (16-aligned); this lane's Acat chunk * 8
   uint32_t lbase = (uint32_t)kOOB;  // LORA: this lane's Acat source row / chunk (waves 0-1)
@@ -364,8 +375,19 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
         c8[s][pc] = c * 8;
         if (s < 2) {
           const int m = m0 + (r / HALF) * Cfg::WM + s * HALF + (r % HALF);
-          base1[s][pc] = m < p.M ? (uint32_t)(m * p.lda1 + c * 8) * 2u : (uint32_t)kOOB;
-          base2[s][pc] = m < p.M ? (uint32_t)(m * p.lda2 + c * 8) * 2u : (uint32_t)kOOB;
+          if constexpr (CONV) {
+            if (pc < NPA) {
+              const int hw = p.OH * p.OW;
+              const int img = m / hw, rem = m - img * hw;
+              cv_img[s][pc] = m < p.M ? img : -1;
+              cv_oy[s][pc] = rem / p.OW;
+              cv_ox[s][pc] = rem - cv_oy[s][pc] * p.OW;
+            }
+            base1[s][pc] = base2[s][pc] = (uint32_t)kOOB;
+          } else {
+            base1[s][pc] = m < p.M ? (uint32_t)(m * p.lda1 + c * 8) * 2u : (uint32_t)kOOB;
+            base2[s][pc] = m < p.M ? (uint32_t)(m * p.lda2 + c * 8) * 2u : (uint32_t)kOOB;
+          }
         } else {
           const int rb = s == 2 ? 32 : RB1;
           const int n = n0 + (r / rb) * Cfg::WN + (s - 2) * 32 + (r % rb);
@@ -373,13 +395,47 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
         }
       }
   };
+  // CONV: A slot s's pieces for its next k-tile (the slot's cursor); live = false issues zeros (counts stay uniform)
+  auto conv_rebase = [&](int s) {
+    const int ky = cv_tap[s] / 3, kx = cv_tap[s] - 3 * (cv_tap[s] / 3);
+    cv_second[s] = cv_ci[s] >= p.C1;
+    const int cs = cv_second[s] ? p.C2 : p.C1;
+    cv_ci0[s] = cv_second[s] ? p.C1 : 0;
+#pragma unroll
+    for (int pc = 0; pc < NPA; ++pc) {
+      int iy, ix;
+      bool ok = cv_img[s][pc] >= 0;
+      if (p.up) {
+        const int uy = cv_oy[s][pc] + ky - 1, ux = cv_ox[s][pc] + kx - 1;
+        ok = ok && uy >= 0 && uy < 2 * p.H && ux >= 0 && ux < 2 * p.W;
+        iy = uy >> 1; ix = ux >> 1;
+      } else {
+        iy = cv_oy[s][pc] * p.stride + ky - 1 + p.pad0; ix = cv_ox[s][pc] * p.stride + kx - 1 + p.pad0;
+        ok = ok && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+      }
+      base1[s][pc] = ok ? (uint32_t)(((cv_img[s][pc] * p.H + iy) * p.W + ix) * cs + c8[s][pc]) * 2u : (uint32_t)kOOB;
+    }
+    cv_rebase[s] = false;
+  };
+  auto conv_dma = [&](int s, bool live, char* dst) {
+    if (cv_rebase[s]) conv_rebase(s);
+    const uint32_t kc = (uint32_t)(cv_ci[s] - cv_ci0[s]) * 2u;
+#pragma unroll
+    for (int pc = 0; pc < NPA; ++pc)
+      p8_dma16(cv_second[s] ? ra2 : ra1, dst + pc * PS * 1024, live ? (int)(base1[s][pc] + kc) : kOOB);
+    cv_ci[s] += 64;
+    if (cv_ci[s] == Ctot) { cv_ci[s] = 0; ++cv_tap[s]; }
+    cv_rebase[s] = cv_ci[s] == 0 || (p.C2 > 0 && cv_ci[s] == p.C1);
+  };
   // slot s of k-tile kt into buffer (kt & 1); kt >= kend: out-of-range offsets (zeros), keeps vmcnt counts uniform
   auto dma_slot = [&](int s, int kt, int kend) {
     if ((abl & 1) && kt > 1) return;
     char* dst = smem + (kt & 1) * BUF + slot_off(s) + PB * 1024;
     const int k0 = kt * 64;
     const bool live = kt < kend && !((abl & 32) && kt > 1);
-    if (s < 2) {
+    if (CONV && s < 2) {
+      conv_dma(s, live, dst);
+    } else if (s < 2) {
       const bool second = k0 >= p.K1;
       const uint32_t kb = (uint32_t)(second ? k0 - p.K1 : k0) * 2u;
 #pragma unroll
@@ -403,7 +459,9 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     if ((abl & 1) && kt > 1) return;
     char* dst = smem + (kt & 1) * BUF + slot_off(s) + PB * 1024;
     const int k0 = kt * 64;
-    if (s < 2) {
+    if (CONV && s < 2) {
+      conv_dma(s, true, dst);
+    } else if (s < 2) {
       const bool second = k0 >= p.K1;
       const uint32_t kb = (uint32_t)(second ? k0 - p.K1 : k0) * 2u;
 #pragma unroll
@@ -693,18 +751,18 @@ static int p8_ph_env() {
   return v;
 }
 
-template <int EPI, int BN, bool LORA, int PH, int BM>
+template <int EPI, int BN, bool LORA, int PH, int BM, bool CONV = false>
 static int launch_p8_ph(const GemmArgs& a, hipStream_t s) {
   static bool attr = false;
   using Cfg = P8Cfg<BN, BM>;
   constexpr int lds = EPI == 4 ? 160 * 1024 : (LORA ? Cfg::LDS_LORA : Cfg::LDS);
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_p8_kernel<EPI, BN, LORA, PH, BM>,
+    (void)hipFuncSetAttribute((const void*)gemm_p8_kernel<EPI, BN, LORA, PH, BM, CONV>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
   const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_p8_kernel<EPI, BN, LORA, PH, BM>), dim3(nwg), dim3(512), lds, s, a);
+  hipLaunchKernelGGL((gemm_p8_kernel<EPI, BN, LORA, PH, BM, CONV>), dim3(nwg), dim3(512), lds, s, a);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 
@@ -726,6 +784,18 @@ int launch_gemm_p8_lora(const GemmArgs& a, int bn, hipStream_t s) {
 int launch_gemm_p8_xattn(const GemmArgs& a, hipStream_t s) {
   if (!a.xa_k || !a.xa_v) return VST_ERR_ARG;
   return a.la ? launch_p8_epi<4, 192, true>(a, s) : launch_p8_epi<4, 192, false>(a, s);
+}
+
+// implicit-GEMM 3x3 conv (GemmArgs conv geometry, Ctot % 64 == 0), epilogue 0; bn: 256, 192 or 320
+int launch_gemm_p8_conv(const GemmArgs& a, int bn, hipStream_t s) {
+  if ((a.C1 & 63) || (a.C2 & 63) || a.K != 9 * (a.C1 + a.C2)) return VST_ERR_ARG;
+  const bool ph2 = p8_ph_env() == 2;
+  switch (bn) {
+    case 256: return ph2 ? launch_p8_ph<0, 256, false, 2, 256, true>(a, s) : launch_p8_ph<0, 256, false, 3, 256, true>(a, s);
+    case 192: return ph2 ? launch_p8_ph<0, 192, false, 2, 256, true>(a, s) : launch_p8_ph<0, 192, false, 3, 256, true>(a, s);
+    case 320: return ph2 ? launch_p8_ph<0, 320, false, 2, 128, true>(a, s) : launch_p8_ph<0, 320, false, 3, 128, true>(a, s);
+    default: return VST_ERR_ARG;
+  }
 }
 
 // epi: 0 bias / row bias / residual, 1 GEGLU, 3 bias + GELU; bn: 256, 192 or 320 (128-row tiles; not with GEGLU)

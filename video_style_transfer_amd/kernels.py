@@ -171,6 +171,21 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
 _LORA_BN = {}
 
 
+class p8_conv:
+    """Context manager routing 3x3 convs to the 8-phase kernel (on=True) or the ring kernel (vst_p8_conv); tests and
+    A/B runs only."""
+
+    def __init__(self, on=True):
+        self.on = int(bool(on))
+
+    def __enter__(self):
+        self.prev = int(_lib.load().vst_p8_conv(self.on))
+        return self
+
+    def __exit__(self, *a):
+        _lib.load().vst_p8_conv(self.prev)
+
+
 class p8_tile_width:
     """Context manager forcing the 8-phase GEMM's tile width (256 / 192 / 320 where legal; 0 = the library's
     policy) for the GEMMs launched inside it (vst_p8_force_bn); tests and A/B runs only."""
