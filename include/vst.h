@@ -61,8 +61,12 @@ int vst_gemm_lora_supported(int M, int N, int K, int P, int group_n, int group_r
  * every later GEMM of this process; returns the previous setting.  Not on the product path. */
 int vst_p8_force_bn(int bn);
 /* Test / A-B knob: 3x3 convs whose channel sources are multiples of 64 run on the 8-phase kernel (1) or the ring
- * kernel (0) for every later conv of this process (default: VST_P8_CONV, else 0); returns the previous setting. */
+ * kernel (0) for every later conv of this process (default: VST_P8_CONV, else 1); returns the previous setting. */
 int vst_p8_conv(int on);
+/* Test / A-B knob: the 8-phase kernel's persistent grid (one workgroup per CU walking the tiles, each tile's last
+ * k-tiles streaming the next tile's first ones) for GEMMs of two or more tile rounds (1) or one workgroup per tile
+ * (0), for every later GEMM of this process (default: VST_P8_PERSIST); returns the previous setting.  Same bits. */
+int vst_p8_persist(int on);
 
 /* attn2 of a BasicTransformerBlock as ONE launch: the q projection (vst_gemm_lora when Acat != NULL, else
  * [x].[W]^T) with the cross-attention over the text tokens as its epilogue,

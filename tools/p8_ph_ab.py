@@ -2,7 +2,8 @@
 denoise step's GEMM shapes, in isolation: each schedule runs in its own child process (the choice is read once per
 process), alternated `passes` times; the children also hash their outputs, which must be equal (same k order).
 python tools/p8_ph_ab.py [passes] [variant ...]  -> one JSON line per shape with us per launch and TF/s per variant.
-A variant is the schedule, optionally '+320' for the 128x320 tile policy (VST_P8_320=1): e.g. 3 2 3+320 2+320."""
+A variant is the schedule, optionally '+320' for the 128x320 tile policy (VST_P8_320=1) and '+persist' for the persistent
+grid (VST_P8_PERSIST=1): e.g. 3 2 3+320 2+320 2+persist."""
 import hashlib
 import json
 import os
@@ -17,6 +18,7 @@ SHAPES = [  # name, kind, M, N, K (16x512^2 CFG pair: 16^2 level M = 8192, 32^2 
     ("ff2_1280", "plain", 8192, 1280, 5120), ("ff2_640", "plain", 32768, 640, 2560), ("proj320", "plain", 131072, 320, 320),
     ("out1280_lora", "lora1", 8192, 1280, 1280), ("qkv1280_lora", "lora3", 8192, 3840, 1280),
     ("out640_lora", "lora1", 32768, 640, 640), ("qkv640_lora", "lora3", 32768, 1920, 640),
+    ("qkv960_320", "plain", 131072, 960, 320), ("ff2_320", "plain", 131072, 320, 1280),
 ]
 
 
@@ -82,7 +84,8 @@ def main():
     res = {}
     for _ in range(passes):
         for ph in phs:
-            env = dict(os.environ, VST_P8_PH=ph.split("+")[0], VST_PH_CHILD="1", VST_P8_320="1" if "+320" in ph else "0")
+            env = dict(os.environ, VST_P8_PH=ph.split("+")[0], VST_PH_CHILD="1", VST_P8_320="1" if "+320" in ph else "0",
+                       VST_P8_PERSIST="1" if "+persist" in ph else "0")
             r = subprocess.run([sys.executable, os.path.abspath(__file__)], env=env, capture_output=True, text=True,
                                timeout=300)
             if r.returncode:

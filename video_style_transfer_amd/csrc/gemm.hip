@@ -634,6 +634,7 @@ static void choose(int M, int N, int K, int geglu, int conv, size_t ws_bytes, in
 
 int launch_gemm_ring(const GemmArgs& a, int amode, int epi, int tile, int splits, hipStream_t s);
 int launch_gemm_p8(const GemmArgs& a, int epi, int bn, hipStream_t s);
+bool p8_persist_applies(int M, int N, int K, int epi, int bn);
 int launch_gemm_p8_lora(const GemmArgs& a, int bn, hipStream_t s);
 int launch_gemm_p8_xattn(const GemmArgs& a, hipStream_t s);
 int launch_gemm_p8_conv(const GemmArgs& a, int bn, hipStream_t s);
@@ -967,21 +968,31 @@ extern "C" const char* vst_gemm_kernel_name(int M, int N, int K, int kind, int t
                                        "gemm_ring<256x160,splitk>", "gemm_ring<192x256,splitk>"};
   if (kind == 3) return "gemm_kernel<conv_in>";
   if (kind == 2 && tile == 0 && splits <= 1 && p8_conv_env() && K % 576 == 0 && N % 64 == 0 &&
-      p8_auto(M, N, K, false))
-    return N % 320 == 0 ? "gemm_p8<128x320,conv>" : p8_bn(M, N, false) == 192 ? "gemm_p8<256x192,conv>"
-                                                                                 : "gemm_p8<256x256,conv>";
+      p8_auto(M, N, K, false)) {
+    const int bn = N % 320 == 0 ? 320 : p8_bn(M, N, false) == 192 ? 192 : 256;
+    if (bn == 320) return p8_persist_applies(M, N, K, 0, bn) ? "gemm_p8<128x320,conv,persist>" : "gemm_p8<128x320,conv>";
+    return bn == 192 ? "gemm_p8<256x192,conv>" : "gemm_p8<256x256,conv>";
+  }
   if (kind == 0 && tile == 0 && rows_applies(M, N, K)) return "gemm_rows";
   if (kind == 0 && (tile == 5 || (tile == 0 && N <= 64 && M >= 1024))) return "gemm_skinny";  // no-epilogue calls
   if (kind < 0 || kind > 3 || tile < 0 || tile > 10 || tile == 5 || splits < 0) return "";
-  if (tile == 9) return kind == 0 ? "gemm_p8<256x192>" : "";
-  if (tile == 10) return kind == 0 ? "gemm_p8<128x320>" : "";
+  // the 8-phase kernel, persistent where p8_persist_applies (kind 0 is reported with its plain epilogue)
+  auto p8name = [&](int bn, bool geglu) -> const char* {
+    const bool pe = p8_persist_applies(M, N, K, geglu ? 1 : 0, bn);
+    if (bn == 320) return pe ? "gemm_p8<128x320,persist>" : "gemm_p8<128x320>";
+    if (bn == 192) return pe ? "gemm_p8<256x192,persist>" : "gemm_p8<256x192>";
+    if (geglu) return pe ? "gemm_p8<256x256,geglu,persist>" : "gemm_p8<256x256,geglu>";
+    return pe ? "gemm_p8<256x256,persist>" : "gemm_p8<256x256>";
+  };
+  if (tile == 9) return kind == 0 ? p8name(192, false) : "";
+  if (tile == 10) return kind == 0 ? p8name(320, false) : "";
   if (tile == 0 && kind <= 1 && p8_auto(M, N, K, kind == 1)) {
-    if (splits <= 1 && kind == 0 && p8_bn(M, N, false) == 320) return "gemm_p8<128x320>";
-    if (splits <= 1 && kind == 0 && p8_bn192(M, N, false)) return "gemm_p8<256x192>";
+    if (splits <= 1 && kind == 0 && p8_bn(M, N, false) == 320) return p8name(320, false);
+    if (splits <= 1 && kind == 0 && p8_bn192(M, N, false)) return p8name(192, false);
     tile = 8;
   }
   choose(M, N, K, kind == 1, kind == 2, ws_bytes, tile, splits);
-  if (tile == 8) return kind == 1 ? "gemm_p8<256x256,geglu>" : "gemm_p8<256x256>";
+  if (tile == 8) return p8name(256, kind == 1);
   if (splits > 1) return split_names[tile - 1];
   return names[tile - 1][kind == 2 ? 2 : kind];
 }

@@ -56,6 +56,8 @@ struct P8Cfg {  // the epilogue's view of the tile (same wave tiling as RingCfg<
   // the tile's up-projection columns V [BN rows][16] (32-B rows), staged once in the prologue
   static constexpr int LORA_OFF = 2 * BUF, V_OFF = 2 * BUF + 5 * 1024, LORA_END = V_OFF + BN * 32;
   static constexpr int LDS_LORA = LORA_END > EPI_BYTES ? LORA_END : EPI_BYTES;
+  // PERSIST: the epilogue stages through the LDS past the ring (the ring holds the next tile's first k-tiles)
+  static constexpr int EPI_OFF = 2 * BUF, EPI_REGION = 160 * 1024 - 2 * BUF;
   static_assert((BM == 256 && (BN == 256 || BN == 192)) || (BM == 128 && BN == 320), "tile shape");
   static_assert(LDS <= 160 * 1024 && LDS_LORA <= 160 * 1024, "LDS budget");
 };
@@ -290,6 +292,114 @@ __device__ __forceinline__ void xattn_epilogue(const GemmArgs& p, char* smem, co
   }
 }
 
+// PERSIST epilogue (EPI 0 bias / row bias / residual, 1 GEGLU, 3 bias + GELU): the same rounding points and stores as
+// tile_epilogue, staged through the EPI_REGION bytes past the ring in passes of 32 * IPP tile rows (IPP 16-row
+// accumulator blocks of both wave rows), so the ring's buffers keep the next tile's first k-tiles in flight.  Staged
+// rows are unpadded; 16-B chunk c of staged row r sits at chunk c ^ (r & 7) (every row holds a multiple of 8 chunks).
+template <class Cfg, int EPI>
+__device__ __forceinline__ void p8_epilogue_passes(const GemmArgs& p, char* R, const int m0, const int n0,
+                                                   f32x4 (&acc)[Cfg::MI][Cfg::NJ], const int wr, const int wc) {
+  constexpr int MI = Cfg::MI, NJ = Cfg::NJ, WM = Cfg::WM, THREADS = Cfg::THREADS;
+  constexpr int OC = EPI == 1 ? Cfg::BN / 2 : Cfg::BN;  // output columns of the tile
+  constexpr int ROWB = OC * 2, REGION = Cfg::EPI_REGION;
+  constexpr int IPP = (MI >= 8 && 256 * ROWB <= REGION) ? 8
+                      : (MI >= 4 && 128 * ROWB <= REGION) ? 4
+                      : (MI >= 2 && 64 * ROWB <= REGION) ? 2 : 1;
+  constexpr int PR = 32 * IPP, NPASS = MI / IPP, CPR = OC / 8, ITEMS = PR * CPR / THREADS;
+  static_assert(PR * ROWB <= REGION && (PR * CPR) % THREADS == 0 && CPR % 8 == 0 && MI % IPP == 0, "pass split");
+  static_assert(EPI != 1 || (Cfg::WN == 64 && NJ == 4), "GEGLU: [32 hidden | 32 gate] per wave column");
+  const int tid = threadIdx.x, lane = tid & 63, fr = lane & 15, fq = lane >> 4;
+  const int lcol0 = wc * Cfg::WN + 4 * fq;
+  auto swz = [](int lr, int byte) { return lr * ROWB + (((byte >> 4) ^ (lr & 7)) << 4) + (byte & 15); };
+  if (p.bias) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int n = n0 + lcol0 + j * 16;
+      f32x4 b4;
+      if (n + 4 <= p.N) {
+        b4 = *reinterpret_cast<const f32x4*>(p.bias + n);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) b4[e] = n + e < p.N ? p.bias[n + e] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i) acc[i][j] += b4;
+    }
+  }
+  const auto rr = make_rsrc(p.R ? p.R : p.Wt, p.R ? p.r_bytes : 0u);
+  const int nout = EPI == 1 ? p.N / 2 : p.N, c0 = EPI == 1 ? n0 / 2 : n0;
+#pragma unroll
+  for (int q = 0; q < NPASS; ++q) {
+    // residual chunks of this pass first: their latency overlaps the staging
+    u32x4 res[EPI == 0 ? ITEMS : 1];
+    if (EPI == 0 && p.R) {
+#pragma unroll
+      for (int k = 0; k < ITEMS; ++k) {
+        const int idx = tid + k * THREADS, lr = idx / CPR, cc = idx - lr * CPR;
+        const int row = (lr / (16 * IPP)) * WM + q * IPP * 16 + lr % (16 * IPP), m = m0 + row, n = n0 + cc * 8;
+        res[k] = buf_load16(rr, (m < p.M && n + 8 <= p.N) ? (m * p.ldr + n) * 2 : kOOB);
+      }
+    }
+#pragma unroll
+    for (int ii = 0; ii < IPP; ++ii) {
+      const int i = q * IPP + ii, lr = wr * 16 * IPP + ii * 16 + fr;
+      if constexpr (EPI == 1) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          float o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float h = bf2f(f2bf(acc[i][j][e])), g = bf2f(f2bf(acc[i][j + 2][e]));
+            o[e] = h * gelu_erf(g);
+          }
+          const u32x2 v{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
+          *reinterpret_cast<u32x2*>(R + swz(lr, (wc * 32 + j * 16 + 4 * fq) * 2)) = v;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          f32x4 a4 = acc[i][j];
+          if constexpr (EPI == 3) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) a4[e] = gelu_erf(a4[e]);
+          }
+          const u32x2 v{pack2bf(a4[0], a4[1]), pack2bf(a4[2], a4[3])};
+          *reinterpret_cast<u32x2*>(R + swz(lr, (lcol0 + j * 16) * 2)) = v;
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+      const int idx = tid + k * THREADS, lr = idx / CPR, cc = idx - lr * CPR;
+      const int row = (lr / (16 * IPP)) * WM + q * IPP * 16 + lr % (16 * IPP), m = m0 + row, n = c0 + cc * 8;
+      if (m >= p.M || n >= nout) continue;  // (nout % 8 == 0: the launcher's condition)
+      float v[8];
+      unpack8(*reinterpret_cast<const u32x4*>(R + swz(lr, cc * 16)), v);
+      if constexpr (EPI == 0) {
+        if (p.rbias) {
+          const float* rb = p.rbias + (size_t)(m / p.rbias_div) * p.ldrb + n;
+          const f32x4 r0 = *reinterpret_cast<const f32x4*>(rb), r1 = *reinterpret_cast<const f32x4*>(rb + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { v[e] += r0[e]; v[e + 4] += r1[e]; }
+        }
+        if (p.R) {
+          float r8[8];
+          unpack8(res[k], r8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += r8[e];
+        }
+      }
+      *reinterpret_cast<u32x4*>(p.C + (size_t)m * p.ldc + n) = pack8(v);
+    }
+    if (q + 1 < NPASS) {  // every wave's reads of this pass done before the next pass restages the region
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+}
+
 // LORA (vst_gemm_lora, UnZipLoRA / LoRA projections): the down-projection u = x . Acat^T is accumulated inside the
 // k-loop from the A fragments already in registers, so no separate pass over x produces it.  Each k-tile also
 // stages Acat's 16 u columns of this tile ([16][64] bf16, one extra DMA per wave issued with slot Amq0: waves 0-1
@@ -303,13 +413,14 @@ __device__ __forceinline__ void xattn_epilogue(const GemmArgs& p, char* smem, co
 // so a 64-deep k-tile is one tap of one source.  Each A slot's DMAs are issued for consecutive k-tiles, so a (tap,
 // channel) cursor per slot advances by 64 per issue and its pieces' row bases are recomputed only when the tap or the
 // source changes (padding rows read out of range: zeros).  Same k order as the ring kernel's conv: same bits.
-template <int EPI, int BN, bool LORA = false, int PH = 3, int BM = 256, bool CONV = false>
+template <int EPI, int BN, bool LORA = false, int PH = 3, int BM = 256, bool CONV = false, bool PERSIST = false>
 __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using Cfg = P8Cfg<BN, BM>;
   static_assert(!CONV || (!LORA && EPI == 0), "conv: plain epilogue");
   static_assert(EPI != 1 || BN == 256, "GEGLU needs 64-column [hidden | gate] blocks");
   static_assert(!LORA || EPI != 1, "in-GEMM LoRA: linear epilogue");
+  static_assert(!PERSIST || (!LORA && EPI != 4 && PH == 2), "persistent tiles: plain / GEGLU / GELU / conv, PH 2");
   static_assert(EPI != 4 || (BN == 192 && BM == 256), "cross-attention epilogue: 256 x 192 tiles (3 heads)");
   constexpr int LX = LORA ? 1 : 0;  // the Acat DMA in the vmcnt counts
   constexpr int BUF = Cfg::BUF, RB1 = Cfg::RB1, NJ1 = Cfg::NJ1, NPB1 = Cfg::NPB1, NPA = Cfg::NPA;
@@ -333,7 +444,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   const auto ra2 = make_rsrc(p.A2 ? p.A2 : p.A1, p.A2 ? p.a2_bytes : 0u);
   const auto rw = make_rsrc(p.Wt, p.w_bytes);
   const int nk = (p.K + 63) / 64;
-  const bool ktail = (p.K & 63) != 0;
+  const bool ktail = !PERSIST && (p.K & 63) != 0;  // (PERSIST: K % 64 == 0 and one A source, the launcher's terms)
   const bool late = wid >= 4;
 #ifdef VST_P8_TRACE
   // diagnostics build only (VST_GEMM_ABLATE): 1 no loop DMA, 2 no MFMA, 4 no loop vmcnt waits, 16 no fragment reads
@@ -357,6 +468,10 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   int ub0 = 0, lc8 = 0;          // LORA: the tile's first u column (16-aligned); this lane's Acat chunk * 8
   uint32_t lbase = (uint32_t)kOOB;  // LORA: this lane's Acat source row / chunk (waves 0-1)
   int n0_tile = 0;
+  // PERSIST: global index of the current tile's first k-tile (the LDS buffer of k-tile kt is (kofs + kt) & 1), and
+  // the next tile of this workgroup, whose first two k-tiles are streamed in by the current tile's last two
+  int kofs = 0, nm0 = 0, nn0 = 0;
+  bool has_next = false;
   auto setup_tile = [&](int m0, int n0) {
     n0_tile = n0;
     if constexpr (LORA) {
@@ -427,16 +542,17 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     if (cv_ci[s] == Ctot) { cv_ci[s] = 0; ++cv_tap[s]; }
     cv_rebase[s] = cv_ci[s] == 0 || (p.C2 > 0 && cv_ci[s] == p.C1);
   };
-  // slot s of k-tile kt into buffer (kt & 1); kt >= kend: out-of-range offsets (zeros), keeps vmcnt counts uniform
-  auto dma_slot = [&](int s, int kt, int kend) {
+  // slot s of k-tile kt into buffer ((kbase + kt) & 1); kt >= kend: out-of-range offsets (zeros), keeps vmcnt counts
+  // uniform
+  auto dma_slot = [&](int s, int kt, int kend, int kbase) {
     if ((abl & 1) && kt > 1) return;
-    char* dst = smem + (kt & 1) * BUF + slot_off(s) + PB * 1024;
+    char* dst = smem + ((kbase + kt) & 1) * BUF + slot_off(s) + PB * 1024;
     const int k0 = kt * 64;
     const bool live = kt < kend && !((abl & 32) && kt > 1);
     if (CONV && s < 2) {
       conv_dma(s, live, dst);
     } else if (s < 2) {
-      const bool second = k0 >= p.K1;
+      const bool second = !PERSIST && k0 >= p.K1;
       const uint32_t kb = (uint32_t)(second ? k0 - p.K1 : k0) * 2u;
 #pragma unroll
       for (int pc = 0; pc < NPA; ++pc) {
@@ -457,12 +573,12 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   // slot s of a k-tile that is live and fully inside K (every k-tile but the last two of a segment): no checks
   auto dma_fast = [&](int s, int kt) {
     if ((abl & 1) && kt > 1) return;
-    char* dst = smem + (kt & 1) * BUF + slot_off(s) + PB * 1024;
+    char* dst = smem + ((kofs + kt) & 1) * BUF + slot_off(s) + PB * 1024;
     const int k0 = kt * 64;
     if (CONV && s < 2) {
       conv_dma(s, true, dst);
     } else if (s < 2) {
-      const bool second = k0 >= p.K1;
+      const bool second = !PERSIST && k0 >= p.K1;
       const uint32_t kb = (uint32_t)(second ? k0 - p.K1 : k0) * 2u;
 #pragma unroll
       for (int pc = 0; pc < NPA; ++pc)
@@ -496,7 +612,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   for (int j = 0; j < 2; ++j) for (int h = 0; h < 2; ++h) fb0[j][h] = bf16x8{};
   for (int j = 0; j < NJ1; ++j) for (int h = 0; h < 2; ++h) fb1[j][h] = bf16x8{};
 #endif
-  auto read_a = [&](int buf, int mq) {
+  auto read_a = [&](int buf, int mq) {  // (buf: the LDS buffer, 0 or 1)
     if (abl & 16) return;
     const char* S = smem + buf * BUF + slot_off(mq);
 #pragma unroll
@@ -561,9 +677,9 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
                    row2 < BN && n2 < p.N ? (int)(((uint32_t)n2 * p.ldw + p.K + ub0 + 8 * (lane & 1)) * 2u) : kOOB);
       }
     }
-    dma_slot(0, kb, ke); dma_lora(kb, ke, true); dma_slot(2, kb, ke); dma_slot(3, kb, ke);
-    dma_slot(1, kb, ke); dma_slot(3, kb + 1, ke); dma_slot(0, kb + 1, ke); dma_lora(kb + 1, ke, true);
-    dma_slot(2, kb + 1, ke);
+    dma_slot(0, kb, ke, 0); dma_lora(kb, ke, true); dma_slot(2, kb, ke, 0); dma_slot(3, kb, ke, 0);
+    dma_slot(1, kb, ke, 0); dma_slot(3, kb + 1, ke, 0); dma_slot(0, kb + 1, ke, 0); dma_lora(kb + 1, ke, true);
+    dma_slot(2, kb + 1, ke, 0);
     p8_vmwait<2 * NPA + 2 + NPB1 + LX>();  // A0, (Acat,) B0, B1 of kb landed
     p8_barrier();
     VST_P8_STAMP(1)
@@ -573,7 +689,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     auto ktile = [&](int t, auto fast_tag) {
       constexpr bool FAST = decltype(fast_tag)::value;
       auto dma = [&](int s_, int kt) {
-        if constexpr (FAST) dma_fast(s_, kt); else dma_slot(s_, kt, ke);
+        if constexpr (FAST) dma_fast(s_, kt); else dma_slot(s_, kt, ke, 0);
       };
       const int buf = t & 1;
       // I0
@@ -623,7 +739,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   // Every load segment ends with its LDS reads retired (lgkmcnt(0)) before its barrier, so a slot read in interval X is
   // refilled from interval X + 1 on (WAR); a slot waited for in interval X is read in X + 1 (RAW, both groups' waits
   // precede the barrier the later reader passes).  Same k order per accumulator as PH = 3: bitwise-equal results.
-  auto run_segment2 = [&](int kb, int ke) {
+  auto run_segment2 = [&](int kb, int ke, bool first) {
 #pragma unroll
     for (int i = 0; i < Cfg::MI; ++i)
 #pragma unroll
@@ -641,10 +757,12 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
                    row2 < BN && n2 < p.N ? (int)(((uint32_t)n2 * p.ldw + p.K + ub0 + 8 * (lane & 1)) * 2u) : kOOB);
       }
     }
-    dma_slot(0, kb, ke); dma_lora(kb, ke, true); dma_slot(2, kb, ke); dma_slot(3, kb, ke);
-    dma_slot(1, kb, ke);
-    dma_slot(0, kb + 1, ke); dma_lora(kb + 1, ke, true); dma_slot(2, kb + 1, ke);
-    p8_vmwait<2 * NPA + 2 + LX>();  // A0, (Acat,) B0, B1 of kb landed; A1(kb), A0/B0(kb + 1) in flight
+    if (!PERSIST || first) {  // (PERSIST: later tiles' first k-tiles were issued by the previous tile and have landed)
+      dma_slot(0, kb, ke, kofs); dma_lora(kb, ke, true); dma_slot(2, kb, ke, kofs); dma_slot(3, kb, ke, kofs);
+      dma_slot(1, kb, ke, kofs);
+      dma_slot(0, kb + 1, ke, kofs); dma_lora(kb + 1, ke, true); dma_slot(2, kb + 1, ke, kofs);
+      p8_vmwait<2 * NPA + 2 + LX>();  // A0, (Acat,) B0, B1 of kb landed; A1(kb), A0/B0(kb + 1) in flight
+    }
     p8_barrier();
     VST_P8_STAMP(1)
     if (late) p8_barrier();
@@ -652,9 +770,15 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     auto ktile2 = [&](int t, auto fast_tag) {
       constexpr bool FAST = decltype(fast_tag)::value;
       auto dma = [&](int s_, int kt) {
-        if constexpr (FAST) dma_fast(s_, kt); else dma_slot(s_, kt, ke);
+        if constexpr (FAST) {
+          dma_fast(s_, kt);
+        } else if (PERSIST && kt >= ke && has_next) {
+          dma_slot(s_, kt - ke, ke, kofs + ke);  // the next tile's first k-tiles (bases switched at J1(ke - 2))
+        } else {
+          dma_slot(s_, kt, ke, kofs);
+        }
       };
-      const int buf = t & 1;
+      const int buf = (kofs + t) & 1;
       // J0
       read_a(buf, 0);
       read_b(buf, 0, fb0);
@@ -673,6 +797,15 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       // J1
       read_a(buf, 1);
       if (!(abl & 4)) p8_vmwait<NPA>();  // A0, (Acat,) B0, B1 of t + 1 landed
+      // PERSIST: every slot has issued its last DMA of this tile (A0 / B0 at J1(ke - 3), A1 / B1 at J0(ke - 2)), so the
+      // slots' source bases switch to the next tile here
+      if (PERSIST && !FAST && t == ke - 2 && has_next) {
+        setup_tile(nm0, nn0);
+        if constexpr (CONV) {  // the A slots' (tap, channel) cursors restart at the next tile's first k-tile
+          cv_tap[0] = cv_tap[1] = cv_ci[0] = cv_ci[1] = 0;
+          cv_rebase[0] = cv_rebase[1] = true;
+        }
+      }
       dma(0, t + 2);
       dma_lora(t + 2, ke, !FAST);
       dma(2, t + 2);
@@ -689,16 +822,49 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     for (; t < ke_fast; ++t) ktile2(t, std::true_type{});
     for (; t < ke; ++t) ktile2(t, std::false_type{});
     if (!late) p8_barrier();
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the trailing zero DMAs land before LDS reuse
+    if constexpr (PERSIST) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the next tile's k-tiles stay in flight
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the trailing zero DMAs land before LDS reuse
+    }
     p8_barrier();
   };
 #undef VST_P8_QUAD
 
   int m0, n0;
   VST_P8_STAMP(0)
+  if constexpr (PERSIST) {
+    // gridDim.x (a multiple of 8) workgroups walk the tiles: the workgroups sharing an XCD (b % 8) take that XCD's
+    // contiguous chunk of logical tiles in rounds, as the one-tile-per-workgroup launch places them.  Each tile's last
+    // two k-tiles stream the next tile's first two into the ring, and its epilogue stages through the LDS past the ring.
+    const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3, per = gridDim.x >> 3;
+    const int q = ntiles >> 3, r = ntiles & 7;
+    const int beg = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    const int cnt = q + (xcd < r ? 1 : 0);
+    if (loc >= cnt) return;  // (whole workgroup; the launcher keeps gridDim.x <= ntiles)
+    int j = loc;
+    tile_origin(beg + j, m0, n0);
+    setup_tile(m0, n0);
+    bool first = true;
+    while (true) {
+      const int jn = j + per;
+      has_next = jn < cnt;
+      if (has_next) tile_origin(beg + jn, nm0, nn0);
+      run_segment2(0, nk, first);
+      p8_epilogue_passes<Cfg, EPI>(p, smem + Cfg::EPI_OFF, m0, n0, acc, wr, wc);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // stores done; the next tile's k-tiles landed
+      p8_barrier();
+      if (!has_next) return;
+      j = jn;
+      m0 = nm0;
+      n0 = nn0;
+      kofs += nk;
+      first = false;
+    }
+  }
   tile_origin(xcd_remap(blockIdx.x, ntiles), m0, n0);
   setup_tile(m0, n0);
-  if constexpr (PH == 2) run_segment2(0, nk);
+  if constexpr (PH == 2) run_segment2(0, nk, true);
   else run_segment(0, nk);
   VST_P8_STAMP(2)
   if constexpr (LORA) {
@@ -766,10 +932,58 @@ static int launch_p8_ph(const GemmArgs& a, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 
+// Persistent tiles (VST_P8_PERSIST=1): a grid of one workgroup per CU walks the tiles; each tile's last two k-tiles
+// stream the next tile's first two into the ring, so a tile's fill overlaps the previous tile's epilogue.
+static int g_p8_persist = -1;  // VST_P8_PERSIST, or vst_p8_persist (tests, A/B)
+static int p8_persist_env() {
+  if (g_p8_persist < 0) {
+    const char* e = getenv("VST_P8_PERSIST");
+    g_p8_persist = e ? atoi(e) : 0;
+  }
+  return g_p8_persist;
+}
+static int p8_cus() {
+  static const int v = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 8)
+      n = 256;
+    return n & ~7;
+  }();
+  return v;
+}
+
+// whether launch_gemm_p8 runs the persistent kernel for this shape: the 2-interval schedule, at least two tiles per
+// workgroup, K a multiple of 64 and >= 128 (the stream hands over two whole k-tiles), whole 8-column output chunks
+// (and one A source: launch_p8_epi)
+bool p8_persist_applies(int M, int N, int K, int epi, int bn) {
+  if (!p8_persist_env() || p8_ph_env() != 2 || (epi != 0 && epi != 1 && epi != 3)) return false;
+  const int bm = bn == 320 ? 128 : 256;
+  const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  return tiles >= 2L * p8_cus() && K >= 128 && (K & 63) == 0 && (N % (epi == 1 ? 16 : 8)) == 0;
+}
+
+template <int EPI, int BN, int BM, bool CONV = false>
+static int launch_p8_persist(const GemmArgs& a, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_p8_kernel<EPI, BN, false, 2, BM, CONV, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  const int ntiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  const int grid = ntiles < p8_cus() ? (ntiles & ~7) : p8_cus();
+  if (grid < 8) return VST_ERR_ARG;
+  hipLaunchKernelGGL((gemm_p8_kernel<EPI, BN, false, 2, BM, CONV, true>), dim3(grid), dim3(512), 160 * 1024, s, a);
+  return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+}
+
 // BN = 320 runs 128-row tiles (P8Cfg)
 template <int EPI, int BN, bool LORA = false>
 static int launch_p8_epi(const GemmArgs& a, hipStream_t s) {
   constexpr int BM = BN == 320 ? 128 : 256;
+  if constexpr (!LORA && EPI != 4)
+    if (!a.A2 && p8_persist_applies(a.M, a.N, a.K, EPI, BN)) return launch_p8_persist<EPI, BN, BM>(a, s);
   return p8_ph_env() == 2 ? launch_p8_ph<EPI, BN, LORA, 2, BM>(a, s) : launch_p8_ph<EPI, BN, LORA, 3, BM>(a, s);
 }
 
@@ -790,6 +1004,9 @@ int launch_gemm_p8_xattn(const GemmArgs& a, hipStream_t s) {
 int launch_gemm_p8_conv(const GemmArgs& a, int bn, hipStream_t s) {
   if ((a.C1 & 63) || (a.C2 & 63) || a.K != 9 * (a.C1 + a.C2)) return VST_ERR_ARG;
   const bool ph2 = p8_ph_env() == 2;
+  // persistent grid: 128x320 tiles only (every SDXL conv width is a multiple of 320; the 256-row conv tiles run
+  // out of registers with the tile loop's state)
+  if (bn == 320 && p8_persist_applies(a.M, a.N, a.K, 0, bn)) return launch_p8_persist<0, 320, 128, true>(a, s);
   switch (bn) {
     case 256: return ph2 ? launch_p8_ph<0, 256, false, 2, 256, true>(a, s) : launch_p8_ph<0, 256, false, 3, 256, true>(a, s);
     case 192: return ph2 ? launch_p8_ph<0, 192, false, 2, 256, true>(a, s) : launch_p8_ph<0, 192, false, 3, 256, true>(a, s);
@@ -818,6 +1035,12 @@ int launch_gemm_p8(const GemmArgs& a, int epi, int bn, hipStream_t s) {
 }
 
 }  // namespace vst
+
+extern "C" int vst_p8_persist(int on) {
+  const int prev = vst::p8_persist_env() ? 1 : 0;
+  vst::g_p8_persist = on ? 1 : 0;
+  return prev;
+}
 
 #ifdef VST_P8_TRACE
 extern "C" int vst_p8_trace_read(void* host_dst, int n_wg) {

@@ -186,6 +186,21 @@ class p8_conv:
         _lib.load().vst_p8_conv(self.prev)
 
 
+class p8_persist:
+    """Context manager switching the 8-phase GEMM's persistent grid on / off (vst_p8_persist) for the GEMMs launched
+    inside it; tests and A/B runs only (the outputs are the same bits either way)."""
+
+    def __init__(self, on=True):
+        self.on = int(bool(on))
+
+    def __enter__(self):
+        self.prev = int(_lib.load().vst_p8_persist(self.on))
+        return self
+
+    def __exit__(self, *a):
+        _lib.load().vst_p8_persist(self.prev)
+
+
 class p8_tile_width:
     """Context manager forcing the 8-phase GEMM's tile width (256 / 192 / 320 where legal; 0 = the library's
     policy) for the GEMMs launched inside it (vst_p8_force_bn); tests and A/B runs only."""
