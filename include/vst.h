@@ -65,7 +65,8 @@ int vst_p8_force_bn(int bn);
 int vst_p8_conv(int on);
 /* Test / A-B knob: the 8-phase kernel's persistent grid (one workgroup per CU walking the tiles, each tile's last
  * k-tiles streaming the next tile's first ones) for GEMMs of two or more tile rounds (1) or one workgroup per tile
- * (0), for every later GEMM of this process (default: VST_P8_PERSIST); returns the previous setting.  Same bits. */
+ * (0), for every later GEMM of this process (default: VST_P8_PERSIST, else 1; not the convs); returns the previous
+ * setting.  Same bits. */
 int vst_p8_persist(int on);
 
 /* attn2 of a BasicTransformerBlock as ONE launch: the q projection (vst_gemm_lora when Acat != NULL, else

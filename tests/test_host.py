@@ -179,7 +179,8 @@ def test_gemm_kernel_policy_host_only():
     name = K.gemm_kernel_name
     assert name(8192, 32, 1280, 0) == "gemm_skinny"            # UnZipLoRA down-projection
     assert name(131072, 320, 40, 3) == "gemm_kernel<conv_in>"  # Cin = 4 gather conv
-    assert name(8192, 10240, 1280, 1).endswith("geglu>")        # GEGLU epilogue kept
+    assert name(8192, 10240, 1280, 1) == "gemm_p8<256x256,geglu,persist>"  # GEGLU epilogue, persistent grid
+    assert name(8192, 1280, 5120, 0) == "gemm_p8<256x192>"      # one round of tiles: one workgroup per tile
     assert name(2, 1280, 1280, 0) == "gemm_rows"                # temb projection: M = 2
     assert name(2, 13760, 1280, 0) == "gemm_rows"               # batched time_emb_proj of every resnet
     assert name(9, 1280, 1280, 0).endswith("splitk>")           # M > 8: split-K tiles

@@ -17,3 +17,5 @@ for v in 0 1 0 1; do
   VST_P8_PERSIST=$v run 300 r4k_bench_persist${v}_$RANDOM.json python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-peaks --no-vae
 done
 for f in gpurun_out/r4k_bench_*.json; do python -c "import json; l=[x for x in open('$f') if x.startswith('{')][-1]; d=json.loads(l); k=d['kernels']; print('$f', d['ms_per_step'], {n: v['ms_per_step'] for n, v in k.items() if 'gemm_p8' in n})"; done
+run 120 r4k_copy.txt python -u tools/copy_roofline.py
+cat gpurun_out/r4k_copy.txt

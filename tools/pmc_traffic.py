@@ -29,12 +29,14 @@ def bench_symbol(name: str) -> str:
         tag = {("0", "0"): "", ("0", "1"): ",geglu", ("1", "0"): ",conv", ("0", "2"): ",splitk",
                ("1", "2"): ",splitk"}.get((amode, epi), f",a{amode}e{epi}")
         return f"gemm_ring<{bm}x{bn}{tag}>"
-    # gemm_p8_kernel<EPI, BN, LORA, PH, BM>
-    m = re.search(r"gemm_p8_kernel<(\d), (\d+)(?:, (true|false))?(?:, \d)?(?:, (\d+))?>", name)
+    # gemm_p8_kernel<EPI, BN, LORA, PH, BM, CONV, PERSIST>
+    m = re.search(r"gemm_p8_kernel<(\d), (\d+), (true|false), \d, (\d+)(?:, (true|false))?(?:, (true|false))?>", name)
     if m:
-        epi, bn, lora, bm = m.groups()
-        tags = (",lora" if lora == "true" else "") + (",geglu" if epi == "1" else "") + (",xattn" if epi == "4" else "")
-        return f"gemm_p8<{bm or 256}x{bn}{tags}>"
+        epi, bn, lora, bm, conv, persist = m.groups()
+        tags = ((",lora" if lora == "true" else "") + (",conv" if conv == "true" else "") +
+                (",geglu" if epi == "1" else "") + (",xattn" if epi == "4" else "") +
+                (",persist" if persist == "true" else ""))
+        return f"gemm_p8<{bm}x{bn}{tags}>"
     if "layernorm_lora_kernel" in name:
         return "layernorm_lora"
     for k, v in (("gemm_skinny", "gemm_skinny"), ("spatial_attn_kernel", "spatial_attn_kernel"),

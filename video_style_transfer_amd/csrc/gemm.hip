@@ -970,8 +970,7 @@ extern "C" const char* vst_gemm_kernel_name(int M, int N, int K, int kind, int t
   if (kind == 2 && tile == 0 && splits <= 1 && p8_conv_env() && K % 576 == 0 && N % 64 == 0 &&
       p8_auto(M, N, K, false)) {
     const int bn = N % 320 == 0 ? 320 : p8_bn(M, N, false) == 192 ? 192 : 256;
-    if (bn == 320) return p8_persist_applies(M, N, K, 0, bn) ? "gemm_p8<128x320,conv,persist>" : "gemm_p8<128x320,conv>";
-    return bn == 192 ? "gemm_p8<256x192,conv>" : "gemm_p8<256x256,conv>";
+    return bn == 320 ? "gemm_p8<128x320,conv>" : bn == 192 ? "gemm_p8<256x192,conv>" : "gemm_p8<256x256,conv>";
   }
   if (kind == 0 && tile == 0 && rows_applies(M, N, K)) return "gemm_rows";
   if (kind == 0 && (tile == 5 || (tile == 0 && N <= 64 && M >= 1024))) return "gemm_skinny";  // no-epilogue calls

@@ -420,7 +420,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   static_assert(!CONV || (!LORA && EPI == 0), "conv: plain epilogue");
   static_assert(EPI != 1 || BN == 256, "GEGLU needs 64-column [hidden | gate] blocks");
   static_assert(!LORA || EPI != 1, "in-GEMM LoRA: linear epilogue");
-  static_assert(!PERSIST || (!LORA && EPI != 4 && PH == 2), "persistent tiles: plain / GEGLU / GELU / conv, PH 2");
+  static_assert(!PERSIST || (!LORA && !CONV && EPI != 4 && PH == 2), "persistent tiles: plain / GEGLU / GELU, PH 2");
   static_assert(EPI != 4 || (BN == 192 && BM == 256), "cross-attention epilogue: 256 x 192 tiles (3 heads)");
   constexpr int LX = LORA ? 1 : 0;  // the Acat DMA in the vmcnt counts
   constexpr int BUF = Cfg::BUF, RB1 = Cfg::RB1, NJ1 = Cfg::NJ1, NPB1 = Cfg::NPB1, NPA = Cfg::NPA;
@@ -799,13 +799,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       if (!(abl & 4)) p8_vmwait<NPA>();  // A0, (Acat,) B0, B1 of t + 1 landed
       // PERSIST: every slot has issued its last DMA of this tile (A0 / B0 at J1(ke - 3), A1 / B1 at J0(ke - 2)), so the
       // slots' source bases switch to the next tile here
-      if (PERSIST && !FAST && t == ke - 2 && has_next) {
-        setup_tile(nm0, nn0);
-        if constexpr (CONV) {  // the A slots' (tap, channel) cursors restart at the next tile's first k-tile
-          cv_tap[0] = cv_tap[1] = cv_ci[0] = cv_ci[1] = 0;
-          cv_rebase[0] = cv_rebase[1] = true;
-        }
-      }
+      if (PERSIST && !FAST && t == ke - 2 && has_next) setup_tile(nm0, nn0);
       dma(0, t + 2);
       dma_lora(t + 2, ke, !FAST);
       dma(2, t + 2);
@@ -932,13 +926,16 @@ static int launch_p8_ph(const GemmArgs& a, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 
-// Persistent tiles (VST_P8_PERSIST=1): a grid of one workgroup per CU walks the tiles; each tile's last two k-tiles
-// stream the next tile's first two into the ring, so a tile's fill overlaps the previous tile's epilogue.
+// Persistent tiles (default; VST_P8_PERSIST=0 restores one workgroup per tile): a grid of one workgroup per CU walks
+// the tiles; each tile's last two k-tiles stream the next tile's first two into the ring, so a tile's fill overlaps
+// the previous tile's epilogue.  Same bits.  Measured (tools/p8_ph_ab.py, profiles/r4_p8_persist_ab.txt): 0-15 %
+// faster per launch on the step's multi-round shapes (K = 320 / 640 most), the denoise step -0.9 ms same-box; the
+// convs stay on one workgroup per tile (their persistent variant spilled SGPRs and ran 2 % slower).
 static int g_p8_persist = -1;  // VST_P8_PERSIST, or vst_p8_persist (tests, A/B)
 static int p8_persist_env() {
   if (g_p8_persist < 0) {
     const char* e = getenv("VST_P8_PERSIST");
-    g_p8_persist = e ? atoi(e) : 0;
+    g_p8_persist = e ? atoi(e) : 1;
   }
   return g_p8_persist;
 }
@@ -963,18 +960,18 @@ bool p8_persist_applies(int M, int N, int K, int epi, int bn) {
   return tiles >= 2L * p8_cus() && K >= 128 && (K & 63) == 0 && (N % (epi == 1 ? 16 : 8)) == 0;
 }
 
-template <int EPI, int BN, int BM, bool CONV = false>
+template <int EPI, int BN, int BM>
 static int launch_p8_persist(const GemmArgs& a, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_p8_kernel<EPI, BN, false, 2, BM, CONV, true>,
+    (void)hipFuncSetAttribute((const void*)gemm_p8_kernel<EPI, BN, false, 2, BM, false, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
   const int ntiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   const int grid = ntiles < p8_cus() ? (ntiles & ~7) : p8_cus();
   if (grid < 8) return VST_ERR_ARG;
-  hipLaunchKernelGGL((gemm_p8_kernel<EPI, BN, false, 2, BM, CONV, true>), dim3(grid), dim3(512), 160 * 1024, s, a);
+  hipLaunchKernelGGL((gemm_p8_kernel<EPI, BN, false, 2, BM, false, true>), dim3(grid), dim3(512), 160 * 1024, s, a);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 
@@ -1004,9 +1001,6 @@ int launch_gemm_p8_xattn(const GemmArgs& a, hipStream_t s) {
 int launch_gemm_p8_conv(const GemmArgs& a, int bn, hipStream_t s) {
   if ((a.C1 & 63) || (a.C2 & 63) || a.K != 9 * (a.C1 + a.C2)) return VST_ERR_ARG;
   const bool ph2 = p8_ph_env() == 2;
-  // persistent grid: 128x320 tiles only (every SDXL conv width is a multiple of 320; the 256-row conv tiles run
-  // out of registers with the tile loop's state)
-  if (bn == 320 && p8_persist_applies(a.M, a.N, a.K, 0, bn)) return launch_p8_persist<0, 320, 128, true>(a, s);
   switch (bn) {
     case 256: return ph2 ? launch_p8_ph<0, 256, false, 2, 256, true>(a, s) : launch_p8_ph<0, 256, false, 3, 256, true>(a, s);
     case 192: return ph2 ? launch_p8_ph<0, 192, false, 2, 256, true>(a, s) : launch_p8_ph<0, 192, false, 3, 256, true>(a, s);
