@@ -49,6 +49,10 @@ def parse():
     ap.add_argument("--parallel", default="frames", choices=["frames", "replicas"],
                     help="N>1: 'frames' shards the frames of every clip over the ranks (all-to-all around each "
                          "motion module, frame_shard.py); 'replicas' runs an independent clip per rank")
+    ap.add_argument("--exchange", default="all_to_all", choices=["all_to_all", "all_gather"],
+                    help="frames mode: the motion modules' exchange; all_to_all (default: frame shard <-> pixel shard, "
+                         "no duplicated work) or all_gather (the north star's: every rank gathers the clip and runs the "
+                         "module over all frames)")
     ap.add_argument("--clips", type=int, default=0,
                     help="frames mode: clips denoised together (default N: per-GPU work fixed at one clip's "
                          "frames = weak scaling; 1 = one clip split N ways = strong scaling); N=1 or replicas: "
@@ -569,7 +573,7 @@ def main():
     shard, nclips = None, max(1, args.clips)
     if world > 1 and args.parallel == "frames":
         from video_style_transfer_amd.frame_shard import FrameShard
-        shard = FrameShard()
+        shard = FrameShard(exchange=args.exchange)
         nclips = args.clips or world
     den = AnimateDiffDenoiser(unet, args.frames, args.size, args.size, num_inference_steps=args.num_inference_steps,
                               guidance_scale=args.guidance, device=dev, shard=shard, num_clips=nclips)
@@ -676,7 +680,9 @@ def main():
                        "global_batch": nclips if shard is not None else nclips * world, "frames": args.frames,
                        "resolution": args.size,
                        "parallelism": (f"frame-shard x{world} ({nclips} clips, {args.frames // world} frames/clip/GPU, "
-                                       f"RCCL all-to-all around each motion module)" if shard is not None else
+                                       + ("RCCL all-to-all around each motion module)" if args.exchange == "all_to_all"
+                                          else "RCCL all-gather of the clip before each motion module)")
+                                       if shard is not None else
                                        f"replicas x{world}" if world > 1 else "single") + (
                                        f", {nclips} clips batched per GPU" if shard is None and nclips > 1 else ""),
                        "graph": graphed,

@@ -59,6 +59,11 @@ def _cpu_worker(rank, world, port, q, F=4):
         assert torch.equal(px, ref), "to_pixels layout"
         # (b) round trip
         assert torch.equal(sh.to_frames(px, B, Fl, HW), x_loc), "to_frames(to_pixels(x)) != x"
+        # (b') the north-star exchange: the all-gather hands every rank the whole clip in (b, f, p) row order, and
+        # local_frames_of takes this rank's frames back out of it
+        gx = sh.gather_frames(x_loc, B, Fl, HW)
+        assert torch.equal(gx, X.reshape(-1, C)), "gather_frames layout"
+        assert torch.equal(sh.local_frames_of(gx, B, Fl, HW), x_loc), "local_frames_of(gather_frames(x)) != x"
         # (c) sharded motion module == oracle motion module
         P = {}
         g = torch.Generator().manual_seed(1)
@@ -185,9 +190,10 @@ def test_frame_shard_unet_two_ranks_one_gpu():
         assert status == "ok", f"rank {rank}: {info}"
 
 
-def _gpu_worker_sdxl768(rank, world, port, q):
+def _gpu_worker_sdxl768(rank, world, port, q, exchange="all_to_all"):
     """BASELINE configs[3] shapes: SDXL + motion modules + UnZipLoRA r=8, 32 frames at 768x768 (96x96 latent),
-    frames split over 2 ranks (16 each) on one GPU, vs the unsharded HIP forward of the whole clip."""
+    frames split over 2 ranks (16 each) on one GPU, vs the unsharded HIP forward of the whole clip; both exchanges
+    (all-to-all around the motion modules, and the north star's all-gather of the clip before them)."""
     try:
         sys.path.insert(0, ROOT)
         _init(rank, world, port)
@@ -206,7 +212,7 @@ def _gpu_worker_sdxl768(rank, world, port, q):
         tids = torch.tensor([[768, 768, 0, 0, 768, 768]], dtype=torch.float32)
         t = torch.tensor([501.0])
         kw = dict(added_cond_kwargs={"text_embeds": pooled.to(dev), "time_ids": tids.to(dev)})
-        sh = FrameShard()
+        sh = FrameShard(exchange=exchange)
         Fl, f0 = sh.local_frames(F)
         part = unet(lat[:, :, f0:f0 + Fl].contiguous().to(dev), t.to(dev), enc.to(dev), frame_shard=sh,
                     **kw).sample.cpu()
@@ -227,12 +233,13 @@ def _gpu_worker_sdxl768(rank, world, port, q):
 
 
 @pytest.mark.gpu
-def test_frame_shard_sdxl_768_32_frames_two_ranks_one_gpu():
+@pytest.mark.parametrize("exchange", ["all_to_all", "all_gather"])
+def test_frame_shard_sdxl_768_32_frames_two_ranks_one_gpu(exchange):
     if torch.cuda.device_count() == 0:
         pytest.skip("no HIP device")
-    res = _spawn(_gpu_worker_sdxl768, 2)
+    res = _spawn(_gpu_worker_sdxl768, 2, exchange)
     for rank, status, info in res:
-        print(f"[shard] configs[3] rank {rank}: {status} {info}")
+        print(f"[shard] configs[3] {exchange} rank {rank}: {status} {info}")
         assert status == "ok", f"rank {rank}: {info}"
 
 

@@ -10,6 +10,8 @@ run() {  # run <limit> <log> cmd...
   return 0
 }
 run 300 r4l_tests.log python -u -m pytest -v -x --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "layer_norm or persistent"
+run 600 r4l_shard.log python -u -m pytest -v -x --timeout 300 --timeout-method thread tests/test_frame_shard.py -k "sdxl_768_32_frames_two"
+grep -E "FAILED|passed|failed|\[shard\]" gpurun_out/r4l_shard.log | tail -6
 grep -E "FAILED|passed|failed" gpurun_out/r4l_tests.log | tail -3
 for v in "0 8" "1 8" "1 4" "1 16" "0 8" "1 8" "1 4" "1 16"; do
   set -- $v

@@ -20,6 +20,12 @@ Per module and rank this moves 2 x (P-1)/P of the rank's activation over xGMI. T
 an all-gather of the clip before the attention (the north-star formulation), and no motion-module
 work is duplicated across ranks.
 
+exchange="all_gather" (opt-in; bench.py --exchange all_gather) is the north-star formulation itself: one all-gather
+of the module's input hands every rank the whole clip, every rank runs the motion module over all frames (GroupNorm,
+proj_in, both frame-attention blocks: frame 0's attn2 K/V depend on every frame's attn1 output, so nothing short of
+the whole module is needed), and keeps its own frames' rows for proj_out + residual.  (P-1)/P of the clip's
+activation per rank and module, and P x the motion-module work; bit-identical to the unsharded forward as well.
+
 The layout permutations around the all-to-all are one HIP kernel each (vst_permute_rows).  A step is captured
 PIECEWISE (PiecewiseGraph): the kernels between two collectives form one HIP graph, and the collectives run between
 the graph replays on the same stream.  So no collective is ever inside a captured graph (RCCL's own graph capture is
@@ -96,9 +102,14 @@ class PiecewiseGraph:
 
 
 class FrameShard:
-    def __init__(self, group=None, permute: Optional[Permute] = None):
+    EXCHANGES = ("all_to_all", "all_gather")
+
+    def __init__(self, group=None, permute: Optional[Permute] = None, exchange: str = "all_to_all"):
         if not dist.is_initialized():
             raise RuntimeError("FrameShard needs an initialised torch.distributed process group")
+        if exchange not in self.EXCHANGES:
+            raise ValueError(f"exchange {exchange!r}: one of {self.EXCHANGES}")
+        self.exchange = exchange
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -184,6 +195,21 @@ class FrameShard:
         recv = torch.empty_like(send)
         self._all_to_all(recv, send)                             # (source rank r, b, f_local, p')
         return self._permute(recv, (P, B, Fl, hp), (1, 0, 2, 3))  # (b, r*Fl + f_local, p')
+
+    def gather_frames(self, h: torch.Tensor, B: int, Fl: int, HW: int) -> torch.Tensor:
+        """rows (b, f_local, p) of this rank's frames -> rows (b, f_global, p) of the whole clip on every rank."""
+        P = self.world
+        if P == 1:
+            return h
+        g = self.all_gather(h)                                          # (rank r, b, f_local, p)
+        return self._permute(g.view(-1, h.shape[1]), (P, B, Fl, HW), (1, 0, 2, 3))  # (b, r*Fl + f_local, p)
+
+    def local_frames_of(self, h: torch.Tensor, B: int, Fl: int, HW: int) -> torch.Tensor:
+        """rows (b, f_global, p) of the whole clip -> rows (b, f_local, p) of this rank's frames."""
+        P = self.world
+        if P == 1:
+            return h
+        return h.view(B, P, Fl * HW, h.shape[1])[:, self.rank].reshape(B * Fl * HW, h.shape[1])
 
     def to_frames(self, h: torch.Tensor, B: int, Fl: int, HW: int) -> torch.Tensor:
         """Inverse of to_pixels."""

@@ -283,6 +283,19 @@ class MotionModule(nn.Module):
         HW = H * W
         shard = ctx.shard
         B, G = nimg // ctx.F, self.norm.num_groups
+        if shard is not None and shard.world > 1 and shard.exchange == "all_gather":
+            # north-star exchange (frame_shard.py): the whole clip on every rank, this rank's frames kept at the end
+            Fl, P = ctx.F, shard.world
+            xf = shard.gather_frames(x, B, Fl, HW)
+            F = Fl * P
+            part = K.group_norm_frame_partials(xf, B * F, HW, G)
+            h = K.group_norm_apply_partials(xf, B, F, HW, G, self.norm.eps, f32(self.norm.weight),
+                                            f32(self.norm.bias), part, 1)
+            h = self.proj_in.run(h)
+            tctx = dataclasses.replace(ctx, F=F)
+            for blk in self.transformer_blocks:
+                h = blk.run(h, B * F, HW, tctx)
+            return self.proj_out.run(shard.local_frames_of(h, B, Fl, HW), residual=x)
         # GroupNorm statistics over every frame of a clip, from per-frame partials merged in one fixed frame order:
         # the same bits whether this process holds the whole clip or a frame shard of it
         part = K.group_norm_frame_partials(x, nimg, HW, G)
