@@ -68,10 +68,6 @@ int vst_p8_conv(int on);
  * (0), for every later GEMM of this process (default: VST_P8_PERSIST, else 1; not the convs); returns the previous
  * setting.  Same bits. */
 int vst_p8_persist(int on);
-/* Test / A-B knob: LayerNorm at C = 320 / 640 / 1280 as a row stream (1: a few waves per SIMD walking the rows, next
- * rows' loads in flight while the current ones are stored) or one row pass per wave (0), for every later LayerNorm of
- * this process (default: VST_LN_STREAM, else 1); returns the previous setting.  Same bits. */
-int vst_layernorm_stream(int on);
 
 /* attn2 of a BasicTransformerBlock as ONE launch: the q projection (vst_gemm_lora when Acat != NULL, else
  * [x].[W]^T) with the cross-attention over the text tokens as its epilogue,

@@ -534,26 +534,6 @@ def test_layer_norm(cuda, K, rows, C, use_pe):
     check(out, ref, name="layernorm")
 
 
-@pytest.mark.parametrize("rows,C,use_pe", [(8192, 1280, False), (32768, 640, True), (131072, 320, True),
-                                           (8193, 1280, True), (1000, 640, False), (7, 320, False),
-                                           (600000, 320, False)])
-def test_layer_norm_stream_bitwise(cuda, K, rows, C, use_pe):
-    """The row-stream LayerNorm (layernorm_r_kernel: waves walking row passes with the next pass's loads in flight,
-    gamma / beta held per lane) against the one-pass-per-wave kernel: the same arithmetic in the same order, so the
-    same bits — step sizes, ragged row counts (a partial last pass, fewer passes than waves, more than two passes per
-    wave) and the motion modules' PE add."""
-    g = torch.Generator().manual_seed(rows + C + 1)
-    x = rnd(rows, C, gen=g).to(cuda)
-    gam, bet = (torch.rand(C, generator=g) + 0.5).to(cuda), (torch.randn(C, generator=g) * 0.1).to(cuda)
-    pe = (torch.randn(32, C, generator=g)).to(cuda) if use_pe else None
-    outs = []
-    for on in (False, True):
-        with K.layernorm_stream(on):
-            outs.append(K.layer_norm(x, gam, bet, 1e-5, pe=pe, pe_div=256, pe_mod=16))
-    torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1])
-
-
 def test_timestep_and_euler(cuda, K):
     t = torch.tensor([981.0, 1.0, 500.0], device=cuda)
     out = torch.zeros(3, 320, dtype=torch.bfloat16, device=cuda)

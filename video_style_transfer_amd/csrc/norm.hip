@@ -491,10 +491,10 @@ __global__ __launch_bounds__(256) void layernorm_g_kernel(const bf16_t* __restri
 #pragma unroll
     for (int i = 0; i < CPL; ++i)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { const float d = v[it][i][e] - mean; sq += d * d; }
+      for (int e = 0; e < 8; ++e) { const float d = v[it][i][e] - mean; sq = fmaf(d, d, sq); }
 #pragma unroll
     for (int o = LPR / 2; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
-    const float rstd = rsqrtf(sq * invc + eps);
+    const float rstd = rsqrtf(fmaf(sq, invc, eps));  // (explicit fmas: codegen-independent rounding)
     if (row >= rows) continue;
     const float* pr = pe ? pe + (size_t)((row / pe_div) % pe_mod) * C : nullptr;
 #pragma unroll
@@ -505,8 +505,8 @@ __global__ __launch_bounds__(256) void layernorm_g_kernel(const bf16_t* __restri
       float o[8];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        o[e] = (v[it][i][e] - mean) * (rstd * g0[e]) + b0[e];
-        o[e + 4] = (v[it][i][e + 4] - mean) * (rstd * g1[e]) + b1[e];
+        o[e] = fmaf(v[it][i][e] - mean, rstd * g0[e], b0[e]);
+        o[e + 4] = fmaf(v[it][i][e + 4] - mean, rstd * g1[e], b1[e]);
       }
       if (pr) {
         const f32x4 p0 = *reinterpret_cast<const f32x4*>(pr + c0), p1 = *reinterpret_cast<const f32x4*>(pr + c0 + 4);
@@ -515,91 +515,6 @@ __global__ __launch_bounds__(256) void layernorm_g_kernel(const bf16_t* __restri
       }
       *reinterpret_cast<u32x4*>(y + (size_t)row * ldy + c0) = pack8(o);
     }
-  }
-}
-
-// LayerNorm as a row stream (same lane layout and the same arithmetic, in the same order, as layernorm_g_kernel:
-// identical bits): a grid of a few waves per SIMD, each wave walking row passes gw, gw + GW, ... with the next pass's
-// 16-B loads in flight while the current one is reduced, normalised and stored, so reads and writes of neighbouring
-// passes overlap instead of every wave loading, then every wave storing; gamma / beta of the lane's channel chunks are
-// loaded once per wave, not once per row (they were 2x the row's own bytes of L1 traffic).
-template <int LPR>
-__global__ __launch_bounds__(256) void layernorm_r_kernel(const bf16_t* __restrict__ x, int ldx, int C, int rows,
-                                                          const float* __restrict__ gamma,
-                                                          const float* __restrict__ beta, float eps,
-                                                          const float* __restrict__ pe, int pe_div, int pe_mod,
-                                                          bf16_t* __restrict__ y, int ldy) {
-  constexpr int CPL = 5, RPW = 64 / LPR;
-  const int lane = threadIdx.x & 63, l = lane % LPR, rsub = lane / LPR;
-  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), GW = gridDim.x * 4;
-  const int npass = (rows + RPW - 1) / RPW;
-  if (gw >= npass) return;
-  f32x4 g[CPL][2], b[CPL][2];
-#pragma unroll
-  for (int i = 0; i < CPL; ++i) {
-    const int c0 = (l + LPR * i) * 8;
-    g[i][0] = *reinterpret_cast<const f32x4*>(gamma + c0);
-    g[i][1] = *reinterpret_cast<const f32x4*>(gamma + c0 + 4);
-    b[i][0] = *reinterpret_cast<const f32x4*>(beta + c0);
-    b[i][1] = *reinterpret_cast<const f32x4*>(beta + c0 + 4);
-  }
-  const float invc = 1.0f / (float)C;
-  auto load = [&](int ps, u32x4 (&raw)[CPL]) {
-    const int row = ps * RPW + rsub;
-#pragma unroll
-    for (int i = 0; i < CPL; ++i) {
-      raw[i] = u32x4{0u, 0u, 0u, 0u};
-      if (ps < npass && row < rows) raw[i] = *reinterpret_cast<const u32x4*>(x + (size_t)row * ldx + (l + LPR * i) * 8);
-    }
-  };
-  auto finish = [&](int ps, const u32x4 (&raw)[CPL]) {
-    const int row = ps * RPW + rsub;
-    float v[CPL][8];
-#pragma unroll
-    for (int i = 0; i < CPL; ++i) unpack8(raw[i], v[i]);
-    float sum = 0.f;
-#pragma unroll
-    for (int i = 0; i < CPL; ++i)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) sum += v[i][e];
-#pragma unroll
-    for (int o = LPR / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
-    const float mean = sum * invc;
-    float sq = 0.f;
-#pragma unroll
-    for (int i = 0; i < CPL; ++i)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { const float d = v[i][e] - mean; sq += d * d; }
-#pragma unroll
-    for (int o = LPR / 2; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
-    const float rstd = rsqrtf(sq * invc + eps);
-    if (row >= rows) return;
-    const float* pr = pe ? pe + (size_t)((row / pe_div) % pe_mod) * C : nullptr;
-#pragma unroll
-    for (int i = 0; i < CPL; ++i) {
-      const int c0 = (l + LPR * i) * 8;
-      float o[8];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        o[e] = (v[i][e] - mean) * (rstd * g[i][0][e]) + b[i][0][e];
-        o[e + 4] = (v[i][e + 4] - mean) * (rstd * g[i][1][e]) + b[i][1][e];
-      }
-      if (pr) {
-        const f32x4 p0 = *reinterpret_cast<const f32x4*>(pr + c0), p1 = *reinterpret_cast<const f32x4*>(pr + c0 + 4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { o[e] += p0[e]; o[e + 4] += p1[e]; }
-      }
-      *reinterpret_cast<u32x4*>(y + (size_t)row * ldy + c0) = pack8(o);
-    }
-  };
-  u32x4 ra[CPL], rb[CPL];
-  load(gw, ra);
-  for (int ps = gw; ps < npass; ps += 2 * GW) {  // two passes per trip: the register buffers are never indexed
-    load(ps + GW, rb);
-    finish(ps, ra);
-    if (ps + GW >= npass) break;
-    load(ps + 2 * GW, ra);
-    finish(ps + GW, rb);
   }
 }
 
@@ -984,35 +899,6 @@ extern "C" int vst_groupnorm_apply_partials(const void* x1, int ld1, int C1, int
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 
-// LayerNorm as a row stream (layernorm_r_kernel, default; VST_LN_STREAM=0 or vst_layernorm_stream(0): the one-pass-
-// per-wave layernorm_g_kernel, same bits); VST_LN_WPC = waves per CU of the stream's grid (default 8)
-static int g_ln_stream = -1;
-static bool ln_stream_on() {
-  if (g_ln_stream < 0) {
-    const char* e = getenv("VST_LN_STREAM");
-    g_ln_stream = e ? atoi(e) : 1;
-  }
-  return g_ln_stream != 0;
-}
-static int ln_stream_blocks(int npass) {
-  static const int cap = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-    const char* e = getenv("VST_LN_WPC");
-    const int wpc = e ? std::max(4, atoi(e)) : 8;
-    return n * wpc / 4;
-  }();
-  return std::max(1, std::min((npass + 3) / 4, cap));
-}
-
-extern "C" int vst_layernorm_stream(int on) {
-  const int prev = ln_stream_on() ? 1 : 0;
-  g_ln_stream = on ? 1 : 0;
-  return prev;
-}
-
 extern "C" int vst_layernorm(const void* x, int ldx, int C, int rows, const float* gamma, const float* beta,
                              float eps, const float* pe, int pe_div, int pe_mod, void* y, int ldy, void* stream) {
   if (!x || !y || !gamma || !beta || rows <= 0 || C <= 0 || C % 8 || (ldx & 7) || (ldy & 7)) return VST_ERR_ARG;
@@ -1040,18 +926,6 @@ extern "C" int vst_layernorm(const void* x, int ldx, int C, int rows, const floa
     else VST_LNG(LPR, 2);                                            \
     return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH; \
   }
-#define VST_LNR(LPR)                                                                                           \
-  {                                                                                                            \
-    hipLaunchKernelGGL((layernorm_r_kernel<LPR>), dim3(ln_stream_blocks((rows + 64 / LPR - 1) / (64 / LPR))), blk, 0, \
-                       s, (const bf16_t*)x, ldx, C, rows, gamma, beta, eps, pe, pe_div, pe_mod, (bf16_t*)y, ldy);   \
-    return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;                                          \
-  }
-  if (g16 && ln_stream_on()) {
-    if (C == 320) VST_LNR(8)
-    if (C == 640) VST_LNR(16)
-    if (C == 1280) VST_LNR(32)
-  }
-#undef VST_LNR
   if (g16 && C == 320) VST_LNG_RIT(8, 2)
   if (g16 && C == 640) VST_LNG_RIT(16, 2)
   if (g16 && C == 1280) VST_LNG_RIT(32, 1)

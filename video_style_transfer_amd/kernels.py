@@ -201,21 +201,6 @@ class p8_persist:
         _lib.load().vst_p8_persist(self.prev)
 
 
-class layernorm_stream:
-    """Context manager switching LayerNorm's row-stream kernel on / off (vst_layernorm_stream); tests and A/B runs
-    only (same bits either way)."""
-
-    def __init__(self, on=True):
-        self.on = int(bool(on))
-
-    def __enter__(self):
-        self.prev = int(_lib.load().vst_layernorm_stream(self.on))
-        return self
-
-    def __exit__(self, *a):
-        _lib.load().vst_layernorm_stream(self.prev)
-
-
 class p8_tile_width:
     """Context manager forcing the 8-phase GEMM's tile width (256 / 192 / 320 where legal; 0 = the library's
     policy) for the GEMMs launched inside it (vst_p8_force_bn); tests and A/B runs only."""
