@@ -69,6 +69,20 @@ int vst_p8_conv(int on);
  * setting.  Same bits. */
 int vst_p8_persist(int on);
 
+/* The motion-module attention's q/k/v projection and its frame-axis self-attention as ONE launch:
+ *   O[(c, f, p), 40h .. 40h+39] = softmax(q_h[c,.,p] k_h[c,.,p]^T * scale) v_h[c,.,p]  over the 16 frames of pixel p,
+ *   [q | k | v] = x . W^T (+ bias) rounded to bf16,
+ * x: [nclip * 16 * HW, K] rows (clip, frame, pixel); Wt: the q/k/v weight rows laid out per group of 256 / (3 d)
+ * heads (two of 40: [q_2t k_2t v_2t q_2t+1 k_2t+1 v_2t+1]; one of 80: [q_t k_t v_t]) + zero rows up to 256, i.e.
+ * [heads / hpt * 256, K] (bias alike, fp32 or NULL).  q/k/v never reach HBM.  Replaces to_q/to_k/to_v +
+ * F.scaled_dot_product_attention of the motion modules' AttnProcessor2_0 (diffusers AnimateDiffTransformer3D;
+ * animatediff/temporal_transformer.py:40-71) for head_dim 40 / 80 and 16 frames (the 64^2 and 32^2 levels of
+ * configs[2]); returns 3 (VST_ERR_UNSUPPORTED) otherwise, _supported answers without a launch. */
+int vst_gemm_temporal_attention(const void* x, int ldx, const void* Wt, int ldw, const float* bias, int M, int K,
+                                int nclip, int F, int HW, int heads, int head_dim, float scale, void* O, int ldo,
+                                void* stream);
+int vst_gemm_temporal_attention_supported(int M, int K, int nclip, int F, int HW, int heads, int head_dim);
+
 /* attn2 of a BasicTransformerBlock as ONE launch: the q projection (vst_gemm_lora when Acat != NULL, else
  * [x].[W]^T) with the cross-attention over the text tokens as its epilogue,
  *   O[m, 64h .. 64h+63] = softmax(q_h K_h^T * scale) V_h,  q = bf16(x.W^T (+bias) (+LoRA)),

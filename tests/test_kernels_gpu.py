@@ -156,7 +156,7 @@ def test_gemm_8phase_128x320_vs_torch(cuda, K, M, N, K1, K2, act):
     r = None if act else rnd(M, N, gen=g).to(cuda)
     K.GEMM_POLICY.update(tile=10, splits=1)
     try:
-        assert K.gemm_kernel_name(M, N, K1 + K2, 0) == "gemm_p8<128x320>"
+        assert K.gemm_kernel_name(M, N, K1 + K2, 0).startswith("gemm_p8<128x320")
         out = K.linear(x, w, b, x2=x2, residual=r, act=act)
     finally:
         K.GEMM_POLICY.update(tile=0, splits=0)
@@ -450,6 +450,49 @@ def test_temporal_attention(cuda, K, nclip, Fr, HW, C, qs):
     o = torch.softmax(q @ k.transpose(-1, -2) / math.sqrt(d), -1) @ v
     ref = o.view(nclip, HW, heads, Fr, d).permute(0, 3, 1, 2, 4).reshape(nclip * Fr * HW, C)
     check(out, ref, name="temporal")
+
+
+@pytest.mark.parametrize("nclip,HW,d,bias,ws", [(2, 4096, 40, False, 1.0), (1, 256, 40, True, 1.0),
+                                             (2, 512, 40, True, 3.0), (3, 1024, 40, False, 2.0),
+                                             (2, 1024, 80, False, 1.0), (1, 512, 80, True, 3.0)])
+def test_gemm_temporal_attention(cuda, K, nclip, HW, d, bias, ws):
+    """The motion modules' q/k/v projection with the frame-axis attention as its epilogue (vst_gemm_temporal_attention,
+    16 frames, 8 heads of 40 (K = 320, the 64^2 level) or 80 (K = 640, 32^2)) against the two-launch path (q/k/v GEMM
+    + vst_temporal_attention) and against fp32 torch on the bf16-rounded q/k/v; ws scales the weights (ws = 3: logit
+    std ~3, a peaked softmax)."""
+    g = torch.Generator().manual_seed(nclip * HW + int(ws) + d)
+    Fr, heads = 16, 8
+    C = heads * d
+    M = nclip * Fr * HW
+    x = rnd(M, C, gen=g)
+    w = rnd(3 * C, C, scale=ws * C ** -0.5, gen=g)
+    b = (torch.randn(3 * C, generator=g) * 0.1) if bias else None
+    xd, wd, bd = x.to(cuda), w.to(cuda), None if b is None else b.to(cuda)
+    assert K.temporal_attention_fusable(M, C, nclip, Fr, HW, heads, d)
+    w_t, b_t = K.temporal_qkv_layout(wd, None if bd is None else bd.float(), heads, d)
+    fused = K.linear_temporal_attention(xd, w_t, b_t, nclip=nclip, F=Fr, HW=HW, heads=heads, head_dim=d,
+                                        scale=d ** -0.5)
+    qkv = K.linear(xd, wd, bd)
+    two = K.temporal_attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], nclip, Fr, HW, heads, d)
+    check(fused, two.float(), rel_l2=2e-3, rel_max=1e-2, name="tattn fused vs two launches")
+    qf = (x.float() @ w.float().t() + (0 if b is None else b)).to(torch.bfloat16).float()
+
+    def seq(t):  # rows (b*F+f)*HW+p -> (b*HW+p, heads, F, d)
+        return t.view(nclip, Fr, HW, heads, d).permute(0, 2, 3, 1, 4).reshape(nclip * HW, heads, Fr, d)
+
+    q, k, v = seq(qf[:, :C]), seq(qf[:, C:2 * C]), seq(qf[:, 2 * C:])
+    o = torch.softmax(q @ k.transpose(-1, -2) / math.sqrt(d), -1) @ v
+    ref = o.view(nclip, HW, heads, Fr, d).permute(0, 3, 1, 2, 4).reshape(M, C)
+    check(fused, ref, name="tattn fused vs fp32")
+
+
+def test_gemm_temporal_attention_refuses(cuda, K):
+    """Outside the fused kernel's contract the policy says no (the processor then takes the two launches)."""
+    assert not K.temporal_attention_fusable(2 * 16 * 4096, 320, 2, 32, 4096, 8, 40)   # 32 frames
+    assert not K.temporal_attention_fusable(2 * 16 * 256, 1280, 2, 16, 256, 8, 160)   # heads of 160 (16^2)
+    assert not K.temporal_attention_fusable(2 * 16 * 100, 320, 2, 16, 100, 8, 40)     # HW % 16
+    assert K.temporal_attention_fusable(2 * 16 * 4096, 320, 2, 16, 4096, 8, 40)       # the 64^2 level
+    assert K.temporal_attention_fusable(2 * 16 * 1024, 640, 2, 16, 1024, 8, 80)       # the 32^2 level
 
 
 @pytest.mark.parametrize("ns,rps,C1,C2,silu", [(4, 64, 320, 0, True), (2, 1000, 640, 0, False),

@@ -34,7 +34,7 @@ def bench_symbol(name: str) -> str:
     if m:
         epi, bn, lora, bm, conv, persist = m.groups()
         tags = ((",lora" if lora == "true" else "") + (",conv" if conv == "true" else "") +
-                (",geglu" if epi == "1" else "") + (",xattn" if epi == "4" else "") +
+                (",geglu" if epi == "1" else "") + (",xattn" if epi == "4" else "") + (",tattn" if epi == "5" else "") +
                 (",persist" if persist == "true" else ""))
         return f"gemm_p8<{bm}x{bn}{tags}>"
     if "layernorm_lora_kernel" in name:

@@ -27,6 +27,8 @@ SIGNATURES = {
     "vst_gemm_cross_attention": (_I, [_P, _I, _P, _I, _I, _I, _I, _P, _I, _P, _I, _I, _I, _P, _P, _I, _I, _I, _I, _I,
                                       _F, _P, _I, _P]),
     "vst_gemm_cross_attention_supported": (_I, [_I, _I, _I, _I, _I, _I, _I, _I, _I]),
+    "vst_gemm_temporal_attention": (_I, [_P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _F, _P, _I, _P]),
+    "vst_gemm_temporal_attention_supported": (_I, [_I, _I, _I, _I, _I, _I, _I]),
     "vst_gemm_kernel_name": (ctypes.c_char_p, [_I, _I, _I, _I, _I, _I, _S]),
     "vst_conv3x3": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P, _I, _P, _I, _P]),
     "vst_conv3x3_ex": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _I, _P, _I, _P, _I, _I, _I, _P,

@@ -20,6 +20,7 @@ input is taken as (batch, seq=F, C), the diffusers layout).
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -182,6 +183,22 @@ def _generic_attention(qkv, batch, heads, N):
     raise NotImplementedError("spatial self-attention kernel is specialised for head_dim 64 (SDXL)")
 
 
+def _tattn_enabled() -> bool:
+    """VST_TATTN=0 keeps the motion attention as q/k/v GEMM + vst_temporal_attention (A/B)."""
+    return os.environ.get("VST_TATTN", "1") != "0"
+
+
+def _tattn_operands(attn, ops, heads, head_dim):
+    """The fused q/k/v weight re-laid out per pair of heads for vst_gemm_temporal_attention, cached on the module
+    against the fused operand it was made from (build_ops caches that one per parameter version; trained weights get
+    a fresh operand, hence a fresh layout, every call)."""
+    c = attn.__dict__.get("_vst_tattn")
+    if c is None or c[0] is not ops:
+        c = (ops,) + K.temporal_qkv_layout(ops.w, ops.bias, heads, head_dim)
+        attn.__dict__["_vst_tattn"] = c
+    return c[1], c[2]
+
+
 class AttnProcessor2_0:
     """Default (motion-module) processor: self-attention along the frame axis."""
 
@@ -197,10 +214,19 @@ class AttnProcessor2_0:
             nclip, Fr, HW = batch, N, 1
         heads = attn.heads
         inner = attn.to_q.out_features
+        D = inner // heads
         x = hidden_states.reshape(batch * N, C)
-        qkv = run_ops(x, build_ops([attn.to_q, attn.to_k, attn.to_v], 1.0))
-        o = K.temporal_attention(qkv[:, :inner], qkv[:, inner:2 * inner], qkv[:, 2 * inner:], nclip, Fr, HW, heads,
-                                 inner // heads)
+        ops = build_ops([attn.to_q, attn.to_k, attn.to_v], 1.0)
+        if num_frames is not None and _tattn_enabled() and ops.a is None and ops.w.shape[1] == C and \
+                K.temporal_attention_fusable(batch * N, C, nclip, Fr, HW, heads, D):
+            # q/k/v projection + frame attention in one launch (vst_gemm_temporal_attention; 16 frames, heads of 40)
+            w_t, b_t = _tattn_operands(attn, ops, heads, D)
+            o = K.linear_temporal_attention(x, w_t, b_t, nclip=nclip, F=Fr, HW=HW, heads=heads, head_dim=D,
+                                            scale=D ** -0.5)
+        else:
+            qkv = run_ops(x, ops)
+            o = K.temporal_attention(qkv[:, :inner], qkv[:, inner:2 * inner], qkv[:, 2 * inner:], nclip, Fr, HW,
+                                     heads, D)
         res2d = None if fused_residual is None else fused_residual.reshape(batch * N, -1)
         out = run_ops(o, build_ops([attn.to_out[0]], 1.0), residual=res2d).view(batch, N, -1)
         return _finish(attn, out, hidden_states)

@@ -635,6 +635,7 @@ static void choose(int M, int N, int K, int geglu, int conv, size_t ws_bytes, in
 int launch_gemm_ring(const GemmArgs& a, int amode, int epi, int tile, int splits, hipStream_t s);
 int launch_gemm_p8(const GemmArgs& a, int epi, int bn, hipStream_t s);
 bool p8_persist_applies(int M, int N, int K, int epi, int bn);
+int launch_gemm_p8_tattn(const GemmArgs& a, hipStream_t s);
 int launch_gemm_p8_lora(const GemmArgs& a, int bn, hipStream_t s);
 int launch_gemm_p8_xattn(const GemmArgs& a, hipStream_t s);
 int launch_gemm_p8_conv(const GemmArgs& a, int bn, hipStream_t s);
@@ -949,6 +950,40 @@ extern "C" int vst_gemm_cross_attention(const void* x, int ldx, const void* Acat
   a.xa_kv_bytes = clamp_bytes(((size_t)(nkv_rows - 1) * ldkv + N) * 2);
   a.stride = 1; a.splits = 1; a.p8_bn = 192;
   return launch_gemm_p8_xattn(a, (hipStream_t)stream);
+}
+
+// The motion modules' q/k/v projection + frame-axis attention in one launch (EPI 5 of the 8-phase kernel): 16 frames
+// per clip, heads of 40 (two per 256-column tile: an even head count) or 80 (one per tile), pixels per frame a
+// multiple of 16.
+static int tattn_hpt(int head_dim) { return head_dim == 40 ? 2 : head_dim == 80 ? 1 : 0; }
+static bool tattn_ok(int M, int K, int nclip, int F, int HW, int heads, int head_dim) {
+  const int hpt = tattn_hpt(head_dim);
+  if (!hpt || F != 16 || heads <= 0 || heads % hpt || HW <= 0 || (HW & 15) || nclip <= 0) return false;
+  // (shape-only, like the other fused paths: a frame-sharded rank decides as the unsharded forward does)
+  return (long)M == (long)nclip * F * HW && !(K & 63) && K >= 128 && gemm_p8_env() != 0;
+}
+
+extern "C" int vst_gemm_temporal_attention_supported(int M, int K, int nclip, int F, int HW, int heads,
+                                                     int head_dim) {
+  return tattn_ok(M, K, nclip, F, HW, heads, head_dim) ? 1 : 0;
+}
+
+extern "C" int vst_gemm_temporal_attention(const void* x, int ldx, const void* Wt, int ldw, const float* bias, int M,
+                                           int K, int nclip, int F, int HW, int heads, int head_dim, float scale,
+                                           void* O, int ldo, void* stream) {
+  if (!x || !Wt || !O || M <= 0 || K <= 0) return VST_ERR_ARG;
+  if ((ldx & 7) || (ldw & 7) || (ldo & 7) || ldx < K || ldw < K || ldo < heads * head_dim) return VST_ERR_ARG;
+  if (!tattn_ok(M, K, nclip, F, HW, heads, head_dim)) return VST_ERR_UNSUPPORTED;
+  const int N = heads / tattn_hpt(head_dim) * 256;
+  GemmArgs a{};
+  a.A1 = (const bf16_t*)x; a.lda1 = ldx; a.K1 = K;
+  a.Wt = (const bf16_t*)Wt; a.ldw = ldw; a.M = M; a.N = N; a.K = K;
+  a.bias = bias; a.C = (bf16_t*)O; a.ldc = ldo;
+  a.a1_bytes = clamp_bytes(((size_t)(M - 1) * ldx + K) * 2);
+  a.w_bytes = clamp_bytes(((size_t)(N - 1) * ldw + K) * 2);
+  a.ta_hw = HW; a.ta_heads = heads; a.ta_d = head_dim; a.ta_scale_log2 = scale * 1.4426950408889634f;
+  a.stride = 1; a.splits = 1; a.p8_bn = 256;
+  return launch_gemm_p8_tattn(a, (hipStream_t)stream);
 }
 
 // Name of the kernel a vst_gemm_ex / vst_conv3x3_ex call with these arguments launches (the

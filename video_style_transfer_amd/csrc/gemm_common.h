@@ -38,6 +38,11 @@ struct GemmArgs {
   int xa_ldkv, xa_nk, xa_nq, xa_kvdiv;
   float xa_scale_log2;
   uint32_t xa_kv_bytes;
+  // temporal attention epilogue (gemm_p8.hip EPI 5, vst_gemm_temporal_attention): frames per clip 16, head dim ta_d
+  // (40: two heads per 256-column tile, 80: one); ta_hw pixels per frame; the output O [M, ta_heads * ta_d]
+  // (p.C / p.ldc) is written in (clip, frame, pixel) rows
+  int ta_hw, ta_heads, ta_d;
+  float ta_scale_log2;
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) {

@@ -60,15 +60,20 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, char* smem, con
     for (int i = 0; i < Cfg::MI; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        float o[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float h = bf2f(f2bf(acc[i][j][e])), g = bf2f(f2bf(acc[i][j + 2][e]));
-          o[e] = h * gelu_erf(g);
-        }
         u32x2 v;
-        v[0] = pack2bf(o[0], o[1]);
-        v[1] = pack2bf(o[2], o[3]);
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const uint32_t hp = pack2bf(acc[i][j][2 * e], acc[i][j][2 * e + 1]);
+          const uint32_t gp = pack2bf(acc[i][j + 2][2 * e], acc[i][j + 2][2 * e + 1]);
+          const f32x2 h = {__uint_as_float(hp << 16), __uint_as_float(hp & 0xffff0000u)};
+          const f32x2 g = {__uint_as_float(gp << 16), __uint_as_float(gp & 0xffff0000u)};
+#ifdef VST_ABL_NOGELU  // diagnostics build only (tools/p8_epi_ablate.sh): the GELU's VALU cost
+          const f32x2 o = h * g;
+#else
+          const f32x2 o = geglu2(h, g);
+#endif
+          v[e] = pack2bf(o.x, o.y);
+        }
         *reinterpret_cast<u32x2*>(smem + (lrow0 + i * 16) * OROW + (wc * 32 + j * 16 + 4 * fq) * 2) = v;
       }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

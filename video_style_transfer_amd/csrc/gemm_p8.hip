@@ -346,13 +346,20 @@ __device__ __forceinline__ void p8_epilogue_passes(const GemmArgs& p, char* R, c
       if constexpr (EPI == 1) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          float o[4];
+          u32x2 v;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float h = bf2f(f2bf(acc[i][j][e])), g = bf2f(f2bf(acc[i][j + 2][e]));
-            o[e] = h * gelu_erf(g);
+          for (int e = 0; e < 2; ++e) {  // the projection output rounded to bf16 first (the reference's tensor)
+            const uint32_t hp = pack2bf(acc[i][j][2 * e], acc[i][j][2 * e + 1]);
+            const uint32_t gp = pack2bf(acc[i][j + 2][2 * e], acc[i][j + 2][2 * e + 1]);
+            const f32x2 h = {__uint_as_float(hp << 16), __uint_as_float(hp & 0xffff0000u)};
+            const f32x2 g = {__uint_as_float(gp << 16), __uint_as_float(gp & 0xffff0000u)};
+#ifdef VST_ABL_NOGELU  // diagnostics build only (tools/p8_epi_ablate.sh): the GELU's VALU cost
+            const f32x2 o = h * g;
+#else
+            const f32x2 o = geglu2(h, g);
+#endif
+            v[e] = pack2bf(o.x, o.y);
           }
-          const u32x2 v{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
           *reinterpret_cast<u32x2*>(R + swz(lr, (wc * 32 + j * 16 + 4 * fq) * 2)) = v;
         }
       } else {
@@ -400,6 +407,94 @@ __device__ __forceinline__ void p8_epilogue_passes(const GemmArgs& p, char* R, c
   }
 }
 
+// EPI 5: the motion modules' frame-axis self-attention as the epilogue of their fused q/k/v projection (AttnProcessor2_0
+// on the AnimateDiffTransformer3D blocks: to_q / to_k / to_v, then F.scaled_dot_product_attention over the frames of
+// every pixel; animatediff/temporal_transformer.py:40-71 restates the same attention).  The GEMM takes its rows in
+// (clip, 16-pixel group, pixel, frame) order (setup_tile's row map), so a 256-row tile holds all 16 frames of 16
+// pixels, and the host lays the weight rows out so a 256-column tile is [q k v] of 256 / (3 d) heads (two of 40 or
+// one of 80; zero rows pad to 256).  (acc + bias) is rounded to bf16 into LDS (the projections' rounding point), then
+// the waves compute the tile's (pixel, head) units on MFMA in temporal_attn_kernel's arithmetic: S^T = K Q^T (32-deep
+// steps, d >= head_dim zeroed), softmax over the 16 keys (exp2, P rounded to bf16 unnormalised, 1/l at the end),
+// O^T = V^T P^T (16x16x16 steps over 16-wide d blocks).  q / k / v never reach HBM: their write and the separate
+// attention launch's read (2 x 252 MB per motion block at the 64^2 level of 16x512^2) are gone.
+template <class Cfg>
+__device__ __forceinline__ void tattn_epilogue(const GemmArgs& p, char* smem, const int m0, const int n0,
+                                               f32x4 (&acc)[Cfg::MI][Cfg::NJ], const int wr, const int wc) {
+  constexpr int LROW = Cfg::BN * 2 + 16, TF = 16;
+  static_assert(Cfg::BM == 256 && Cfg::BN == 256 && Cfg::BM * LROW <= 160 * 1024, "256x256 tiles");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, g = lane >> 4;
+  {
+    const int lrow0 = wr * Cfg::WM + fr, lcol0 = wc * Cfg::WN + 4 * g;
+#pragma unroll
+    for (int j = 0; j < Cfg::NJ; ++j) {
+      f32x4 b4 = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (p.bias) {
+        const int n = n0 + lcol0 + j * 16;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) b4[e] = n + e < p.N ? p.bias[n + e] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < Cfg::MI; ++i) {
+        const f32x4 a4 = acc[i][j] + b4;
+        const u32x2 v{pack2bf(a4[0], a4[1]), pack2bf(a4[2], a4[3])};
+        *reinterpret_cast<u32x2*>(smem + (lrow0 + i * 16) * LROW + (lcol0 + j * 16) * 2) = v;
+      }
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int TD = p.ta_d, HPT = 256 / (3 * TD), KS = (TD + 31) / 32, DB = (TD + 15) / 16;
+  const int ngrp = p.ta_hw / 16, mt = m0 / 256;
+  const int b = mt / ngrp, pg = mt - b * ngrp;
+  const float sl2 = p.ta_scale_log2;
+  for (int u = wid; u < 16 * HPT; u += 8) {
+    const int pl = u / HPT, hh = u - pl * HPT, h = (n0 / 256) * HPT + hh;
+    if (h >= p.ta_heads) continue;  // (wave-uniform)
+    const char* R = smem + pl * TF * LROW;  // the 16 frame rows of pixel pl
+    const int cq = hh * 3 * TD, ck = cq + TD, cv = cq + 2 * TD;
+    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};  // S^T: lane (query fr) holds keys 4g + i
+    for (int kk = 0; kk < KS; ++kk) {
+      const int d0 = kk * 32 + g * 8;
+      bf16x8 kf = bf16x8{}, qf = bf16x8{};
+      if (d0 < TD) {
+        kf = *reinterpret_cast<const bf16x8*>(R + fr * LROW + (ck + d0) * 2);
+        qf = *reinterpret_cast<const bf16x8*>(R + fr * LROW + (cq + d0) * 2);
+      }
+      s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf, s, 0, 0, 0);
+    }
+    float mx = fmaxf(fmaxf(s[0], s[1]), fmaxf(s[2], s[3]));
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float mb = mx * sl2;
+    float ls = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      s[i] = fast_exp2(s[i] * sl2 - mb);
+      ls += s[i];
+    }
+    ls += __shfl_xor(ls, 16);
+    ls += __shfl_xor(ls, 32);
+    const float inv = 1.0f / ls;
+    const u32x2 pw{pack2bf(s[0], s[1]), pack2bf(s[2], s[3])};
+    const s16x4 pb = __builtin_bit_cast(s16x4, pw);  // B = P^T: keys 4g .. 4g+3 of query fr
+    bf16_t* orow = p.C + (size_t)((b * TF + fr) * p.ta_hw + pg * 16 + pl) * p.ldc + h * TD;
+    for (int db = 0; db < DB; ++db) {
+      const int d = db * 16 + fr;  // A = V^T: row d, keys 4g .. 4g+3
+      s16x4 va = s16x4{0, 0, 0, 0};
+      if (d < TD) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) va[i] = *reinterpret_cast<const short*>(R + (4 * g + i) * LROW + (cv + d) * 2);
+      }
+      const f32x4 o = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(va, pb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0) * inv;
+      // o[i] = O^T[d = 16 db + 4g + i][query fr]
+      if (db * 16 + 4 * g < TD)
+        *reinterpret_cast<u32x2*>(orow + db * 16 + 4 * g) = u32x2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
+    }
+  }
+}
+
 // LORA (vst_gemm_lora, UnZipLoRA / LoRA projections): the down-projection u = x . Acat^T is accumulated inside the
 // k-loop from the A fragments already in registers, so no separate pass over x produces it.  Each k-tile also
 // stages Acat's 16 u columns of this tile ([16][64] bf16, one extra DMA per wave issued with slot Amq0: waves 0-1
@@ -420,7 +515,8 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   static_assert(!CONV || (!LORA && EPI == 0), "conv: plain epilogue");
   static_assert(EPI != 1 || BN == 256, "GEGLU needs 64-column [hidden | gate] blocks");
   static_assert(!LORA || EPI != 1, "in-GEMM LoRA: linear epilogue");
-  static_assert(!PERSIST || (!LORA && !CONV && EPI != 4 && PH == 2), "persistent tiles: plain / GEGLU / GELU, PH 2");
+  static_assert(!PERSIST || (!LORA && !CONV && EPI != 4 && EPI != 5 && PH == 2), "persistent tiles: plain / GEGLU / GELU, PH 2");
+  static_assert(EPI != 5 || (BN == 256 && BM == 256 && !LORA && !CONV), "temporal attention epilogue: 256x256 tiles");
   static_assert(EPI != 4 || (BN == 192 && BM == 256), "cross-attention epilogue: 256 x 192 tiles (3 heads)");
   constexpr int LX = LORA ? 1 : 0;  // the Acat DMA in the vmcnt counts
   constexpr int BUF = Cfg::BUF, RB1 = Cfg::RB1, NJ1 = Cfg::NJ1, NPB1 = Cfg::NPB1, NPA = Cfg::NPA;
@@ -500,8 +596,14 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
             }
             base1[s][pc] = base2[s][pc] = (uint32_t)kOOB;
           } else {
-            base1[s][pc] = m < p.M ? (uint32_t)(m * p.lda1 + c * 8) * 2u : (uint32_t)kOOB;
-            base2[s][pc] = m < p.M ? (uint32_t)(m * p.lda2 + c * 8) * 2u : (uint32_t)kOOB;
+            int src = m;
+            if constexpr (EPI == 5) {  // tile rows (pixel pl, frame f) of 16-pixel group mt -> x row (clip, frame, pixel)
+              const int ngrp = p.ta_hw >> 4, mt = m >> 8, r = m & 255;
+              const int bb = mt / ngrp, pgg = mt - bb * ngrp;
+              src = ((bb << 4) + (r & 15)) * p.ta_hw + (pgg << 4) + (r >> 4);
+            }
+            base1[s][pc] = m < p.M ? (uint32_t)(src * p.lda1 + c * 8) * 2u : (uint32_t)kOOB;
+            base2[s][pc] = m < p.M ? (uint32_t)(src * p.lda2 + c * 8) * 2u : (uint32_t)kOOB;
           }
         } else {
           const int rb = s == 2 ? 32 : RB1;
@@ -845,7 +947,17 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       has_next = jn < cnt;
       if (has_next) tile_origin(beg + jn, nm0, nn0);
       run_segment2(0, nk, first);
+#ifdef VST_ABL_NOEPI  // diagnostics build only: no epilogue (a guarded store of every accumulator's first lane
+                      // element keeps all the MFMAs live)
+      {
+        float sink = 0.f;
+        for (int i = 0; i < Cfg::MI; ++i)
+          for (int jj = 0; jj < Cfg::NJ; ++jj) sink += acc[i][jj][0];
+        if (sink == 1234.5f) p.C[0] = 0;
+      }
+#else
       p8_epilogue_passes<Cfg, EPI>(p, smem + Cfg::EPI_OFF, m0, n0, acc, wr, wc);
+#endif
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // stores done; the next tile's k-tiles landed
       p8_barrier();
       if (!has_next) return;
@@ -892,7 +1004,17 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     __builtin_amdgcn_s_barrier();  // every wave's u reads done before the epilogue stages the tile over them
   }
   if constexpr (EPI == 4) xattn_epilogue<Cfg>(p, smem, m0, n0, acc, wr, wc);
+  else if constexpr (EPI == 5) tattn_epilogue<Cfg>(p, smem, m0, n0, acc, wr, wc);
+#ifdef VST_ABL_NOEPI
+  else {
+    float sink = 0.f;
+    for (int i = 0; i < Cfg::MI; ++i)
+      for (int jj = 0; jj < Cfg::NJ; ++jj) sink += acc[i][jj][0];
+    if (sink == 1234.5f) p.C[0] = 0;
+  }
+#else
   else tile_epilogue<Cfg, EPI>(p, smem, m0, n0, acc, wr, wc);
+#endif
 #ifdef VST_P8_TRACE
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -979,7 +1101,7 @@ static int launch_p8_persist(const GemmArgs& a, hipStream_t s) {
 template <int EPI, int BN, bool LORA = false>
 static int launch_p8_epi(const GemmArgs& a, hipStream_t s) {
   constexpr int BM = BN == 320 ? 128 : 256;
-  if constexpr (!LORA && EPI != 4)
+  if constexpr (!LORA && EPI != 4 && EPI != 5)
     if (!a.A2 && p8_persist_applies(a.M, a.N, a.K, EPI, BN)) return launch_p8_persist<EPI, BN, BM>(a, s);
   return p8_ph_env() == 2 ? launch_p8_ph<EPI, BN, LORA, 2, BM>(a, s) : launch_p8_ph<EPI, BN, LORA, 3, BM>(a, s);
 }
@@ -989,6 +1111,12 @@ int launch_gemm_p8_lora(const GemmArgs& a, int bn, hipStream_t s) {
   if (!a.la) return VST_ERR_ARG;
   if (bn == 320) return launch_p8_epi<0, 320, true>(a, s);
   return bn == 192 ? launch_p8_epi<0, 192, true>(a, s) : launch_p8_epi<0, 256, true>(a, s);
+}
+
+// temporal attention epilogue (a.ta_hw set), 256x256 tiles
+int launch_gemm_p8_tattn(const GemmArgs& a, hipStream_t s) {
+  if (a.ta_hw <= 0 || (a.ta_hw & 15) || a.A2 || (a.M & 255)) return VST_ERR_ARG;
+  return launch_p8_epi<5, 256>(a, s);
 }
 
 // cross-attention epilogue (a.xa_k set), 256x192 tiles, with or without the in-GEMM LoRA

@@ -83,6 +83,27 @@ __device__ __forceinline__ float erf_fast(float x) {
 }
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
 
+// h * GELU(g) for two columns at once (the GEGLU GEMM epilogues), the same A&S 7.1.26 erf on packed fp32 (v_pk_*):
+//   0.5 g (1 + erf(g / sqrt2)) = 0.5 g + 0.5 |g| erf(|g| / sqrt2),  erf(z) = 1 - poly(t) exp(-z^2), t = 1 / (1 + p z)
+// (erf odd: no copysign); only |g|, the rcp and the exp2 are per element.  ~10 VALU per output instead of ~18 for
+// the scalar form, whose cost was ~12 % of the 16^2 GEGLU launch (tools/p8_epi_ablate.sh).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 geglu2(f32x2 h, f32x2 g) {
+  const f32x2 ag = {fabsf(g.x), fabsf(g.y)};
+  const f32x2 u = __builtin_elementwise_fma(ag, f32x2(0.3275911f * 0.70710678118654752f), f32x2(1.0f));
+  const f32x2 t = {__builtin_amdgcn_rcpf(u.x), __builtin_amdgcn_rcpf(u.y)};
+  f32x2 poly = __builtin_elementwise_fma(t, f32x2(1.061405429f), f32x2(-1.453152027f));
+  poly = __builtin_elementwise_fma(poly, t, f32x2(1.421413741f));
+  poly = __builtin_elementwise_fma(poly, t, f32x2(-0.284496736f));
+  poly = __builtin_elementwise_fma(poly, t, f32x2(0.254829592f));
+  poly = poly * t;
+  const f32x2 w = (g * g) * f32x2(-0.5f * 1.4426950408889634f);
+  const f32x2 e = {__builtin_amdgcn_exp2f(w.x), __builtin_amdgcn_exp2f(w.y)};
+  const f32x2 hag = ag * f32x2(0.5f);
+  const f32x2 y = __builtin_elementwise_fma(-(poly * e), hag, hag);  // 0.5 |g| erf(|g| / sqrt2)
+  return h * __builtin_elementwise_fma(g, f32x2(0.5f), y);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);

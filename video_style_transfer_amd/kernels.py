@@ -326,6 +326,70 @@ def linear_cross_attention(x: torch.Tensor, w: torch.Tensor, a: torch.Tensor | N
     return out
 
 
+_TATTN_OK = {}
+
+
+def temporal_attention_fusable(M: int, K: int, nclip: int, F: int, HW: int, heads: int, head_dim: int) -> bool:
+    """vst_gemm_temporal_attention_supported (host policy, cached): the motion modules' q/k/v + frame attention in one
+    launch (16 frames, heads of 40)."""
+    key = (M, K, nclip, F, HW, heads, head_dim)
+    ok = _TATTN_OK.get(key)
+    if ok is None:
+        ok = _TATTN_OK[key] = bool(_lib.load().vst_gemm_temporal_attention_supported(*key))
+    return ok
+
+
+def temporal_qkv_layout(w: torch.Tensor, b: torch.Tensor | None, heads: int, head_dim: int):
+    """The fused q/k/v weight [3C, K] (+ bias [3C]) re-laid out for vst_gemm_temporal_attention: per group of
+    hpt = 256 // (3 head_dim) heads (2 of 40, 1 of 80) [q k v of each head] then zero rows up to 256.
+    Returns (w_t bf16, b_t fp32)."""
+    C = heads * head_dim
+    hpt = 256 // (3 * head_dim)
+    if w.shape[0] != 3 * C or hpt == 0 or heads % hpt:
+        raise _lib.VstError(f"temporal_qkv_layout: w {tuple(w.shape)} heads={heads} head_dim={head_dim}")
+    d = torch.arange(head_dim, device=w.device)
+    rows, valid = [], []
+    for t in range(heads // hpt):
+        for h in range(hpt * t, hpt * t + hpt):
+            for part in range(3):
+                rows.append(part * C + h * head_dim + d)
+        pad = 256 - 3 * hpt * head_dim
+        rows.append(torch.zeros(pad, dtype=torch.long, device=w.device))
+        valid.append(torch.cat([torch.ones(3 * hpt * head_dim, device=w.device), torch.zeros(pad, device=w.device)]))
+    idx = torch.cat(rows)
+    keep = torch.cat(valid)
+    w_t = (w.detach().float()[idx] * keep[:, None]).to(BF16).contiguous()
+    b_t = None if b is None else (b.detach().float()[idx] * keep).contiguous()
+    return w_t, b_t
+
+
+def linear_temporal_attention(x: torch.Tensor, w_t: torch.Tensor, b_t: torch.Tensor | None, *, nclip: int, F: int,
+                              HW: int, heads: int, head_dim: int, scale: float,
+                              out: torch.Tensor | None = None) -> torch.Tensor:
+    """o = the motion modules' frame-axis attention of q/k/v = x w^T + b, in one launch (vst_gemm_temporal_attention);
+    x: [nclip*F*HW, K] rows (clip, frame, pixel), w_t / b_t from temporal_qkv_layout.  Returns [M, heads*head_dim]."""
+    _dev(x, BF16, "x")
+    _dev(w_t, BF16, "w_t")
+    M, K = x.shape
+    N = heads // (256 // (3 * head_dim)) * 256
+    if w_t.shape != (N, K):
+        raise _lib.VstError(f"linear_temporal_attention: w_t {tuple(w_t.shape)} != {(N, K)}")
+    if b_t is not None and (b_t.dtype != F32 or b_t.numel() != N or not b_t.is_cuda):
+        raise _lib.VstError("linear_temporal_attention: b_t must be fp32 [N] on device")
+    if not temporal_attention_fusable(M, K, nclip, F, HW, heads, head_dim):
+        raise _lib.VstError(f"linear_temporal_attention: M={M} K={K} F={F} HW={HW} heads={heads} not fusable")
+    C = heads * head_dim
+    if out is None:
+        out = torch.empty((M, C), dtype=BF16, device=x.device)
+    _dev(out, BF16, "out")
+    flops = 2.0 * M * 3 * C * K + 4.0 * M * F * C
+    nbytes = 2.0 * (M * K + 3 * C * K + M * C)
+    with _Rec("gemm_tattn", flops, nbytes, lambda: "gemm_p8<256x256,tattn>", (M, N, K)):
+        _lib.call("vst_gemm_temporal_attention", _p(x), _ld(x), _p(w_t), _ld(w_t), _p(b_t), M, K, nclip, F, HW, heads,
+                  head_dim, float(scale), _p(out), _ld(out), _stream())
+    return out
+
+
 def conv3x3(x1: torch.Tensor, nimg: int, H: int, W: int, w: torch.Tensor, bias: torch.Tensor | None, *,
             x2: torch.Tensor | None = None, stride: int = 1, upsample: bool = False,
             row_bias: torch.Tensor | None = None, row_bias_div: int = 1, residual: torch.Tensor | None = None,
