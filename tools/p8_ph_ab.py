@@ -86,7 +86,7 @@ def main():
         for ph in phs:
             env = dict(os.environ, VST_P8_PH=ph.split("+")[0], VST_PH_CHILD="1", VST_P8_320="1" if "+320" in ph else "0",
                        VST_P8_PERSIST="1" if "+persist" in ph else "0",
-                       VST_P8_STAGGER=next((f[2:] for f in ph.split("+") if f.startswith("st")), "0"))
+                       )
             r = subprocess.run([sys.executable, os.path.abspath(__file__)], env=env, capture_output=True, text=True,
                                timeout=300)
             if r.returncode:

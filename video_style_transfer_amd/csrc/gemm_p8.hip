@@ -292,10 +292,11 @@ __device__ __forceinline__ void xattn_epilogue(const GemmArgs& p, char* smem, co
   }
 }
 
-// PERSIST epilogue (EPI 0 bias / row bias / residual, 1 GEGLU, 3 bias + GELU): the same rounding points and stores as
-// tile_epilogue, staged through the EPI_REGION bytes past the ring in passes of 32 * IPP tile rows (IPP 16-row
-// accumulator blocks of both wave rows), so the ring's buffers keep the next tile's first k-tiles in flight.  Staged
-// rows are unpadded; 16-B chunk c of staged row r sits at chunk c ^ (r & 7) (every row holds a multiple of 8 chunks).
+// PERSIST epilogue (EPI 0 bias / row bias / residual, 1 GEGLU, 3 bias + GELU): the same rounding points as
+// tile_epilogue.  EPI 0 / 3 stage through the EPI_REGION bytes past the ring in passes of 32 * IPP tile rows (IPP
+// 16-row accumulator blocks of both wave rows), so the ring's buffers keep the next tile's first k-tiles in flight;
+// staged rows are unpadded, 16-B chunk c of staged row r at chunk c ^ (r & 7) (rows hold a multiple of 8 chunks).
+// GEGLU stores its half-width output straight from the accumulators.
 template <class Cfg, int EPI>
 __device__ __forceinline__ void p8_epilogue_passes(const GemmArgs& p, char* R, const int m0, const int n0,
                                                    f32x4 (&acc)[Cfg::MI][Cfg::NJ], const int wr, const int wc) {
@@ -328,6 +329,33 @@ __device__ __forceinline__ void p8_epilogue_passes(const GemmArgs& p, char* R, c
   }
   const auto rr = make_rsrc(p.R ? p.R : p.Wt, p.R ? p.r_bytes : 0u);
   const int nout = EPI == 1 ? p.N / 2 : p.N, c0 = EPI == 1 ? n0 / 2 : n0;
+  if constexpr (EPI == 1) {
+    // GEGLU: no staging -- each lane's 4 output columns (8 B) of its 16-row blocks go straight out (the 64-B row
+    // segments of a wave column merge in L2; staged through the LDS in passes measured 0.15 ms per step slower,
+    // profiles/r4_ab_geglu_direct.txt)
+    {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int m = m0 + wr * WM + i * 16 + fr;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          u32x2 v;
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const uint32_t hp = pack2bf(acc[i][j][2 * e], acc[i][j][2 * e + 1]);
+            const uint32_t gp = pack2bf(acc[i][j + 2][2 * e], acc[i][j + 2][2 * e + 1]);
+            const f32x2 h = {__uint_as_float(hp << 16), __uint_as_float(hp & 0xffff0000u)};
+            const f32x2 g = {__uint_as_float(gp << 16), __uint_as_float(gp & 0xffff0000u)};
+            const f32x2 o = geglu2(h, g);
+            v[e] = pack2bf(o.x, o.y);
+          }
+          const int n = c0 + wc * 32 + j * 16 + 4 * fq;
+          if (m < p.M && n < nout) *reinterpret_cast<u32x2*>(p.C + (size_t)m * p.ldc + n) = v;
+        }
+      }
+      return;
+    }
+  } else {
 #pragma unroll
   for (int q = 0; q < NPASS; ++q) {
     // residual chunks of this pass first: their latency overlaps the staging
@@ -343,26 +371,7 @@ __device__ __forceinline__ void p8_epilogue_passes(const GemmArgs& p, char* R, c
 #pragma unroll
     for (int ii = 0; ii < IPP; ++ii) {
       const int i = q * IPP + ii, lr = wr * 16 * IPP + ii * 16 + fr;
-      if constexpr (EPI == 1) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          u32x2 v;
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {  // the projection output rounded to bf16 first (the reference's tensor)
-            const uint32_t hp = pack2bf(acc[i][j][2 * e], acc[i][j][2 * e + 1]);
-            const uint32_t gp = pack2bf(acc[i][j + 2][2 * e], acc[i][j + 2][2 * e + 1]);
-            const f32x2 h = {__uint_as_float(hp << 16), __uint_as_float(hp & 0xffff0000u)};
-            const f32x2 g = {__uint_as_float(gp << 16), __uint_as_float(gp & 0xffff0000u)};
-#ifdef VST_ABL_NOGELU  // diagnostics build only (tools/p8_epi_ablate.sh): the GELU's VALU cost
-            const f32x2 o = h * g;
-#else
-            const f32x2 o = geglu2(h, g);
-#endif
-            v[e] = pack2bf(o.x, o.y);
-          }
-          *reinterpret_cast<u32x2*>(R + swz(lr, (wc * 32 + j * 16 + 4 * fq) * 2)) = v;
-        }
-      } else {
+      {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           f32x4 a4 = acc[i][j];
@@ -404,6 +413,7 @@ __device__ __forceinline__ void p8_epilogue_passes(const GemmArgs& p, char* R, c
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
     }
+  }
   }
 }
 
