@@ -461,9 +461,9 @@ __global__ __launch_bounds__(256) void layernorm_g_kernel(const bf16_t* __restri
                                                           const float* __restrict__ pe, int pe_div, int pe_mod,
                                                           bf16_t* __restrict__ y, int ldy) {
   constexpr int CPL = 5, RPW = 64 / LPR;
+  __shared__ f32x4 sgb[2][CPL * LPR * 2];  // gamma, beta of the row (C = 40 LPR floats = 10 LPR f32x4)
   const int lane = threadIdx.x & 63, l = lane % LPR, rsub = lane / LPR;
   const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW * RIT;
-  if (row0 >= rows) return;
   float v[RIT][CPL][8];
 #pragma unroll
   for (int it = 0; it < RIT; ++it) {
@@ -475,6 +475,14 @@ __global__ __launch_bounds__(256) void layernorm_g_kernel(const bf16_t* __restri
       unpack8(raw, v[it][i]);
     }
   }
+  // gamma / beta staged once per workgroup (every wave of it used to fetch the whole row's 10 LPR x 32 B through the
+  // vector memory path per row pass: 4x the row's own bytes)
+  for (int i = threadIdx.x; i < CPL * LPR * 2; i += 256) {
+    sgb[0][i] = reinterpret_cast<const f32x4*>(gamma)[i];
+    sgb[1][i] = reinterpret_cast<const f32x4*>(beta)[i];
+  }
+  __syncthreads();
+  if (row0 >= rows) return;
   const float invc = 1.0f / (float)C;
 #pragma unroll
   for (int it = 0; it < RIT; ++it) {
@@ -500,8 +508,8 @@ __global__ __launch_bounds__(256) void layernorm_g_kernel(const bf16_t* __restri
 #pragma unroll
     for (int i = 0; i < CPL; ++i) {
       const int c0 = (l + LPR * i) * 8;
-      const f32x4 g0 = *reinterpret_cast<const f32x4*>(gamma + c0), g1 = *reinterpret_cast<const f32x4*>(gamma + c0 + 4);
-      const f32x4 b0 = *reinterpret_cast<const f32x4*>(beta + c0), b1 = *reinterpret_cast<const f32x4*>(beta + c0 + 4);
+      const f32x4 g0 = sgb[0][c0 / 4], g1 = sgb[0][c0 / 4 + 1];
+      const f32x4 b0 = sgb[1][c0 / 4], b1 = sgb[1][c0 / 4 + 1];
       float o[8];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
