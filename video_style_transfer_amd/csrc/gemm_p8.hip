@@ -296,10 +296,22 @@ __device__ __forceinline__ void xattn_epilogue(const GemmArgs& p, char* smem, co
 // tile_epilogue.  EPI 0 / 3 stage through the EPI_REGION bytes past the ring in passes of 32 * IPP tile rows (IPP
 // 16-row accumulator blocks of both wave rows), so the ring's buffers keep the next tile's first k-tiles in flight;
 // staged rows are unpadded, 16-B chunk c of staged row r at chunk c ^ (r & 7) (rows hold a multiple of 8 chunks).
-// GEGLU stores its half-width output straight from the accumulators.
+// GEGLU stores its half-width output straight from the accumulators, as unconditional buffer stores (out-of-range
+// chunks get out-of-range offsets), so every wave issues exactly p8_epi_stores<Cfg, EPI>() of them.  pre() runs after
+// the bias add (the caller's next-tile DMAs, issued before any store).
 template <class Cfg, int EPI>
+constexpr int p8_epi_stores() {
+#ifdef VST_ABL_NOEPI
+  return 0;
+#else
+  return EPI == 1 ? 2 * Cfg::MI : 0;
+#endif
+}
+
+template <class Cfg, int EPI, class Pre>
 __device__ __forceinline__ void p8_epilogue_passes(const GemmArgs& p, char* R, const int m0, const int n0,
-                                                   f32x4 (&acc)[Cfg::MI][Cfg::NJ], const int wr, const int wc) {
+                                                   f32x4 (&acc)[Cfg::MI][Cfg::NJ], const int wr, const int wc,
+                                                   Pre&& pre) {
   constexpr int MI = Cfg::MI, NJ = Cfg::NJ, WM = Cfg::WM, THREADS = Cfg::THREADS;
   constexpr int OC = EPI == 1 ? Cfg::BN / 2 : Cfg::BN;  // output columns of the tile
   constexpr int ROWB = OC * 2, REGION = Cfg::EPI_REGION;
@@ -327,6 +339,7 @@ __device__ __forceinline__ void p8_epilogue_passes(const GemmArgs& p, char* R, c
       for (int i = 0; i < MI; ++i) acc[i][j] += b4;
     }
   }
+  pre();
   const auto rr = make_rsrc(p.R ? p.R : p.Wt, p.R ? p.r_bytes : 0u);
   const int nout = EPI == 1 ? p.N / 2 : p.N, c0 = EPI == 1 ? n0 / 2 : n0;
   if constexpr (EPI == 1) {
@@ -334,6 +347,7 @@ __device__ __forceinline__ void p8_epilogue_passes(const GemmArgs& p, char* R, c
     // segments of a wave column merge in L2; staged through the LDS in passes measured 0.15 ms per step slower,
     // profiles/r4_ab_geglu_direct.txt)
     {
+      const auto rc = make_rsrc(p.C, (uint32_t)((size_t)p.M * p.ldc * 2));  // (launch_p8_epi: < 2^31 bytes)
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const int m = m0 + wr * WM + i * 16 + fr;
@@ -350,7 +364,7 @@ __device__ __forceinline__ void p8_epilogue_passes(const GemmArgs& p, char* R, c
             v[e] = pack2bf(o.x, o.y);
           }
           const int n = c0 + wc * 32 + j * 16 + 4 * fq;
-          if (m < p.M && n < nout) *reinterpret_cast<u32x2*>(p.C + (size_t)m * p.ldc + n) = v;
+          __builtin_amdgcn_raw_buffer_store_b64(v, rc, m < p.M && n < nout ? (m * p.ldc + n) * 2 : kOOB, 0, 0);
         }
       }
       return;
@@ -869,7 +883,11 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
                    row2 < BN && n2 < p.N ? (int)(((uint32_t)n2 * p.ldw + p.K + ub0 + 8 * (lane & 1)) * 2u) : kOOB);
       }
     }
-    if (!PERSIST || first) {  // (PERSIST: later tiles' first k-tiles were issued by the previous tile and have landed)
+    // PERSIST, later tiles: k-tiles kb and kb + 1 were issued by the previous tile (B1 / A1 of kb + 1 just before its
+    // epilogue) and have landed (its post-epilogue wait), so J0(kb) issues nothing and the waits of J0(kb), J1(kb),
+    // J0(kb + 1) are skipped: the epilogue's stores, younger than those DMAs, stay in flight until J1(kb + 1)
+    const bool handed = PERSIST && !first;
+    if (!PERSIST || first) {
       dma_slot(0, kb, ke, kofs); dma_lora(kb, ke, true); dma_slot(2, kb, ke, kofs); dma_slot(3, kb, ke, kofs);
       dma_slot(1, kb, ke, kofs);
       dma_slot(0, kb + 1, ke, kofs); dma_lora(kb + 1, ke, true); dma_slot(2, kb + 1, ke, kofs);
@@ -896,9 +914,11 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       read_b(buf, 0, fb0);
       read_b(buf, 1, fb1);
       read_l(buf);
-      if (!(abl & 4)) p8_vmwait<NPA + 2 + LX>();  // A1(t) landed
-      dma(3, t + 1);
-      dma(1, t + 1);
+      if (!(abl & 4) && !(handed && t <= kb + 1)) p8_vmwait<NPA + 2 + LX>();  // A1(t) landed
+      if (!(handed && t == kb)) {
+        dma(3, t + 1);
+        dma(1, t + 1);
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       p8_barrier();
       lora_mfma(acc_u[0], 0);
@@ -908,7 +928,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       p8_barrier();
       // J1
       read_a(buf, 1);
-      if (!(abl & 4)) p8_vmwait<NPA>();  // A0, (Acat,) B0, B1 of t + 1 landed
+      if (!(abl & 4) && !(handed && t == kb)) p8_vmwait<NPA>();  // A0, (Acat,) B0, B1 of t + 1 landed
       // PERSIST: every slot has issued its last DMA of this tile (A0 / B0 at J1(ke - 3), A1 / B1 at J0(ke - 2)), so the
       // slots' source bases switch to the next tile here
       if (PERSIST && !FAST && t == ke - 2 && has_next) setup_tile(nm0, nn0);
@@ -964,11 +984,25 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
         for (int i = 0; i < Cfg::MI; ++i)
           for (int jj = 0; jj < Cfg::NJ; ++jj) sink += acc[i][jj][0];
         if (sink == 1234.5f) p.C[0] = 0;
+        if (has_next) {
+          dma_slot(3, 1, nk, kofs + nk);
+          dma_slot(1, 1, nk, kofs + nk);
+        }
       }
 #else
-      p8_epilogue_passes<Cfg, EPI>(p, smem + Cfg::EPI_OFF, m0, n0, acc, wr, wc);
+      p8_epilogue_passes<Cfg, EPI>(p, smem + Cfg::EPI_OFF, m0, n0, acc, wr, wc, [&] {
+        if (has_next) {  // B1 / A1 of the next tile's second k-tile (their slots' last reads retired in the k-loop)
+          dma_slot(3, 1, nk, kofs + nk);
+          dma_slot(1, 1, nk, kofs + nk);
+        }
+      });
 #endif
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // stores done; the next tile's k-tiles landed
+      if (has_next) {  // the next tile's k-tiles landed; this wave's (exactly counted) stores may stay in flight
+        p8_vmwait<p8_epi_stores<Cfg, EPI>()>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // no LDS-DMA outlives the workgroup
+      }
       p8_barrier();
       if (!has_next) return;
       j = jn;
@@ -1112,7 +1146,8 @@ template <int EPI, int BN, bool LORA = false>
 static int launch_p8_epi(const GemmArgs& a, hipStream_t s) {
   constexpr int BM = BN == 320 ? 128 : 256;
   if constexpr (!LORA && EPI != 4 && EPI != 5)
-    if (!a.A2 && p8_persist_applies(a.M, a.N, a.K, EPI, BN)) return launch_p8_persist<EPI, BN, BM>(a, s);
+    if (!a.A2 && (size_t)a.M * a.ldc * 2 < 0x7fff0000u && p8_persist_applies(a.M, a.N, a.K, EPI, BN))
+      return launch_p8_persist<EPI, BN, BM>(a, s);
   return p8_ph_env() == 2 ? launch_p8_ph<EPI, BN, LORA, 2, BM>(a, s) : launch_p8_ph<EPI, BN, LORA, 3, BM>(a, s);
 }
 
