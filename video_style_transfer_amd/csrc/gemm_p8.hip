@@ -300,11 +300,22 @@ __device__ __forceinline__ void xattn_epilogue(const GemmArgs& p, char* smem, co
 // chunks get out-of-range offsets), so every wave issues exactly p8_epi_stores<Cfg, EPI>() of them.  pre() runs after
 // the bias add (the caller's next-tile DMAs, issued before any store).
 template <class Cfg, int EPI>
+constexpr int p8_epi_ipp() {  // 16-row accumulator blocks per staged pass (both wave rows)
+  constexpr int ROWB = (EPI == 1 ? Cfg::BN / 2 : Cfg::BN) * 2, REGION = Cfg::EPI_REGION, MI = Cfg::MI;
+  return (MI >= 8 && 256 * ROWB <= REGION) ? 8
+         : (MI >= 4 && 128 * ROWB <= REGION) ? 4
+         : (MI >= 2 && 64 * ROWB <= REGION) ? 2 : 1;
+}
+template <class Cfg, int EPI>
+constexpr int p8_epi_items() {  // 16-B output chunks per thread per staged pass
+  return 32 * p8_epi_ipp<Cfg, EPI>() * ((EPI == 1 ? Cfg::BN / 2 : Cfg::BN) / 8) / Cfg::THREADS;
+}
+template <class Cfg, int EPI>
 constexpr int p8_epi_stores() {
 #ifdef VST_ABL_NOEPI
   return 0;
 #else
-  return EPI == 1 ? 2 * Cfg::MI : 0;
+  return EPI == 1 ? 2 * Cfg::MI : p8_epi_items<Cfg, EPI>() * (Cfg::MI / p8_epi_ipp<Cfg, EPI>());
 #endif
 }
 
@@ -315,10 +326,9 @@ __device__ __forceinline__ void p8_epilogue_passes(const GemmArgs& p, char* R, c
   constexpr int MI = Cfg::MI, NJ = Cfg::NJ, WM = Cfg::WM, THREADS = Cfg::THREADS;
   constexpr int OC = EPI == 1 ? Cfg::BN / 2 : Cfg::BN;  // output columns of the tile
   constexpr int ROWB = OC * 2, REGION = Cfg::EPI_REGION;
-  constexpr int IPP = (MI >= 8 && 256 * ROWB <= REGION) ? 8
-                      : (MI >= 4 && 128 * ROWB <= REGION) ? 4
-                      : (MI >= 2 && 64 * ROWB <= REGION) ? 2 : 1;
+  constexpr int IPP = p8_epi_ipp<Cfg, EPI>();
   constexpr int PR = 32 * IPP, NPASS = MI / IPP, CPR = OC / 8, ITEMS = PR * CPR / THREADS;
+  static_assert(ITEMS == p8_epi_items<Cfg, EPI>(), "store count");
   static_assert(PR * ROWB <= REGION && (PR * CPR) % THREADS == 0 && CPR % 8 == 0 && MI % IPP == 0, "pass split");
   static_assert(EPI != 1 || (Cfg::WN == 64 && NJ == 4), "GEGLU: [32 hidden | 32 gate] per wave column");
   const int tid = threadIdx.x, lane = tid & 63, fr = lane & 15, fq = lane >> 4;
@@ -341,13 +351,13 @@ __device__ __forceinline__ void p8_epilogue_passes(const GemmArgs& p, char* R, c
   }
   pre();
   const auto rr = make_rsrc(p.R ? p.R : p.Wt, p.R ? p.r_bytes : 0u);
+  const auto rc = make_rsrc(p.C, (uint32_t)((size_t)p.M * p.ldc * 2));  // (launch_p8_epi: < 2^31 bytes)
   const int nout = EPI == 1 ? p.N / 2 : p.N, c0 = EPI == 1 ? n0 / 2 : n0;
   if constexpr (EPI == 1) {
     // GEGLU: no staging -- each lane's 4 output columns (8 B) of its 16-row blocks go straight out (the 64-B row
     // segments of a wave column merge in L2; staged through the LDS in passes measured 0.15 ms per step slower,
     // profiles/r4_ab_geglu_direct.txt)
     {
-      const auto rc = make_rsrc(p.C, (uint32_t)((size_t)p.M * p.ldc * 2));  // (launch_p8_epi: < 2^31 bytes)
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const int m = m0 + wr * WM + i * 16 + fr;
@@ -404,11 +414,11 @@ __device__ __forceinline__ void p8_epilogue_passes(const GemmArgs& p, char* R, c
     for (int k = 0; k < ITEMS; ++k) {
       const int idx = tid + k * THREADS, lr = idx / CPR, cc = idx - lr * CPR;
       const int row = (lr / (16 * IPP)) * WM + q * IPP * 16 + lr % (16 * IPP), m = m0 + row, n = c0 + cc * 8;
-      if (m >= p.M || n >= nout) continue;  // (nout % 8 == 0: the launcher's condition)
+      const bool ok = m < p.M && n < nout;  // (nout % 8 == 0: the launcher's condition)
       float v[8];
       unpack8(*reinterpret_cast<const u32x4*>(R + swz(lr, cc * 16)), v);
       if constexpr (EPI == 0) {
-        if (p.rbias) {
+        if (p.rbias && ok) {
           const float* rb = p.rbias + (size_t)(m / p.rbias_div) * p.ldrb + n;
           const f32x4 r0 = *reinterpret_cast<const f32x4*>(rb), r1 = *reinterpret_cast<const f32x4*>(rb + 4);
 #pragma unroll
@@ -421,7 +431,7 @@ __device__ __forceinline__ void p8_epilogue_passes(const GemmArgs& p, char* R, c
           for (int e = 0; e < 8; ++e) v[e] += r8[e];
         }
       }
-      *reinterpret_cast<u32x4*>(p.C + (size_t)m * p.ldc + n) = pack8(v);
+      __builtin_amdgcn_raw_buffer_store_b128(pack8(v), rc, ok ? (m * p.ldc + n) * 2 : kOOB, 0, 0);
     }
     if (q + 1 < NPASS) {  // every wave's reads of this pass done before the next pass restages the region
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
