@@ -298,7 +298,8 @@ __device__ __forceinline__ void xattn_epilogue(const GemmArgs& p, char* smem, co
 // staged rows are unpadded, 16-B chunk c of staged row r at chunk c ^ (r & 7) (rows hold a multiple of 8 chunks).
 // GEGLU stores its half-width output straight from the accumulators, as unconditional buffer stores (out-of-range
 // chunks get out-of-range offsets), so every wave issues exactly p8_epi_stores<Cfg, EPI>() of them.  pre() runs after
-// the bias add (the caller's next-tile DMAs, issued before any store).
+// the bias add (the caller's next-tile DMAs, issued before any store).  GEGLU reads its bias from R, where the k-loop
+// brought it by LDS-DMA.
 template <class Cfg, int EPI>
 constexpr int p8_epi_ipp() {  // 16-row accumulator blocks per staged pass (both wave rows)
   constexpr int ROWB = (EPI == 1 ? Cfg::BN / 2 : Cfg::BN) * 2, REGION = Cfg::EPI_REGION, MI = Cfg::MI;
@@ -334,7 +335,14 @@ __device__ __forceinline__ void p8_epilogue_passes(const GemmArgs& p, char* R, c
   const int tid = threadIdx.x, lane = tid & 63, fr = lane & 15, fq = lane >> 4;
   const int lcol0 = wc * Cfg::WN + 4 * fq;
   auto swz = [](int lr, int byte) { return lr * ROWB + (((byte >> 4) ^ (lr & 7)) << 4) + (byte & 15); };
-  if (p.bias) {
+  if (EPI == 1 && p.bias) {  // (the k-loop's LDS-DMA put the tile's bias at R: no global load waits here)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const f32x4 b4 = *reinterpret_cast<const f32x4*>(R + (lcol0 + j * 16) * 4);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) acc[i][j] += b4;
+    }
+  } else if (p.bias) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int n = n0 + lcol0 + j * 16;
@@ -602,6 +610,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   // the next tile of this workgroup, whose first two k-tiles are streamed in by the current tile's last two
   int kofs = 0, nm0 = 0, nn0 = 0;
   bool has_next = false;
+  int bias_n0 = 0;  // PERSIST GEGLU: the current tile's first column (its bias DMA at J0(ke - 2))
   auto setup_tile = [&](int m0, int n0) {
     n0_tile = n0;
     if constexpr (LORA) {
@@ -925,6 +934,16 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       read_b(buf, 1, fb1);
       read_l(buf);
       if (!(abl & 4) && !(handed && t <= kb + 1)) p8_vmwait<NPA + 2 + LX>();  // A1(t) landed
+      // PERSIST GEGLU: the tile's 256 bias floats into the (otherwise unused) epilogue region by one LDS-DMA piece
+      // of wave 0 (the other waves write a zero piece into a sink, so every wave's counts shift alike); issued before
+      // B1 / A1 of ke - 1, so every counted wait keeps its count, and J1(ke - 2) covers it
+      if constexpr (EPI == 1 && PERSIST) {
+        if (!FAST && t == ke - 2) {
+          const int c = bias_n0 + 4 * lane;
+          p8_dma16(make_rsrc(p.bias, p.bias ? (uint32_t)p.N * 4u : 0u), smem + Cfg::EPI_OFF + (wid ? 1024 : 0),
+                   wid == 0 && p.bias && c < p.N ? c * 4 : kOOB);
+        }
+      }
       if (!(handed && t == kb)) {
         dma(3, t + 1);
         dma(1, t + 1);
@@ -986,6 +1005,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       const int jn = j + per;
       has_next = jn < cnt;
       if (has_next) tile_origin(beg + jn, nm0, nn0);
+      bias_n0 = n0;
       run_segment2(0, nk, first);
 #ifdef VST_ABL_NOEPI  // diagnostics build only: no epilogue (a guarded store of every accumulator's first lane
                       // element keeps all the MFMAs live)
