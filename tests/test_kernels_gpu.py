@@ -562,10 +562,12 @@ def test_permute_rows(cuda, K, dims, perm):
     assert torch.equal(out, ref)
 
 
-@pytest.mark.parametrize("rows,C,use_pe", [(300, 320, False), (64, 1280, True), (513, 640, True), (10, 64, False)])
-def test_layer_norm(cuda, K, rows, C, use_pe):
+@pytest.mark.parametrize("rows,C,use_pe,offset", [(300, 320, False, 0.0), (64, 1280, True, 0.0), (513, 640, True, 0.0),
+                                                 (10, 64, False, 0.0), (256, 1280, False, 40.0), (96, 320, False, -25.0)])
+def test_layer_norm(cuda, K, rows, C, use_pe, offset):
+    """offset: rows whose mean is far from 0 relative to their spread (the statistics' cancellation case)."""
     g = torch.Generator().manual_seed(rows + C)
-    x = rnd(rows, C, gen=g)
+    x = (rnd(rows, C, gen=g).float() + offset).to(torch.bfloat16)
     gam, bet = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g) * 0.1
     pe = torch.randn(32, C, generator=g) if use_pe else None
     HW, Fr = 4, 8
