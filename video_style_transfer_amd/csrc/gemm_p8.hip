@@ -561,6 +561,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   static_assert(EPI != 5 || (BN == 256 && BM == 256 && !LORA && !CONV), "temporal attention epilogue: 256x256 tiles");
   static_assert(EPI != 4 || (BN == 192 && BM == 256), "cross-attention epilogue: 256 x 192 tiles (3 heads)");
   constexpr int LX = LORA ? 1 : 0;  // the Acat DMA in the vmcnt counts
+  constexpr bool B1E = EPI != 1 && !LORA;  // PH = 2: B1 fragments read in J1's MFMA segment (run_segment2)
   constexpr int BUF = Cfg::BUF, RB1 = Cfg::RB1, NJ1 = Cfg::NJ1, NPB1 = Cfg::NPB1, NPA = Cfg::NPA;
   constexpr int HALF = Cfg::HALF, MQR = Cfg::MQR;
   // slot offsets inside a buffer: A0, A1, B0, B1
@@ -879,11 +880,18 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   // PH = 2: two barrier intervals of 32 MFMAs per k-tile (24 at BN = 192), so every load segment of one wave group
   // runs beside a full-length MFMA segment of the other, and each wave's DMAs split evenly over the two (the 3-interval
   // schedule pairs its 4-DMA interval with a 16-MFMA one):
-  //   J0(t) = {read A0(t), B0(t), B1(t), Acat(t); wait A1(t); issue B1(t+1), A1(t+1)} | Q(0,0) + Q(0,1)
-  //   J1(t) = {read A1(t);                        wait A0/B0/B1(t+1); issue A0(t+2) (+Acat), B0(t+2)} | Q(1,1) + Q(1,0)
-  // Every load segment ends with its LDS reads retired (lgkmcnt(0)) before its barrier, so a slot read in interval X is
-  // refilled from interval X + 1 on (WAR); a slot waited for in interval X is read in X + 1 (RAW, both groups' waits
-  // precede the barrier the later reader passes).  Same k order per accumulator as PH = 3: bitwise-equal results.
+  //   J0(t) = {read A0(t), B0(t), Acat(t); wait A1(t), B1(t+1); issue A1(t+1)}        | Q(0,0) + Q(0,1)
+  //   J1(t) = {read A1(t); wait A0/B0(t+1); issue B1(t+2), A0(t+2) (+Acat), B0(t+2)} | Q(1,1), read B1(t+1), Q(1,0)
+  // B1E (every kernel but GEGLU and the in-GEMM LoRA ones): B1's fragments are read inside J1's MFMA segment, after Q(1,1) frees fb1 (rounds
+  // 2-4 read them in J0's load segment, 16 ds_reads against J1's 8; the loop ablations showed the load segments, not
+  // the waits, idling the matrix core: profiles/r4_p8_loop_ablation.txt); so B1(t+1) is issued one interval earlier
+  // (J1(t-1), first of that segment's DMAs) and waited with A1(t) in J0(t), before both groups' J1(t) MFMA segments.
+  // GEGLU keeps   J0(t) = {read A0(t), B0(t), B1(t); wait A1(t); issue B1(t+1), A1(t+1)},  J1(t) = {read A1(t);
+  // wait A0/B0/B1(t+1); issue A0(t+2), B0(t+2)}, as do the LoRA kernels: in the step GEGLU measured 0.9 % slower
+  // with B1 moved and the LoRA kernels 1 %, the plain GEMMs and the convs 2-4 % faster (profiles/r4_ab_b1_j1.txt).  Every segment that reads
+  // LDS ends with its reads retired (lgkmcnt(0)) before its barrier, so a slot read in interval X is refilled from
+  // interval X + 1 on (WAR); a slot waited for in interval X is read in X + 1 (RAW, both groups' waits precede the
+  // barrier the later reader passes).  Same k order per accumulator as PH = 3: bitwise-equal results.
   auto run_segment2 = [&](int kb, int ke, bool first) {
 #pragma unroll
     for (int i = 0; i < Cfg::MI; ++i)
@@ -902,17 +910,21 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
                    row2 < BN && n2 < p.N ? (int)(((uint32_t)n2 * p.ldw + p.K + ub0 + 8 * (lane & 1)) * 2u) : kOOB);
       }
     }
-    // PERSIST, later tiles: k-tiles kb and kb + 1 were issued by the previous tile (B1 / A1 of kb + 1 just before its
-    // epilogue) and have landed (its post-epilogue wait), so J0(kb) issues nothing and the waits of J0(kb), J1(kb),
-    // J0(kb + 1) are skipped: the epilogue's stores, younger than those DMAs, stay in flight until J1(kb + 1)
+    // PERSIST, later tiles: k-tiles kb and kb + 1 were issued by the previous tile (A1 (!B1E: and B1) of kb + 1 just
+    // before its epilogue) and have landed (its post-epilogue wait), so J0(kb) issues nothing and the waits of J0(kb),
+    // J1(kb) (!B1E: and J0(kb + 1)) are skipped: the epilogue's stores, younger than those DMAs, stay in flight until
+    // J0(kb + 1) (B1E: B1(kb + 2) is younger) / J1(kb + 1)
     const bool handed = PERSIST && !first;
     if (!PERSIST || first) {
       dma_slot(0, kb, ke, kofs); dma_lora(kb, ke, true); dma_slot(2, kb, ke, kofs); dma_slot(3, kb, ke, kofs);
       dma_slot(1, kb, ke, kofs);
+      if constexpr (B1E) dma_slot(3, kb + 1, ke, kofs);
       dma_slot(0, kb + 1, ke, kofs); dma_lora(kb + 1, ke, true); dma_slot(2, kb + 1, ke, kofs);
-      p8_vmwait<2 * NPA + 2 + LX>();  // A0, (Acat,) B0, B1 of kb landed; A1(kb), A0/B0(kb + 1) in flight
+      // A0, (Acat,) B0, B1 of kb landed; A1(kb), (B1,) A0, B0 of kb + 1 in flight
+      p8_vmwait<2 * NPA + (B1E ? NPB1 : 0) + 2 + LX>();
     }
     p8_barrier();
+    if constexpr (B1E) read_b((kofs + kb) & 1, 1, fb1);  // B1(kb): every later B1 is read in the J1 before its k-tile
     VST_P8_STAMP(1)
     if (late) p8_barrier();
     if (late) __builtin_amdgcn_s_setprio(1);
@@ -931,12 +943,13 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       // J0
       read_a(buf, 0);
       read_b(buf, 0, fb0);
-      read_b(buf, 1, fb1);
+      if constexpr (!B1E) read_b(buf, 1, fb1);
       read_l(buf);
-      if (!(abl & 4) && !(handed && t <= kb + 1)) p8_vmwait<NPA + 2 + LX>();  // A1(t) landed
+      // A1(t) (B1E: and B1(t + 1)) landed
+      if (!(abl & 4) && !(handed && (B1E ? t == kb : t <= kb + 1))) p8_vmwait<NPA + 2 + LX>();
       // PERSIST GEGLU: the tile's 256 bias floats into the (otherwise unused) epilogue region by one LDS-DMA piece
       // of wave 0 (the other waves write a zero piece into a sink, so every wave's counts shift alike); issued before
-      // B1 / A1 of ke - 1, so every counted wait keeps its count, and J1(ke - 2) covers it
+      // A1 of ke - 1, so J0(ke - 1)'s wait keeps its count, and J1(ke - 2)'s covers it
       if constexpr (EPI == 1 && PERSIST) {
         if (!FAST && t == ke - 2) {
           const int c = bias_n0 + 4 * lane;
@@ -945,7 +958,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
         }
       }
       if (!(handed && t == kb)) {
-        dma(3, t + 1);
+        if constexpr (!B1E) dma(3, t + 1);
         dma(1, t + 1);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -957,10 +970,11 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       p8_barrier();
       // J1
       read_a(buf, 1);
-      if (!(abl & 4) && !(handed && t == kb)) p8_vmwait<NPA>();  // A0, (Acat,) B0, B1 of t + 1 landed
-      // PERSIST: every slot has issued its last DMA of this tile (A0 / B0 at J1(ke - 3), A1 / B1 at J0(ke - 2)), so the
-      // slots' source bases switch to the next tile here
+      if (!(abl & 4) && !(handed && t == kb)) p8_vmwait<NPA>();  // A0, (Acat,) B0 (!B1E: B1) of t + 1 landed
+      // PERSIST: every slot has issued its last DMA of this tile (A0 / B0 (B1E: B1) at J1(ke - 3), A1 (!B1E: B1) at
+      // J0(ke - 2)), so the slots' source bases switch to the next tile here
       if (PERSIST && !FAST && t == ke - 2 && has_next) setup_tile(nm0, nn0);
+      if constexpr (B1E) dma(3, t + 2);
       dma(0, t + 2);
       dma_lora(t + 2, ke, !FAST);
       dma(2, t + 2);
@@ -968,8 +982,12 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       p8_barrier();
       lora_mfma(acc_u[1], 0);
       VST_P8_QUAD(1, 1, fb1)
+      if constexpr (B1E) {
+        if (t + 1 < ke) read_b(buf ^ 1, 1, fb1);  // B1(t + 1), waited by both groups in J0(t)
+      }
       VST_P8_QUAD(1, 0, fb0)
       lora_mfma(acc_u[1], 1);
+      if constexpr (B1E) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       p8_barrier();
     };
     int t = kb;
@@ -1015,14 +1033,15 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
           for (int jj = 0; jj < Cfg::NJ; ++jj) sink += acc[i][jj][0];
         if (sink == 1234.5f) p.C[0] = 0;
         if (has_next) {
-          dma_slot(3, 1, nk, kofs + nk);
+          if constexpr (!B1E) dma_slot(3, 1, nk, kofs + nk);
           dma_slot(1, 1, nk, kofs + nk);
         }
       }
 #else
       p8_epilogue_passes<Cfg, EPI>(p, smem + Cfg::EPI_OFF, m0, n0, acc, wr, wc, [&] {
-        if (has_next) {  // B1 / A1 of the next tile's second k-tile (their slots' last reads retired in the k-loop)
-          dma_slot(3, 1, nk, kofs + nk);
+        if (has_next) {  // A1 (!B1E: and B1) of the next tile's second k-tile (slots free: their last reads retired
+                         // in the k-loop)
+          if constexpr (!B1E) dma_slot(3, 1, nk, kofs + nk);
           dma_slot(1, 1, nk, kofs + nk);
         }
       });
