@@ -57,6 +57,14 @@ def parse():
                     help="frames mode: clips denoised together (default N: per-GPU work fixed at one clip's "
                          "frames = weak scaling; 1 = one clip split N ways = strong scaling); N=1 or replicas: "
                          "clips batched per GPU (throughput mode, not the headline)")
+    ap.add_argument("--strong-record", default="auto", choices=["auto", "on", "off"],
+                    help="frames mode, N>1: also time ONE --frames clip split over the N ranks (strong scaling) and "
+                         "report it under sub_records.strong_1clip (auto: whenever the headline has more than 1 clip)")
+    ap.add_argument("--configs3", default="auto", choices=["auto", "on", "off"],
+                    help="frames mode, N>1: also time BASELINE configs[3] (one --configs3-frames x --configs3-size^2 "
+                         "clip frame-sharded over the ranks) under sub_records.configs3 (auto: at N=8)")
+    ap.add_argument("--configs3-frames", type=int, default=32)
+    ap.add_argument("--configs3-size", type=int, default=768)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
@@ -333,14 +341,12 @@ def _cpu_model():
     return None
 
 
-# Weak scaling (clips == ranks, the driver's default): every rank runs the unsharded forward's GEMM / norm shapes on
-# its frames, the motion GroupNorm merges the same per-frame partials in the same order, the exchange only moves
-# rows -- the sharded forward must equal the unsharded one bit for bit (tests/test_frame_shard.py).  Strong scaling
-# (fewer clips than ranks) runs smaller per-rank row counts, where a GEMM may pick another split-K / fusion policy:
-# fp32 summation orders there reach ~1e-2 through the whole UNet; a layout or exchange error is O(1).
-PREFLIGHT_TOL_STRONG = 0.1
-
-
+# Frame-sharded N-GPU runs, weak (clips == ranks, the driver's default) and strong (fewer clips than ranks, the
+# sub-records) alike: every rank runs the unsharded forward's GEMM / norm kernels with a k order that does not depend on
+# the row count (kernels.row_invariant), takes every shape-dependent fusion decision as the unsharded forward does
+# under kernels.fusion_world(P), merges the motion GroupNorm's per-frame partials in the same order, and the exchange
+# only moves rows -- so the sharded forward must equal the unsharded one bit for bit in both modes
+# (tests/test_frame_shard.py: 2, 4 and 8 ranks on one GPU, configs[3]'s 8 x 4 frames of 32 x 768^2 included).
 def _gather0(t, world, rank):
     """All ranks' equal-shaped tensors -> list on rank 0 (None elsewhere); staged through host memory on gloo."""
     import torch.distributed as dist
@@ -377,16 +383,15 @@ def shard_preflight(den, unet, world, rank):
         x = torch.empty(B * world * rows, Cl, dtype=torch.bfloat16, device=den.x.device)
         K.pack_latents(lat_full, x, sigmas=den.sigmas, step_idx=den.step_idx, ncopy=den.ncopy)
         with torch.no_grad():
-            ref = unet.forward_tokens(x, B, F * world, h, w, emb, den.enc)
+            ref = unet.forward_tokens(x, B, F * world, h, w, emb, den.enc, fusion_world=world)
         e2 = ((got.float() - ref.float()).norm() / ref.float().norm()).item()
         em = ((got.float() - ref.float()).abs().max() / ref.float().abs().max()).item()
         exact = bool(torch.equal(got, ref))
-        weak = n == world
         out = {"rel_l2": round(e2, 9), "rel_max": round(em, 9), "bitwise_equal": exact,
-               "gate": "bitwise equality" if weak else f"rel_l2 <= {PREFLIGHT_TOL_STRONG} (strong scaling)",
-               "what": f"{n} clip(s) x CFG pair noise prediction, {world}-way frame-sharded eager forward vs rank 0's "
-                       f"unsharded forward of all {F * world} frames"}
-        ok = (exact if weak else e2 <= PREFLIGHT_TOL_STRONG) and bool(torch.isfinite(got.float()).all())
+               "gate": "bitwise equality (" + ("weak" if n == world else "strong") + " scaling)",
+               "what": f"{n} clip(s) x CFG pair noise prediction at {8 * h}x{8 * w}, {world}-way frame-sharded eager "
+                       f"forward ({F} frames per rank) vs rank 0's unsharded forward of all {F * world} frames"}
+        ok = exact and bool(torch.isfinite(got.float()).all())
         if not ok:
             print(json.dumps({"preflight_failed": out}), file=sys.stderr)
         del ref, x, got
@@ -563,19 +568,116 @@ def main():
 
     from video_style_transfer_amd.config import UNetMotionConfig
     from video_style_transfer_amd.lora_linear import set_lora_mode
-    from video_style_transfer_amd.pipeline import AnimateDiffDenoiser
     from video_style_transfer_amd.utils import build_unet
 
     cfg = UNetMotionConfig.sdxl()
     set_lora_mode(args.lora_mode)
     t_build = time.perf_counter()
     unet = build_unet(cfg, seed=args.seed, lora_rank=args.lora_rank or None, device=dev)
-    shard, nclips = None, max(1, args.clips)
-    if world > 1 and args.parallel == "frames":
+    t_build = time.perf_counter() - t_build
+    sharded = world > 1 and args.parallel == "frames"
+    nclips = (args.clips or world) if sharded else max(1, args.clips)
+    head = timed_denoise(args, unet, cfg, world, rank, dev, rehearsal, frames=args.frames, size=args.size,
+                         nclips=nclips, sharded=sharded)
+    den, ms_step, value = head["den"], head["ms_per_step"], head["value"]
+    ok = bool(torch.isfinite(den.lat).all().item())
+
+    rl, table = (None, None) if args.no_roofline else roofline(den, ms_step)
+    step = None
+    if rl is not None:
+        # whole denoise step against the chip: algorithmic flops of every launch (table in DESIGN.md 3) per
+        # graph-replayed step time
+        fl = rl.pop("step_flops")
+        step = {"alg_tflop": round(fl / 1e12, 2), "achieved_tflops": round(fl / (ms_step * 1e-3) / 1e12, 1),
+                "frac": round(fl / (ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4)}
+        if rank == 0 and not rehearsal and not args.no_peaks:
+            rl["peak_measured"] = measured_peaks(dev, rl)
+            step["frac_of_measured"] = round(step["achieved_tflops"] / rl["peak_measured"]["mfma_bf16_tflops"], 4)
+    graphed = den.graph is not None
+    vae_rec = None if args.no_vae else vae_decode_timing(args, den, dev, ms_step)
+    den.graph = None  # (piecewise graphs hold no collective; released before the next run's memory)
+    del den, head["den"]
+    torch.cuda.empty_cache()
+
+    # N-GPU frame sharding: the north star's curve needs more than the weak-scaling headline -- one 16-frame clip split
+    # N ways (strong scaling) and, on 8 GPUs, BASELINE configs[3] (one 32 x 768^2 clip, 4 frames per GPU); each runs
+    # its own bitwise preflight, piecewise capture and timing with the same --steps / --warmup
+    subs = {}
+    if sharded and world > 1:
+        want_strong = args.strong_record == "on" or (args.strong_record == "auto" and nclips != 1)
+        want_c3 = args.configs3 == "on" or (args.configs3 == "auto" and world == 8)
+        plans = []
+        if want_strong:
+            plans.append(("strong_1clip", args.frames, args.size))
+        if want_c3:
+            plans.append(("configs3", args.configs3_frames, args.configs3_size))
+        for name, fr, sz in plans:
+            if fr % world:
+                subs[name] = {"skipped": f"{fr} frames do not split over {world} ranks"}
+                continue
+            r = timed_denoise(args, unet, cfg, world, rank, dev, rehearsal, frames=fr, size=sz, nclips=1,
+                              sharded=True)
+            subs[name] = {
+                "value": round(r["value"], 4), "unit": "frames/s", "ms_per_step": round(r["ms_per_step"], 3),
+                "n_gpus": world, "scaling": "strong", "frames": fr, "resolution": sz, "clips": 1,
+                "frames_per_gpu": fr // world, "graph": r["den"].graph is not None, "note": r["graph_note"],
+                "shard_preflight": r["preflight"],
+                "finite": bool(torch.isfinite(r["den"].lat).all().item()),
+                "workload": ("BASELINE configs[3]: " if name == "configs3" else "") +
+                            f"one {fr}x{sz}x{sz} clip + UnZipLoRA rank-{args.lora_rank}, CFG pair, frame-sharded "
+                            f"x{world} ({fr // world} frames/GPU, "
+                            + ("all-to-all" if args.exchange == "all_to_all" else "all-gather") + ")"}
+            r["den"].graph = None
+            del r
+            torch.cuda.empty_cache()
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        del unet
+        torch.cuda.empty_cache()
+        cpu = cpu_baseline(args, cfg)
+    if rank == 0:
+        out = {
+            "metric": f"denoised frames/sec, {args.frames}x{args.size}x{args.size} clip, "
+                      f"{args.num_inference_steps}-step AnimateDiff-XL",
+            "value": round(value, 4), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
+            "scaling": "strong" if (sharded and nclips < world) else "weak",
+            "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "config": {"workload": f"BASELINE configs[2]: {args.frames}x{args.size}x{args.size} clip + UnZipLoRA "
+                                   f"rank-{args.lora_rank} ({args.lora_mode}) on all 560 spatial q/k/v/out, "
+                                   f"{args.num_inference_steps}-step Euler, CFG {args.guidance} batched (B=2)",
+                       "model": "SDXL UNet + AnimateDiff-SDXL motion modules (synthetic weights)",
+                       "global_batch": nclips if sharded else nclips * world, "frames": args.frames,
+                       "resolution": args.size,
+                       "parallelism": (f"frame-shard x{world} ({nclips} clips, {args.frames // world} frames/clip/GPU, "
+                                       + ("RCCL all-to-all around each motion module)" if args.exchange == "all_to_all"
+                                          else "RCCL all-gather of the clip before each motion module)")
+                                       if sharded else
+                                       f"replicas x{world}" if world > 1 else "single") + (
+                                       f", {nclips} clips batched per GPU" if not sharded and nclips > 1 else ""),
+                       "graph": graphed,
+                       "note": head["graph_note"]},
+            "roofline": rl, "step_roofline": step, "vae_decode": vae_rec, "cpu_baseline": cpu, "kernels": table,
+            "finite": ok, "shard_preflight": head["preflight"], "sub_records": subs or None,
+            "setup_s": round(t_build, 1),
+        }
+        print(json.dumps(out))
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()  # (every HIP graph released above: a graph must not outlive the communicator)
+
+
+def timed_denoise(args, unet, cfg, world, rank, dev, rehearsal, *, frames, size, nclips, sharded):
+    """One denoiser of `nclips` clips of `frames` x size^2 (frame-sharded over the ranks when `sharded`): preflight
+    (sharded), capture (one HIP graph; piecewise at N > 1), --warmup untimed and --steps timed replays bracketed by
+    barrier + synchronize, the max over ranks.  Returns the denoiser (for the roofline / VAE records) and the timing."""
+    from video_style_transfer_amd.pipeline import AnimateDiffDenoiser
+    shard = None
+    if sharded:
         from video_style_transfer_amd.frame_shard import FrameShard
         shard = FrameShard(exchange=args.exchange)
-        nclips = args.clips or world
-    den = AnimateDiffDenoiser(unet, args.frames, args.size, args.size, num_inference_steps=args.num_inference_steps,
+    den = AnimateDiffDenoiser(unet, frames, size, size, num_inference_steps=args.num_inference_steps,
                               guidance_scale=args.guidance, device=dev, shard=shard, num_clips=nclips)
     seed_rank = 0 if shard is not None else rank  # sharded ranks hold frames of the SAME clips
     g = torch.Generator().manual_seed(7 + seed_rank)
@@ -612,7 +714,6 @@ def main():
             elif shard is not None:
                 graph_note = (f"piecewise capture: {den.graph.num_graphs} HIP graphs per step, the "
                               f"{len(den.graph.items) - den.graph.num_graphs} collectives ({shard.backend}) between them")
-    t_build = time.perf_counter() - t_build
 
     def one_step():
         if den.graph is not None:
@@ -643,55 +744,9 @@ def main():
         dt = float(tt.item())
     ms_step = dt / args.steps * 1e3
     # frames mode: nclips whole clips spread over all ranks; replicas: every rank denoises its own clip
-    frames_total = args.frames * nclips if shard is not None else args.frames * nclips * world
+    frames_total = frames * nclips if shard is not None else frames * nclips * world
     value = frames_total / (args.num_inference_steps * ms_step * 1e-3)
-    ok = bool(torch.isfinite(den.lat).all().item())
-
-    rl, table = (None, None) if args.no_roofline else roofline(den, ms_step)
-    step = None
-    if rl is not None:
-        # whole denoise step against the chip: algorithmic flops of every launch (table in DESIGN.md 3) per
-        # graph-replayed step time
-        fl = rl.pop("step_flops")
-        step = {"alg_tflop": round(fl / 1e12, 2), "achieved_tflops": round(fl / (ms_step * 1e-3) / 1e12, 1),
-                "frac": round(fl / (ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4)}
-        if rank == 0 and not rehearsal and not args.no_peaks:
-            rl["peak_measured"] = measured_peaks(dev, rl)
-            step["frac_of_measured"] = round(step["achieved_tflops"] / rl["peak_measured"]["mfma_bf16_tflops"], 4)
-    graphed = den.graph is not None
-    vae_rec = None if args.no_vae else vae_decode_timing(args, den, dev, ms_step)
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        del den, unet
-        torch.cuda.empty_cache()
-        cpu = cpu_baseline(args, cfg)
-    if rank == 0:
-        out = {
-            "metric": f"denoised frames/sec, {args.frames}x{args.size}x{args.size} clip, "
-                      f"{args.num_inference_steps}-step AnimateDiff-XL",
-            "value": round(value, 4), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
-            "scaling": "strong" if (shard is not None and nclips < world) else "weak",
-            "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
-            "config": {"workload": f"BASELINE configs[2]: {args.frames}x{args.size}x{args.size} clip + UnZipLoRA "
-                                   f"rank-{args.lora_rank} ({args.lora_mode}) on all 560 spatial q/k/v/out, "
-                                   f"{args.num_inference_steps}-step Euler, CFG {args.guidance} batched (B=2)",
-                       "model": "SDXL UNet + AnimateDiff-SDXL motion modules (synthetic weights)",
-                       "global_batch": nclips if shard is not None else nclips * world, "frames": args.frames,
-                       "resolution": args.size,
-                       "parallelism": (f"frame-shard x{world} ({nclips} clips, {args.frames // world} frames/clip/GPU, "
-                                       + ("RCCL all-to-all around each motion module)" if args.exchange == "all_to_all"
-                                          else "RCCL all-gather of the clip before each motion module)")
-                                       if shard is not None else
-                                       f"replicas x{world}" if world > 1 else "single") + (
-                                       f", {nclips} clips batched per GPU" if shard is None and nclips > 1 else ""),
-                       "graph": graphed,
-                       "note": graph_note},
-            "roofline": rl, "step_roofline": step, "vae_decode": vae_rec, "cpu_baseline": cpu, "kernels": table,
-            "finite": ok, "shard_preflight": preflight,
-            "setup_s": round(t_build, 1),
-        }
-        print(json.dumps(out))
+    return {"den": den, "ms_per_step": ms_step, "value": value, "preflight": preflight, "graph_note": graph_note}
 
 
 if __name__ == "__main__":

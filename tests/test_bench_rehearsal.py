@@ -2,7 +2,8 @@
 both on cuda:0 over gloo (VST_BENCH_REHEARSAL=gloo; RCCL cannot put two ranks on one device), frame sharding of every
 clip over the ranks.  Before anything is timed, bench.py runs its shard preflight -- one eager frame-sharded UNet
 forward, gathered to rank 0 and compared with rank 0's unsharded forward of the same clips -- and exits non-zero
-unless the two are bit-identical (weak scaling, clips == ranks); the JSON line carries the result.  The driver's 8-GPU run goes through the same code with
+unless the two are bit-identical (weak scaling, clips == ranks; and the strong-scaling sub-records: one clip split over the
+ranks, configs[3]'s shape class); the JSON line carries the results.  The driver's 8-GPU run goes through the same code with
 the nccl backend (and the step captured in a HIP graph)."""
 import json
 import os
@@ -29,7 +30,8 @@ def test_bench_two_rank_frame_shard_rehearsal():
     env = dict(os.environ, VST_BENCH_REHEARSAL="gloo", OMP_NUM_THREADS="4")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps",
-           "1", "--warmup", "0", "--frames", "16", "--size", "256", "--no-cpu-baseline", "--no-vae", "--no-roofline"]
+           "1", "--warmup", "0", "--frames", "16", "--size", "256", "--no-cpu-baseline", "--no-vae", "--no-roofline",
+           "--configs3", "on", "--configs3-frames", "8", "--configs3-size", "256"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
@@ -38,3 +40,12 @@ def test_bench_two_rank_frame_shard_rehearsal():
     print(f"[rehearsal] {d['config']['parallelism']}: {d['ms_per_step']} ms/step, preflight {pf}")
     assert d["n_gpus"] == 2 and d["finite"]
     assert pf is not None and pf["bitwise_equal"] and pf["rel_l2"] == 0.0
+    # the sub-records the driver's N-GPU run adds: one clip split over the ranks (strong scaling) and configs[3]'s
+    # shape class (here 8 frames at 256^2 so the rehearsal stays short), each with its own bitwise preflight
+    subs = d["sub_records"]
+    for name in ("strong_1clip", "configs3"):
+        r = subs[name]
+        print(f"[rehearsal] {name}: {r['ms_per_step']} ms/step, {r['frames_per_gpu']} frames/GPU, "
+              f"preflight {r['shard_preflight']}")
+        assert r["scaling"] == "strong" and r["finite"] and r["value"] > 0
+        assert r["shard_preflight"]["bitwise_equal"], r["shard_preflight"]

@@ -4,10 +4,11 @@ CPU (gloo, world sizes 2, 4 and 8 -- the last is configs[3]'s 8 ranks x 4 frames
 sharded motion module (all-reduced GroupNorm statistics + frame-axis work on pixel shards) equals the
 oracle's unsharded motion module (oracle/unet.py motion_module) on each rank's frames.
 
-GPU (gloo transport, 2-4 ranks on one GPU, HIP kernels): a frame-sharded tiny-UNet forward is as close
+GPU (gloo transport, 2-8 ranks on one GPU, HIP kernels): a frame-sharded tiny-UNet forward is as close
 to the fp32 oracle's whole-clip forward as the unsharded HIP forward is (both bf16); at configs[3]'s SDXL 32 x 768^2
-shape (B = 1 over 2 ranks, and the CFG pair over 4 ranks) the gathered shards ARE the unsharded HIP forward, bit for
-bit.
+shape (B = 1 over 2 ranks, and the CFG pair over 4 and 8 ranks -- 8 x 4 frames is configs[3]'s own split), the
+16 x 512^2 clip over 8 ranks (2 frames each) and 16 x 576^2 over 2 ranks (a motion level whose per-rank pixel count is
+not a multiple of 16) the gathered shards ARE the unsharded HIP forward, bit for bit.
 """
 import os
 import socket
@@ -216,7 +217,7 @@ def _gpu_worker_sdxl768(rank, world, port, q, exchange="all_to_all"):
         Fl, f0 = sh.local_frames(F)
         part = unet(lat[:, :, f0:f0 + Fl].contiguous().to(dev), t.to(dev), enc.to(dev), frame_shard=sh,
                     **kw).sample.cpu()
-        full = unet(lat.to(dev), t.to(dev), enc.to(dev), **kw).sample.cpu()[:, :, f0:f0 + Fl]
+        full = unet(lat.to(dev), t.to(dev), enc.to(dev), fusion_world=world, **kw).sample.cpu()[:, :, f0:f0 + Fl]
         # every op outside the motion modules is frame-local with frame-invariant bits (GroupNorm chunking and GEMM
         # k order depend on the frame shape only); the motion GroupNorm merges the same per-frame partials in the
         # same order; the exchange only moves rows: the shards must be the unsharded bits exactly
@@ -243,13 +244,18 @@ def test_frame_shard_sdxl_768_32_frames_two_ranks_one_gpu(exchange):
         assert status == "ok", f"rank {rank}: {info}"
 
 
-def _gpu_worker_sdxl768_cfg(rank, world, port, q):
-    """BASELINE configs[3] with the CFG pair (B = 2: uncond + cond text states, as the denoise loop batches them):
-    32 frames at 768x768 split over 4 ranks (8 frames each) on one GPU.  Rank 0 gathers the shards and compares
-    them with its unsharded forward of the whole clip (the other ranks run the sharded forward only)."""
+def _gpu_worker_sdxl_cfg(rank, world, port, q, F=32, hw=96, exchange="all_to_all"):
+    """The CFG pair (B = 2: uncond + cond text states, as the denoise loop batches them) of one SDXL clip of F frames
+    at (8 hw)^2, split over `world` ranks (F / world frames each) on one GPU.  Rank 0 gathers the shards and compares
+    them with its unsharded forward of the whole clip under kernels.fusion_world(world) (the other ranks run the sharded
+    forward only): BASELINE configs[3] (32 x 768^2) over 4 and 8 ranks -- 8 x 4 frames is configs[3]'s own split --
+    the 16 x 512^2 clip split 8 ways (bench.py's strong-scaling sub-record at N = 8), and 16 x 576^2 over 2 ranks, whose
+    36 x 36 motion level gives each all-to-all rank 648 pixels (not a multiple of 16: that layer's motion attention
+    is not fused into its q/k/v GEMM on the ranks, so the unsharded forward must not fuse it either)."""
     try:
         sys.path.insert(0, ROOT)
         _init(rank, world, port)
+        from video_style_transfer_amd import kernels as K
         from video_style_transfer_amd.config import UNetMotionConfig
         from video_style_transfer_amd.frame_shard import FrameShard
         from video_style_transfer_amd.utils import build_unet
@@ -257,30 +263,37 @@ def _gpu_worker_sdxl768_cfg(rank, world, port, q):
         torch.cuda.set_device(dev)
         cfg = UNetMotionConfig.sdxl()
         unet = build_unet(cfg, seed=43, lora_rank=8, device=dev)
-        F, hw = 32, 96
+        print(f"[shard] rank {rank}/{world}: UNet built", flush=True)
         g = torch.Generator().manual_seed(44)
         lat1 = torch.randn(1, 4, F, hw, hw, generator=g)
         lat = torch.cat([lat1, lat1])  # the CFG pair shares the latents
         enc = torch.randn(2, 77, cfg.cross_attention_dim, generator=g)
         pooled = torch.randn(2, cfg.text_embed_dim, generator=g)
-        tids = torch.tensor([[768, 768, 0, 0, 768, 768]] * 2, dtype=torch.float32)
+        tids = torch.tensor([[8 * hw, 8 * hw, 0, 0, 8 * hw, 8 * hw]] * 2, dtype=torch.float32)
         t = torch.tensor([501.0, 501.0])
         kw = dict(added_cond_kwargs={"text_embeds": pooled.to(dev), "time_ids": tids.to(dev)})
-        sh = FrameShard()
+        sh = FrameShard(exchange=exchange)
         Fl, f0 = sh.local_frames(F)
         part = unet(lat[:, :, f0:f0 + Fl].contiguous().to(dev), t.to(dev), enc.to(dev), frame_shard=sh,
                     **kw).sample.float().cpu()
+        print(f"[shard] rank {rank}/{world}: sharded forward done", flush=True)
         parts = [torch.empty_like(part) for _ in range(world)]
         dist.all_gather(parts, part)
         if rank != 0:
             q.put((rank, "ok", f"frames {f0}..{f0 + Fl - 1} sent to rank 0"))
             return
         whole = torch.cat(parts, 2)
-        full = unet(lat.to(dev), t.to(dev), enc.to(dev), **kw).sample.float().cpu()
+        full = unet(lat.to(dev), t.to(dev), enc.to(dev), fusion_world=world, **kw).sample.float().cpu()
+        print(f"[shard] rank 0: unsharded forward done", flush=True)
         same = torch.equal(whole, full)
         d = [(whole[b] - full[b]).abs().max().item() for b in range(2)]
-        q.put((rank, "ok" if same else "fail", f"4 shards x {Fl} frames, CFG pair: gathered shards == unsharded: "
-                                               f"{same} (max |diff| uncond {d[0]:.3e}, cond {d[1]:.3e})"))
+        msg = (f"{F}x{8 * hw}^2, {world} shards x {Fl} frames, CFG pair: gathered shards == unsharded: {same} "
+               f"(max |diff| uncond {d[0]:.3e}, cond {d[1]:.3e})")
+        if same and any(s_ * s_ % (16 * world) for s_ in (hw, hw // 2)):
+            # the case the policy exists for: without it the unsharded forward fuses a layer the ranks cannot
+            fused = unet(lat.to(dev), t.to(dev), enc.to(dev), **kw).sample.float().cpu()
+            msg += f"; unsharded without the policy differs: {not torch.equal(fused, full)}"
+        q.put((rank, "ok" if same else "fail", msg))
     except BaseException:  # noqa: BLE001
         import traceback
         q.put((rank, "fail", traceback.format_exc()[-2000:]))
@@ -290,12 +303,15 @@ def _gpu_worker_sdxl768_cfg(rank, world, port, q):
 
 
 @pytest.mark.gpu
-def test_frame_shard_sdxl_768_32_frames_cfg_pair_four_ranks_one_gpu():
+@pytest.mark.parametrize("world,F,hw", [(4, 32, 96), (8, 32, 96), (8, 16, 64), (2, 16, 72)],
+                         ids=["configs3_4ranks", "configs3_8ranks_x4frames", "strong_16x512_8ranks",
+                              "576_2ranks_fusion_policy"])
+def test_frame_shard_sdxl_cfg_pair_one_gpu(world, F, hw):
     if torch.cuda.device_count() == 0:
         pytest.skip("no HIP device")
-    res = _spawn(_gpu_worker_sdxl768_cfg, 4)
+    res = _spawn(_gpu_worker_sdxl_cfg, world, F, hw)
     for rank, status, info in res:
-        print(f"[shard] configs[3] CFG pair rank {rank}: {status} {info}")
+        print(f"[shard] CFG pair rank {rank}: {status} {info}")
         assert status == "ok", f"rank {rank}: {info}"
 
 

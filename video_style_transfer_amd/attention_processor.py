@@ -217,7 +217,10 @@ class AttnProcessor2_0:
         D = inner // heads
         x = hidden_states.reshape(batch * N, C)
         ops = build_ops([attn.to_q, attn.to_k, attn.to_v], 1.0)
+        # (HW % (16 P) under K.fusion_world(P): a P-way all-to-all rank holds HW / P pixels and fuses only when that
+        # is a multiple of 16, so the unsharded forward it is compared with decides the same way)
         if num_frames is not None and _tattn_enabled() and ops.a is None and ops.w.shape[1] == C and \
+                HW % (16 * K.fusion_pixel_div()) == 0 and \
                 K.temporal_attention_fusable(batch * N, C, nclip, Fr, HW, heads, D):
             # q/k/v projection + frame attention in one launch (vst_gemm_temporal_attention; 16 frames, heads of 40)
             w_t, b_t = _tattn_operands(attn, ops, heads, D)

@@ -48,7 +48,14 @@ class PiecewiseGraph:
     """A HIP-graph capture split at the collectives: capture() runs `fn` once under capture; every collective that
     FrameShard issues meanwhile closes the current graph, is recorded as a host call, and a new graph opens after it.
     replay() replays graph, collective, graph, ... in capture order on the current stream.  All pieces share one
-    memory pool (replayed in capture order, as torch requires for pool sharing)."""
+    memory pool (replayed in capture order, as torch requires for pool sharing).
+
+    Why the collectives stay outside the graphs: a collective captured INTO a graph makes RCCL keep a persistent plan
+    that references the communicator for as long as the graph lives; destroy_process_group with such a graph still
+    alive waits for it forever (round 4's hang, profiles/r4_rccl_diag.log: a captured all_to_all_single -- RCCL
+    send/recv -- at world 1).  Destroying the graph first exits cleanly (profiles/r5_rccl_diag_del.log), so whole-step
+    capture is possible with that teardown order; the piecewise form is kept because it is the one the 1-GPU box can
+    exercise with real collectives (gloo, 2-8 ranks) and it costs ~1 % of a step."""
 
     def __init__(self):
         self.items = []
@@ -84,6 +91,18 @@ class PiecewiseGraph:
                 fn()
                 self._end()
             torch.cuda.current_stream().wait_stream(stream)
+        except BaseException:
+            # end the open capture (else the side stream stays in capture mode and every later HIP call fails
+            # confusingly) and drop every piece: a half-captured step is never replayed
+            if self._g is not None:
+                try:
+                    with torch.cuda.stream(stream):
+                        self._g.capture_end()
+                except Exception:  # noqa: BLE001 -- the original error is the one to report
+                    pass
+                self._g = None
+            self.items.clear()
+            raise
         finally:
             for sh in shards:
                 sh._pw = None

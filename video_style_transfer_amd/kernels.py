@@ -78,6 +78,37 @@ class row_invariant:
         _ROW_INVARIANT[0] -= 1
 
 
+_FUSION_WORLD = [1]
+
+
+class fusion_world:
+    """Inside: shape-dependent fusion decisions are taken as a P-way frame-sharded rank takes them, so a forward here
+    computes exactly the bits of a P-way sharded forward.  The one such decision is the motion attention fused into
+    its q/k/v GEMM (vst_gemm_temporal_attention), which needs the pixels a rank holds to be a multiple of 16: with the
+    all-to-all exchange a rank holds H*W/P pixels, so an unsharded forward (or an all-gather rank, which holds all
+    H*W) under fusion_world(P) fuses a layer only when (H*W) % (16 P) == 0.  UNetMotionModel.forward_tokens enters it
+    with the shard's world size (or its `fusion_world` argument); the all-to-all branch of MotionModule, whose
+    pixels are already split, re-enters it with 1."""
+
+    def __init__(self, world: int):
+        if world < 1:
+            raise ValueError(f"fusion_world({world})")
+        self.world = int(world)
+
+    def __enter__(self):
+        self._prev = _FUSION_WORLD[0]
+        _FUSION_WORLD[0] = self.world
+        return self
+
+    def __exit__(self, *a):
+        _FUSION_WORLD[0] = self._prev
+
+
+def fusion_pixel_div() -> int:
+    """The P of the enclosing fusion_world (1 outside any)."""
+    return _FUSION_WORLD[0]
+
+
 def _splits():
     s = GEMM_POLICY["splits"]
     return s if s or not _ROW_INVARIANT[0] else 1
@@ -723,8 +754,7 @@ def colsum(x, out=None):
     if N % 8 or _ld(x) % 8 or x.data_ptr() % 16:
         n8 = (N + 7) // 8 * 8
         xp = torch.zeros((M, n8), dtype=BF16, device=x.device)
-        K_copy = xp[:, :N]
-        K_copy.copy_(x)
+        xp[:, :N].copy_(x)  # (stream-ordered scratch: no cached buffer, which a captured graph would alias)
         full = colsum(xp)
         out.copy_(full[:N])
         return out

@@ -313,8 +313,9 @@ class MotionModule(nn.Module):
         Fl = ctx.F
         h = shard.to_pixels(h, B, Fl, HW)
         tctx = dataclasses.replace(ctx, F=Fl * P)
-        for blk in self.transformer_blocks:
-            h = blk.run(h, B * Fl * P, HW // P, tctx)
+        with K.fusion_world(1):  # (these HW // P pixels are this rank's share already)
+            for blk in self.transformer_blocks:
+                h = blk.run(h, B * Fl * P, HW // P, tctx)
         h = shard.to_frames(h, B, Fl, HW)
         return self.proj_out.run(h, residual=x)
 
@@ -539,10 +540,15 @@ class UNetMotionModel(nn.Module):
         return out
 
     # ---- core (NHWC tokens) -----------------------------------------------------------------
-    def forward_tokens(self, x, B, F, h, w, emb_silu, enc, cross_kwargs=None, shard=None):
+    def forward_tokens(self, x, B, F, h, w, emb_silu, enc, cross_kwargs=None, shard=None, fusion_world=None):
         """x: [B*F*h*w, in_channels] bf16 -> noise prediction [B*F*h*w, out_channels] bf16.
-        With `shard` (frame_shard.FrameShard), F is this rank's frames of each clip."""
-        with K.row_invariant():  # no split-K: a row's bits do not depend on the launch's row count (frame shards)
+        With `shard` (frame_shard.FrameShard), F is this rank's frames of each clip.  `fusion_world` P (default: the
+        shard's world size, else 1): take the shape-dependent fusion decisions a P-way frame-sharded rank takes
+        (kernels.fusion_world), so an unsharded forward equals a P-way sharded one bit for bit."""
+        if fusion_world is None:
+            fusion_world = shard.world if shard is not None else 1
+        # no split-K: a row's bits do not depend on the launch's row count (frame shards)
+        with K.row_invariant(), K.fusion_world(fusion_world):
             ctx = FwdCtx(B, F, emb_silu, enc, cross_kwargs or {}, shard, self.batched_temb(emb_silu))
             nimg = B * F
             H, W = h, w
@@ -558,9 +564,11 @@ class UNetMotionModel(nn.Module):
             return self.conv_out.run(x, nimg, H, W)
 
     def forward(self, sample, timestep, encoder_hidden_states, timestep_cond=None, attention_mask=None,
-                cross_attention_kwargs=None, added_cond_kwargs=None, return_dict=True, frame_shard=None, **kwargs):
+                cross_attention_kwargs=None, added_cond_kwargs=None, return_dict=True, frame_shard=None,
+                fusion_world=None, **kwargs):
         """diffusers UNetMotionModel.forward signature (inference_animatediff.py:110-121).  With
-        `frame_shard` (frame_shard.FrameShard) `sample` holds this rank's frames of each clip."""
+        `frame_shard` (frame_shard.FrameShard) `sample` holds this rank's frames of each clip; `fusion_world`: see
+        forward_tokens."""
         if not sample.is_cuda:
             raise K._lib.VstError("UNetMotionModel: sample is on CPU; the HIP path has no CPU fallback")
         B, Cin, F, h, w = sample.shape
@@ -576,6 +584,7 @@ class UNetMotionModel(nn.Module):
         enc = encoder_hidden_states.to(dev, BF16).contiguous()
         x = torch.empty(B * F * h * w, Cin, dtype=BF16, device=dev)
         K.pack_latents(sample.float().contiguous(), x)
-        y = self.forward_tokens(x, B, F, h, w, emb_silu, enc, cross_attention_kwargs, shard=frame_shard)
+        y = self.forward_tokens(x, B, F, h, w, emb_silu, enc, cross_attention_kwargs, shard=frame_shard,
+                                fusion_world=fusion_world)
         out = y.view(B, F, h, w, -1).permute(0, 4, 1, 2, 3).contiguous().to(sample.dtype)
         return UNetMotionOutput(out) if return_dict else (out,)
