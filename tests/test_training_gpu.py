@@ -457,10 +457,15 @@ def test_unet_training_step_grads_vs_oracle(cuda, config):
     G = torch.randn(B * Fr * h * h, 4, generator=g).to(BF).float()
 
     # oracle: fp32 leaves (trainable where the module's parameter is), temporal LoRA as W + s B A; run as torch fp32
-    # ops on the GPU (full fp32: no TF32), and once more under torch.autocast("cuda", bf16) -- the reference's own
-    # mixed precision (accelerate mixed_precision="bf16", train_animatediff.py:51-54) -- as the yardstick
-    def oracle_grads(autocast):
-        leaves = {n: p.detach().float().clone().requires_grad_(p.requires_grad) for n, p in unet.named_parameters()}
+    # ops on the GPU (full fp32: no TF32) for the reference gradients, and once more on the CPU under
+    # torch.autocast("cpu", bf16) -- the reference's own mixed precision (accelerate mixed_precision="bf16",
+    # train_animatediff.py:51-54) -- as the yardstick.  The yardstick runs on the CPU with a fixed thread count because
+    # there it is the same bits every run (checked: all 390 motion gradients of two SDXL runs torch.equal); torch's GPU
+    # autocast is not (its SDXL median moved 4.78e-2 .. 5.54e-2 over four runs, profiles/r4_train_grads_ab.txt), and a
+    # gate keyed to it moved with it
+    def oracle_grads(autocast, dev):
+        leaves = {n: p.detach().float().to(dev).clone().requires_grad_(p.requires_grad)
+                  for n, p in unet.named_parameters()}
         P = {}
         for n, v in leaves.items():
             if ".base." in n:
@@ -471,21 +476,24 @@ def test_unet_training_step_grads_vs_oracle(cuda, config):
             if isinstance(m, TemporalLoRALinear):
                 P[n + ".weight"] = leaves[n + ".base.weight"] + m.scale * leaves[n + ".lora_B"] @ leaves[n + ".lora_A"]
         for n, b in unet.named_buffers():
-            P[n] = b.detach().float()
-        with torch.autocast("cuda", dtype=BF, enabled=autocast):
-            ref = unet_forward(P, cfg.to_dict(), sample.to(cuda), t, enc.to(cuda), pooled.to(cuda), tids.to(cuda),
+            P[n] = b.detach().float().to(dev)
+        with torch.autocast(dev.type, dtype=BF, enabled=autocast):
+            ref = unet_forward(P, cfg.to_dict(), sample.to(dev), t.to(dev), enc.to(dev), pooled.to(dev), tids.to(dev),
                                LoRAState())
         ref_tok = ref.float().permute(0, 2, 3, 4, 1).reshape(-1, 4)
-        (ref_tok * G.to(cuda)).sum().backward()
-        return ref_tok.detach(), {n: v.grad for n, v in leaves.items() if v.requires_grad}
+        (ref_tok * G.to(dev)).sum().backward()
+        return ref_tok.detach().to(cuda), {n: v.grad.to(cuda) for n, v in leaves.items() if v.requires_grad}
 
     tf32 = torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32
     torch.backends.cuda.matmul.allow_tf32 = torch.backends.cudnn.allow_tf32 = False
+    nthreads = torch.get_num_threads()
     try:
-        ref_tok, want = oracle_grads(False)
-        yard_tok, yard = oracle_grads(True)
+        ref_tok, want = oracle_grads(False, cuda)
+        torch.set_num_threads(16)
+        yard_tok, yard = oracle_grads(True, torch.device("cpu"))
     finally:
         torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32 = tf32
+        torch.set_num_threads(nthreads)
 
     emb = unet.embed(t.expand(B).contiguous(), pooled.to(cuda, BF), tids.to(cuda), B)
     x = torch.empty(B * Fr * h * h, 4, dtype=BF, device=cuda)
@@ -518,24 +526,33 @@ def test_unet_training_step_grads_vs_oracle(cuda, config):
         kinds[k] = max(kinds.get(k, 0.0), errs[n])
     print(f"[train] {config}: {len(errs)} trainable tensors ({sum(named[n].numel() for n in trainable) / 1e6:.1f} M "
           f"params); grad rel_l2 median {errs[order[len(order) // 2]]:.2e}, 95th pct "
-          f"{errs[order[int(0.95 * (len(order) - 1))]]:.2e}, worst {order[-1]} {errs[order[-1]]:.2e} | bf16-autocast "
-          f"oracle: median {yorder[len(yorder) // 2]:.2e}, 95th pct {yorder[int(0.95 * (len(yorder) - 1))]:.2e}, "
-          f"worst {yorder[-1]:.2e}")
+          f"{errs[order[int(0.95 * (len(order) - 1))]]:.2e}, worst {order[-1]} {errs[order[-1]]:.2e} | CPU bf16-autocast "
+          f"oracle (yardstick): median {yorder[len(yorder) // 2]:.2e}, 95th pct "
+          f"{yorder[int(0.95 * (len(yorder) - 1))]:.2e}, worst {yorder[-1]:.2e}")
+    ratio = sorted(errs[n] / yerr[n] for n in trainable)
+    print(f"[train] {config}: per-tensor HIP / yardstick error ratio: median {ratio[len(ratio) // 2]:.2f}, 95th pct "
+          f"{ratio[int(0.95 * (len(ratio) - 1))]:.2f}, max {ratio[-1]:.2f}")
+    for n in trainable:
+        print(f"[train] {config}   {n:90s} {errs[n]:.3e}  yardstick {yerr[n]:.3e}")
     for k, v in sorted(kinds.items(), key=lambda kv: -kv[1]):
         print(f"[train] {config}   worst per kind {k:40s} {v:.2e}")
-    # Gates (round 4): the error DISTRIBUTION over all trainable tensors at the reference's own bf16-autocast one --
-    # median and 95th percentile within 1.25x of the autocast gradients' (or 3e-2 / 6e-2 absolute) -- and every
-    # tensor within 2x its autocast error (or 5e-2).  Why not round 3's per-tensor 1.5x: the yardstick is not
-    # reproducible (torch's bf16-autocast GEMMs on the GPU: its SDXL median measured 4.78e-2, 4.88e-2, 5.04e-2 and
-    # 5.54e-2 in four runs of this test on the same inputs), and an ulp-level change of the forward moves the HIP
-    # gradients' median by the same ~10 % (in-GEMM vs two-pass UnZipLoRA down-projection, numerically equivalent to
-    # 1e-3: 5.46e-2 vs 4.97e-2); per tensor, two such noisy estimates differ by more than 1.5x somewhere among 480
-    # (9.1e-2 vs 5.9e-2 on one tensor).  Recorded in DESIGN.md §5 and profiles/r4_train_grads_ab.txt.
-    bad = {n: (e, yerr[n]) for n, e in errs.items() if e >= max(5e-2, 2.0 * yerr[n])}
+    # Gates (round 5), fixed once against the deterministic CPU bf16-autocast yardstick (profiles/r5_train_grads.log):
+    #   sdxl (the production architecture, 480 tensors): every tensor within 1.25x its yardstick error (measured max
+    #        1.10x), and the distribution no worse than the yardstick's (median 4.18e-2 vs 5.46e-2, 95th pct 7.01e-2 vs
+    #        9.35e-2): the HIP gradients are at least as close to fp32 as the reference's own precision;
+    #   tiny (F=8, 16x16, C=32/64: tensors of a few hundred elements, where one rounding flip moves a tensor's error):
+    #        every tensor within 2x its yardstick error or 3e-2 (max 1.77x, at 3.5e-2 vs 2.0e-2), median and 95th pct
+    #        within 1.1x of the yardstick's (0.91x / 0.89x measured).
+    # Both sides are the same bits every run (the HIP path and the CPU yardstick at 16 threads), so these gates do not
+    # move between runs; round 4's moved with torch's GPU autocast.
+    tol_t, floor_t, tol_d = (1.25, 0.0, 1.0) if config == "sdxl" else (2.0, 3e-2, 1.1)
+    bad = {n: (e, yerr[n]) for n, e in errs.items() if e > max(floor_t, tol_t * yerr[n])}
     assert not bad, bad
     med, ymed = errs[order[len(order) // 2]], yorder[len(yorder) // 2]
     p95, yp95 = errs[order[int(0.95 * (len(order) - 1))]], yorder[int(0.95 * (len(yorder) - 1))]
-    assert med <= max(3e-2, 1.25 * ymed) and p95 <= max(6e-2, 1.25 * yp95), (med, ymed, p95, yp95)
+    print(f"[train] {config}: gates: every tensor <= max({floor_t}, {tol_t} x yardstick); median {med:.3e} <= "
+          f"{tol_d} x {ymed:.3e}; 95th pct {p95:.3e} <= {tol_d} x {yp95:.3e}")
+    assert med <= tol_d * ymed and p95 <= tol_d * yp95, (med, ymed, p95, yp95)
 
 
 @pytest.mark.parametrize("M,N,ld,c0", [(512, 512, 512, 0), (65536, 1280, 1280, 0), (1000, 64, 72, 0), (3, 8, 8, 0),
