@@ -19,7 +19,11 @@ SHAPES = [  # name, kind, M, N, K (16x512^2 CFG pair: 16^2 level M = 8192, 32^2 
     ("out1280_lora", "lora1", 8192, 1280, 1280), ("qkv1280_lora", "lora3", 8192, 3840, 1280),
     ("out640_lora", "lora1", 32768, 640, 640), ("qkv640_lora", "lora3", 32768, 1920, 640),
     ("qkv960_320", "plain", 131072, 960, 320), ("ff2_320", "plain", 131072, 320, 1280),
+    ("xattn1280_lora", "xattn", 8192, 1280, 1280), ("xattn640_lora", "xattn", 32768, 640, 640),
 ]
+if os.environ.get("VST_AB_SHAPES"):  # comma-separated subset of the names above
+    _keep = set(os.environ["VST_AB_SHAPES"].split(","))
+    SHAPES = [s for s in SHAPES if s[0] in _keep]
 
 
 def child(passes_inner=2):
@@ -33,7 +37,18 @@ def child(passes_inner=2):
         x = torch.randn(M, Kd, device=dev, generator=g).to(torch.bfloat16)
         r = torch.randn(M, N, device=dev, generator=g).to(torch.bfloat16)
         b = torch.randn(N, device=dev, generator=g) * 0.1
-        if kind.startswith("lora"):
+        if kind == "xattn":  # attn2: to_q + UnZipLoRA (r 8: 16 u columns) + the 77-key text attention epilogue
+            P = 32
+            w = (torch.randn(N, Kd + P, device=dev, generator=g) * Kd ** -0.5).to(torch.bfloat16)
+            a = torch.zeros(P, Kd, device=dev)
+            a[:16] = torch.randn(16, Kd, device=dev, generator=g) * Kd ** -0.5
+            a = a.to(torch.bfloat16)
+            kt = torch.randn(32 * 77, N, device=dev, generator=g).to(torch.bfloat16)
+            vt = torch.randn(32 * 77, N, device=dev, generator=g).to(torch.bfloat16)
+            nq = M // 32
+            fn = (lambda: K.linear_cross_attention(x, w, a, N, 16, b, kt, vt, Nq=nq, Nk=77, kv_div=1, scale=0.125))
+            fl = 2.0 * M * N * (Kd + 16) + 2.0 * M * Kd * 16 + 4.0 * M * N * 77
+        elif kind.startswith("lora"):
             nproj = int(kind[-1])
             P = 32 if nproj == 1 else 64
             w = (torch.randn(N, Kd + P, device=dev, generator=g) * Kd ** -0.5).to(torch.bfloat16)
@@ -70,7 +85,8 @@ def child(passes_inner=2):
         out.append({"ph": os.environ.get("VST_P8_PH", "3"), "shape": name, "M": M, "N": N, "K": Kd,
                     "lora_tile": K.gemm_lora_tile(M, N, Kd, 32 if kind == "lora1" else 64, N // int(kind[-1]), 16)
                     if kind.startswith("lora") else None,
-                    "kernel": None if kind.startswith("lora") else K.gemm_kernel_name(M, N, Kd, 1 if kind == "geglu" else 0),
+                    "kernel": "xattn" if kind == "xattn" else None if kind.startswith("lora") else
+                    K.gemm_kernel_name(M, N, Kd, 1 if kind == "geglu" else 0),
                     "us": round(best, 2), "tflops": round(fl / best / 1e6, 1), "md5": h})
     for o in out:
         print(json.dumps(o), flush=True)

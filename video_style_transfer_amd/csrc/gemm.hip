@@ -896,7 +896,7 @@ extern "C" int vst_gemm_lora(const void* x, int ldx, const void* Acat, int ld_ac
   a.la_bytes = clamp_bytes((size_t)P * ld_acat * 2);
   a.stride = 1; a.splits = 1;
   a.p8_bn = bn;
-  a.ablate = 0;
+  a.ablate = gemm_ablate_env();  // (reaches the kernel in the diagnostics build only, -DVST_P8_TRACE)
   a.group_m = 0;
   return launch_gemm_p8_lora(a, bn, (hipStream_t)stream);
 }
@@ -949,6 +949,7 @@ extern "C" int vst_gemm_cross_attention(const void* x, int ldx, const void* Acat
   a.xa_kvdiv = kv_div; a.xa_scale_log2 = scale * 1.4426950408889634f;
   a.xa_kv_bytes = clamp_bytes(((size_t)(nkv_rows - 1) * ldkv + N) * 2);
   a.stride = 1; a.splits = 1; a.p8_bn = 192;
+  a.ablate = gemm_ablate_env();  // (diagnostics build only)
   return launch_gemm_p8_xattn(a, (hipStream_t)stream);
 }
 

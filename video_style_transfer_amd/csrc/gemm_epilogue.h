@@ -7,7 +7,21 @@
 
 namespace vst {
 
-template <class Cfg, int EPI>
+// Tile row (relative to the wave row's first row) of accumulator row block i.  ROT (the 8-phase kernel's in-GEMM
+// LoRA variants): wave column wc reads the row blocks of each A quadrant rotated by wc, so block i of quadrant
+// i / MQR is ((i mod MQR) + wc) mod MQR (MQR = MI / 2 blocks per quadrant, a power of two there).
+template <class Cfg, bool ROT>
+__device__ __forceinline__ int p8_acc_row(const int i, const int wc) {
+  if constexpr (!ROT) {
+    return i * 16;
+  } else {
+    constexpr int MQR = Cfg::MI / 2;
+    static_assert((MQR & (MQR - 1)) == 0, "rotated row blocks: MQR a power of two");
+    return (i / MQR) * (MQR * 16) + (((i % MQR) + wc) & (MQR - 1)) * 16;
+  }
+}
+
+template <class Cfg, int EPI, bool ROT = false>
 __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, char* smem, const int m0, const int n0,
                                               f32x4 (&acc)[Cfg::MI][Cfg::NJ], const int wr, const int wc,
                                               const int tid = threadIdx.x) {
@@ -74,7 +88,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, char* smem, con
 #endif
           v[e] = pack2bf(o.x, o.y);
         }
-        *reinterpret_cast<u32x2*>(smem + (lrow0 + i * 16) * OROW + (wc * 32 + j * 16 + 4 * fq) * 2) = v;
+        *reinterpret_cast<u32x2*>(smem + (lrow0 + p8_acc_row<Cfg, ROT>(i, wc)) * OROW + (wc * 32 + j * 16 + 4 * fq) * 2) = v;
       }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -105,7 +119,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, char* smem, con
       u32x2 v;
       v[0] = pack2bf(a4[0], a4[1]);
       v[1] = pack2bf(a4[2], a4[3]);
-      *reinterpret_cast<u32x2*>(smem + (lrow0 + i * 16) * LROW + (lcol0 + j * 16) * 2) = v;
+      *reinterpret_cast<u32x2*>(smem + (lrow0 + p8_acc_row<Cfg, ROT>(i, wc)) * LROW + (lcol0 + j * 16) * 2) = v;
     }
   // publish the staged tile; a raw barrier (no vmcnt drain) keeps the residual loads in flight
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

@@ -102,7 +102,7 @@ __device__ __forceinline__ void p8_barrier() {
 // S^T = K.Q^T and O^T = V^T.P^T on MFMA (the spatial_attn_kernel layouts, one pass over all keys).  q is never
 // written to HBM and read back, and the separate attention launch disappears.  LDS: 256 x 400 B of q + 3 x 20 KiB of
 // K/V = 160 KiB exactly.
-template <class Cfg>
+template <class Cfg, bool ROT>
 __device__ __forceinline__ void xattn_epilogue(const GemmArgs& p, char* smem, const int m0, const int n0,
                                                f32x4 (&acc)[Cfg::MI][Cfg::NJ], const int wr, const int wc) {
   constexpr int BM = Cfg::BM, BN = Cfg::BN, NH = BN / 64;
@@ -146,7 +146,7 @@ __device__ __forceinline__ void xattn_epilogue(const GemmArgs& p, char* smem, co
         u32x2 v;
         v[0] = pack2bf(a4[0], a4[1]);
         v[1] = pack2bf(a4[2], a4[3]);
-        *reinterpret_cast<u32x2*>(smem + (lrow0 + i * 16) * LROW + (lcol0 + j * 16) * 2) = v;
+        *reinterpret_cast<u32x2*>(smem + (lrow0 + p8_acc_row<Cfg, ROT>(i, wc)) * LROW + (lcol0 + j * 16) * 2) = v;
       }
     }
   }
@@ -560,7 +560,17 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   static_assert(!PERSIST || (!LORA && !CONV && EPI != 4 && EPI != 5 && PH == 2), "persistent tiles: plain / GEGLU / GELU, PH 2");
   static_assert(EPI != 5 || (BN == 256 && BM == 256 && !LORA && !CONV), "temporal attention epilogue: 256x256 tiles");
   static_assert(EPI != 4 || (BN == 192 && BM == 256), "cross-attention epilogue: 256 x 192 tiles (3 heads)");
-  constexpr int LX = LORA ? 1 : 0;  // the Acat DMA in the vmcnt counts
+  // LORA: the Acat DMA of a k-tile is issued by waves 0-1 only (one 1-KiB piece each), so their counted vmcnt waits
+  // count it and the other waves' do not (VST_P8_VMWAIT_LX; rounds 3-4 had waves 2-7 DMA a zero piece into a sink
+  // to keep one count: 6 extra LDS writes and DMA issues per k-tile)
+#define VST_P8_VMWAIT_LX(X)                  \
+  do {                                       \
+    if (LORA && wid < 2) p8_vmwait<(X) + 1>(); \
+    else p8_vmwait<(X)>();                   \
+  } while (0)
+  // one A source (the launchers of the persistent, LoRA, cross- and temporal-attention variants pass no A2): the
+  // loader's per-k-tile source selection is compiled out
+  constexpr bool ONE_A = PERSIST || LORA || EPI == 4 || EPI == 5;
   constexpr bool B1E = EPI != 1 && !LORA;  // PH = 2: B1 fragments read in J1's MFMA segment (run_segment2)
   constexpr int BUF = Cfg::BUF, RB1 = Cfg::RB1, NJ1 = Cfg::NJ1, NPB1 = Cfg::NPB1, NPA = Cfg::NPA;
   constexpr int HALF = Cfg::HALF, MQR = Cfg::MQR;
@@ -698,7 +708,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     if (CONV && s < 2) {
       conv_dma(s, live, dst);
     } else if (s < 2) {
-      const bool second = !PERSIST && k0 >= p.K1;
+      const bool second = ONE_A ? false : k0 >= p.K1;
       const uint32_t kb = (uint32_t)(second ? k0 - p.K1 : k0) * 2u;
 #pragma unroll
       for (int pc = 0; pc < NPA; ++pc) {
@@ -724,7 +734,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     if (CONV && s < 2) {
       conv_dma(s, true, dst);
     } else if (s < 2) {
-      const bool second = !PERSIST && k0 >= p.K1;
+      const bool second = ONE_A ? false : k0 >= p.K1;
       const uint32_t kb = (uint32_t)(second ? k0 - p.K1 : k0) * 2u;
 #pragma unroll
       for (int pc = 0; pc < NPA; ++pc)
@@ -736,12 +746,14 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     }
   };
 
-  // LORA: Acat columns of k-tile kt into its slot (buffer kt & 1); waves 2-7 write a zero piece into the sink
+  // LORA: Acat columns of k-tile kt into its slot (buffer kt & 1), by waves 0-1 (the others issue nothing)
   auto dma_lora = [&](int kt, int kend, bool checked) {
+    if ((abl & 1) && kt > 1) return;
     if constexpr (LORA) {
-      char* dst = wid < 2 ? smem + Cfg::LORA_OFF + (kt & 1) * 2048 + wid * 1024 : smem + Cfg::LORA_OFF + 4096;
+      if (wid >= 2) return;
+      char* dst = smem + Cfg::LORA_OFF + (kt & 1) * 2048 + wid * 1024;
       const int k0 = kt * 64;
-      const bool kin = wid < 2 && (!checked || (kt < kend && k0 + lc8 < p.K));
+      const bool kin = !checked || (kt < kend && k0 + lc8 < p.K);
       p8_dma16(rl, dst, kin ? (int)(lbase + (uint32_t)k0 * 2u) : kOOB);
     }
   };
@@ -749,9 +761,13 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   f32x4 acc[Cfg::MI][Cfg::NJ];
   f32x4 acc_u[2];   // LORA: u of row block wc of row quadrants 0 / 1 (this wave's row half)
   bf16x8 fl[2];     // LORA: Acat fragments of the current k-tile (16 u columns x 2 k-halves)
-  bf16x8 fu[2];     // LORA: A fragments of row block wc of the current row quadrant (a copy of fa[wc], read
-                    // separately so the u MFMAs index no register array by the runtime wc)
-  bf16x8 fa[MQR][2];       // A fragments of the current row quadrant (mq): MQR x 16 rows x 2 k-halves
+  // A fragments of the current row quadrant (mq): MQR x 16 rows x 2 k-halves.  LORA: wave column wc reads the
+  // quadrant's row blocks rotated by wc (fa[i] = block (i + wc) mod MQR), so fa[0] is block wc, whose 16 u rows this
+  // wave accumulates: the u MFMAs use fa[0] and no register array is indexed by the runtime wc (rounds 3-4 read block
+  // wc a second time into a dedicated fu pair: 4 of the 28 ds_read_b128 per wave and k-tile).  acc[mq MQR + i] then
+  // holds row block (i + wc) mod MQR of quadrant mq (p8_acc_row), which only the epilogues' row addressing sees: the
+  // same operands meet in the same k order, so the bits are unchanged.
+  bf16x8 fa[MQR][2];
   bf16x8 fb0[2][2], fb1[NJ1 > 2 ? NJ1 : 2][2];  // W fragments of column quadrants nq0 / nq1
 #ifdef VST_P8_TRACE
   for (int i = 0; i < MQR; ++i) for (int h = 0; h < 2; ++h) fa[i][h] = bf16x8{};
@@ -762,13 +778,10 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     if (abl & 16) return;
     const char* S = smem + buf * BUF + slot_off(mq);
 #pragma unroll
-    for (int i = 0; i < MQR; ++i)
+    for (int i = 0; i < MQR; ++i) {
+      const int ib = LORA ? ((i + wc) & (MQR - 1)) : i;  // (MQR < 4: waves wc >= MQR repeat a block, their u unused)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) fa[i][h] = *reinterpret_cast<const bf16x8*>(S + p8_off(wr * HALF + i * 16 + fr, h * 4 + fq));
-    if constexpr (LORA) {  // row block wc of the quadrant (MQR < 4: waves wc >= MQR repeat a block, their u unused)
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        fu[h] = *reinterpret_cast<const bf16x8*>(S + p8_off(wr * HALF + (wc % MQR) * 16 + fr, h * 4 + fq));
+      for (int h = 0; h < 2; ++h) fa[i][h] = *reinterpret_cast<const bf16x8*>(S + p8_off(wr * HALF + ib * 16 + fr, h * 4 + fq));
     }
   };
   auto read_b = [&](int buf, int nq, auto& fb) {
@@ -781,6 +794,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       for (int h = 0; h < 2; ++h) fb[j][h] = *reinterpret_cast<const bf16x8*>(S + p8_off(wc * rb + j * 16 + fr, h * 4 + fq));
   };
   auto read_l = [&](int buf) {
+    if (abl & 16) return;
     if constexpr (LORA) {
       const char* S = smem + Cfg::LORA_OFF + buf * 2048;
 #pragma unroll
@@ -789,7 +803,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   };
   // LORA: u rows of row block wc of the current row quadrant
   auto lora_mfma = [&](f32x4& au, int h) {
-    if constexpr (LORA) au = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fl[h], fu[h], au, 0, 0, 0);
+    if constexpr (LORA) if (!(abl & 2)) au = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fl[h], fa[0][h], au, 0, 0, 0);
   };
 #define VST_P8_QUAD(MQ, NQ, FB)                                                                        \
   if (!(abl & 2)) {                                                                                  \
@@ -826,7 +840,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     dma_slot(0, kb, ke, 0); dma_lora(kb, ke, true); dma_slot(2, kb, ke, 0); dma_slot(3, kb, ke, 0);
     dma_slot(1, kb, ke, 0); dma_slot(3, kb + 1, ke, 0); dma_slot(0, kb + 1, ke, 0); dma_lora(kb + 1, ke, true);
     dma_slot(2, kb + 1, ke, 0);
-    p8_vmwait<2 * NPA + 2 + NPB1 + LX>();  // A0, (Acat,) B0, B1 of kb landed
+    VST_P8_VMWAIT_LX(2 * NPA + 2 + NPB1);  // A0, (Acat,) B0, B1 of kb landed
     p8_barrier();
     VST_P8_STAMP(1)
     read_b(kb & 1, 1, fb1);
@@ -842,7 +856,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       read_a(buf, 0);
       read_b(buf, 0, fb0);
       read_l(buf);
-      if (!(abl & 4)) p8_vmwait<NPA + 2 + NPB1 + LX>();  // A1(t) landed
+      if (!(abl & 4)) VST_P8_VMWAIT_LX(NPA + 2 + NPB1);  // A1(t) landed
       dma(1, t + 1);
       p8_barrier();
       lora_mfma(acc_u[0], 0);
@@ -852,7 +866,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       p8_barrier();
       // I1
       read_a(buf, 1);
-      if (!(abl & 4)) p8_vmwait<2 * NPA + 2 + LX>();  // B1(t+1) landed
+      if (!(abl & 4)) VST_P8_VMWAIT_LX(2 * NPA + 2);  // B1(t+1) landed
       dma(3, t + 2);
       p8_barrier();
       lora_mfma(acc_u[1], 0);
@@ -921,7 +935,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       if constexpr (B1E) dma_slot(3, kb + 1, ke, kofs);
       dma_slot(0, kb + 1, ke, kofs); dma_lora(kb + 1, ke, true); dma_slot(2, kb + 1, ke, kofs);
       // A0, (Acat,) B0, B1 of kb landed; A1(kb), (B1,) A0, B0 of kb + 1 in flight
-      p8_vmwait<2 * NPA + (B1E ? NPB1 : 0) + 2 + LX>();
+      VST_P8_VMWAIT_LX(2 * NPA + (B1E ? NPB1 : 0) + 2);
     }
     p8_barrier();
     if constexpr (B1E) read_b((kofs + kb) & 1, 1, fb1);  // B1(kb): every later B1 is read in the J1 before its k-tile
@@ -946,7 +960,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       if constexpr (!B1E) read_b(buf, 1, fb1);
       read_l(buf);
       // A1(t) (B1E: and B1(t + 1)) landed
-      if (!(abl & 4) && !(handed && (B1E ? t == kb : t <= kb + 1))) p8_vmwait<NPA + 2 + LX>();
+      if (!(abl & 4) && !(handed && (B1E ? t == kb : t <= kb + 1))) VST_P8_VMWAIT_LX(NPA + 2);
       // PERSIST GEGLU: the tile's 256 bias floats into the (otherwise unused) epilogue region by one LDS-DMA piece
       // of wave 0 (the other waves write a zero piece into a sink, so every wave's counts shift alike); issued before
       // A1 of ke - 1, so J0(ke - 1)'s wait keeps its count, and J1(ke - 2)'s covers it
@@ -1003,6 +1017,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     p8_barrier();
   };
 #undef VST_P8_QUAD
+#undef VST_P8_VMWAIT_LX
 
   int m0, n0;
   VST_P8_STAMP(0)
@@ -1088,7 +1103,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     }
 #pragma unroll
     for (int i = 0; i < Cfg::MI; ++i) {
-      bf16x8 fu = *reinterpret_cast<const bf16x8*>(U + (wr * Cfg::WM + i * 16 + fr) * 32 + (fq & 1) * 16);
+      bf16x8 fu = *reinterpret_cast<const bf16x8*>(U + (wr * Cfg::WM + p8_acc_row<Cfg, true>(i, wc) + fr) * 32 + (fq & 1) * 16);
       fu = fq < 2 ? fu : zero8;
 #pragma unroll
       for (int j = 0; j < Cfg::NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fv[j], fu, acc[i][j], 0, 0, 0);
@@ -1096,17 +1111,17 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave's u reads done before the epilogue stages the tile over them
   }
-  if constexpr (EPI == 4) xattn_epilogue<Cfg>(p, smem, m0, n0, acc, wr, wc);
-  else if constexpr (EPI == 5) tattn_epilogue<Cfg>(p, smem, m0, n0, acc, wr, wc);
-#ifdef VST_ABL_NOEPI
-  else {
+#ifdef VST_ABL_NOEPI  // diagnostics build only: no epilogue of any kind (attention epilogues included)
+  {
     float sink = 0.f;
     for (int i = 0; i < Cfg::MI; ++i)
       for (int jj = 0; jj < Cfg::NJ; ++jj) sink += acc[i][jj][0];
     if (sink == 1234.5f) p.C[0] = 0;
   }
 #else
-  else tile_epilogue<Cfg, EPI>(p, smem, m0, n0, acc, wr, wc);
+  if constexpr (EPI == 4) xattn_epilogue<Cfg, LORA>(p, smem, m0, n0, acc, wr, wc);
+  else if constexpr (EPI == 5) tattn_epilogue<Cfg>(p, smem, m0, n0, acc, wr, wc);
+  else tile_epilogue<Cfg, EPI, LORA>(p, smem, m0, n0, acc, wr, wc);
 #endif
 #ifdef VST_P8_TRACE
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
