@@ -87,6 +87,19 @@ __device__ __forceinline__ void p8_dma16(__amdgpu_buffer_rsrc_t r, char* lds_pie
 
 __device__ __forceinline__ int p8_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
 
+// scheduling hint for an MFMA segment that also issues NV LDS-DMAs (VMEM) among its NM MFMAs: one DMA after every
+// NM / (NV + 1) MFMAs, the rest of the MFMAs after the last one
+template <int NM, int NV>
+__device__ __forceinline__ void p8_interleave_dma() {
+  constexpr int PER = NM / (NV + 1) > 0 ? NM / (NV + 1) : 1;
+#pragma unroll
+  for (int g = 0; g < NV; ++g) {
+    __builtin_amdgcn_sched_group_barrier(0x008, PER, 0);  // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);    // VMEM read (buffer_load ... lds)
+  }
+  __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
+}
+
 __device__ __forceinline__ void p8_barrier() {
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
@@ -571,7 +584,21 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   // one A source (the launchers of the persistent, LoRA, cross- and temporal-attention variants pass no A2): the
   // loader's per-k-tile source selection is compiled out
   constexpr bool ONE_A = PERSIST || LORA || EPI == 4 || EPI == 5;
+  // DMM (A/B build VST_P8_DMM): a k-tile interval's LDS-DMAs issued inside the wave's MFMA segment, interleaved with
+  // its MFMAs, instead of in its load segment after the fragment reads (an LDS-DMA costs its wave ~60 cycles among
+  // bare MFMAs and 100-185 in a segment that carries 16 ds_read_b128, MI355X_MICROARCH.md constants table; the loop
+  // ablations put the load segments, not the MFMAs, on the critical path).  Same DMAs in the same order per wave, so
+  // every counted wait keeps its count; the slots they refill were read one interval earlier still.
+#ifdef VST_P8_DMM
+  constexpr bool DMM = true;
+#else
+  constexpr bool DMM = false;
+#endif
+#ifdef VST_P8_LORA_B1E  // (A/B build: the in-GEMM LoRA kernels with the B1 placement of the plain GEMMs)
+  constexpr bool B1E = EPI != 1;
+#else
   constexpr bool B1E = EPI != 1 && !LORA;  // PH = 2: B1 fragments read in J1's MFMA segment (run_segment2)
+#endif
   constexpr int BUF = Cfg::BUF, RB1 = Cfg::RB1, NJ1 = Cfg::NJ1, NPB1 = Cfg::NPB1, NPA = Cfg::NPA;
   constexpr int HALF = Cfg::HALF, MQR = Cfg::MQR;
   // slot offsets inside a buffer: A0, A1, B0, B1
@@ -596,7 +623,9 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   const bool ktail = !PERSIST && (p.K & 63) != 0;  // (PERSIST: K % 64 == 0 and one A source, the launcher's terms)
   const bool late = wid >= 4;
 #ifdef VST_P8_TRACE
-  // diagnostics build only (VST_GEMM_ABLATE): 1 no loop DMA, 2 no MFMA, 4 no loop vmcnt waits, 16 no fragment reads
+  // diagnostics build only (VST_GEMM_ABLATE): 1 no loop DMA, 2 no MFMA, 4 no loop vmcnt waits, 16 no fragment reads,
+  // 64 no W-operand traffic in the loop (its DMAs and fragment reads; the upper bound of taking W out of the LDS),
+  // 128 no A-operand traffic in the loop
   const int abl = p.ablate;
 #else
   constexpr int abl = 0;
@@ -702,6 +731,8 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   // uniform
   auto dma_slot = [&](int s, int kt, int kend, int kbase) {
     if ((abl & 1) && kt > 1) return;
+    if ((abl & 64) && s >= 2 && kt > 1) return;
+    if ((abl & 128) && s < 2 && kt > 1) return;
     char* dst = smem + ((kbase + kt) & 1) * BUF + slot_off(s) + PB * 1024;
     const int k0 = kt * 64;
     const bool live = kt < kend && !((abl & 32) && kt > 1);
@@ -729,6 +760,8 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   // slot s of a k-tile that is live and fully inside K (every k-tile but the last two of a segment): no checks
   auto dma_fast = [&](int s, int kt) {
     if ((abl & 1) && kt > 1) return;
+    if ((abl & 64) && s >= 2 && kt > 1) return;
+    if ((abl & 128) && s < 2 && kt > 1) return;
     char* dst = smem + ((kofs + kt) & 1) * BUF + slot_off(s) + PB * 1024;
     const int k0 = kt * 64;
     if (CONV && s < 2) {
@@ -775,7 +808,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   for (int j = 0; j < NJ1; ++j) for (int h = 0; h < 2; ++h) fb1[j][h] = bf16x8{};
 #endif
   auto read_a = [&](int buf, int mq) {  // (buf: the LDS buffer, 0 or 1)
-    if (abl & 16) return;
+    if (abl & (16 | 128)) return;
     const char* S = smem + buf * BUF + slot_off(mq);
 #pragma unroll
     for (int i = 0; i < MQR; ++i) {
@@ -785,7 +818,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     }
   };
   auto read_b = [&](int buf, int nq, auto& fb) {
-    if (abl & 16) return;
+    if (abl & (16 | 64)) return;
     const char* S = smem + buf * BUF + slot_off(2 + nq);
     const int rb = nq == 0 ? 32 : RB1;
 #pragma unroll
@@ -971,16 +1004,21 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
                    wid == 0 && p.bias && c < p.N ? c * 4 : kOOB);
         }
       }
-      if (!(handed && t == kb)) {
-        if constexpr (!B1E) dma(3, t + 1);
-        dma(1, t + 1);
-      }
+      auto dma_j0 = [&] {
+        if (!(handed && t == kb)) {
+          if constexpr (!B1E) dma(3, t + 1);
+          dma(1, t + 1);
+        }
+      };
+      if constexpr (!DMM) dma_j0();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       p8_barrier();
       lora_mfma(acc_u[0], 0);
       VST_P8_QUAD(0, 0, fb0)
+      if constexpr (DMM) dma_j0();
       VST_P8_QUAD(0, 1, fb1)
       lora_mfma(acc_u[0], 1);
+      if constexpr (DMM) p8_interleave_dma<(2 + NJ1) * MQR * 2 + (LORA ? 2 : 0), (B1E ? 0 : NPB1) + NPA>();
       p8_barrier();
       // J1
       read_a(buf, 1);
@@ -988,19 +1026,28 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       // PERSIST: every slot has issued its last DMA of this tile (A0 / B0 (B1E: B1) at J1(ke - 3), A1 (!B1E: B1) at
       // J0(ke - 2)), so the slots' source bases switch to the next tile here
       if (PERSIST && !FAST && t == ke - 2 && has_next) setup_tile(nm0, nn0);
-      if constexpr (B1E) dma(3, t + 2);
-      dma(0, t + 2);
-      dma_lora(t + 2, ke, !FAST);
-      dma(2, t + 2);
+      // (DMM: the Acat piece, issued by waves 0-1 only, stays in the load segment, ahead of A0 / B0: a wave-dependent
+      // branch inside the MFMA segment would split it; every wait that counts it counts A0 and B0 as well)
+      static_assert(!(DMM && LORA && B1E), "DMM + LoRA: the Acat piece must stay younger than B1");
+      auto dma_j1 = [&] {
+        if constexpr (B1E) dma(3, t + 2);
+        dma(0, t + 2);
+        if constexpr (!DMM) dma_lora(t + 2, ke, !FAST);
+        dma(2, t + 2);
+      };
+      if constexpr (DMM) dma_lora(t + 2, ke, !FAST);
+      if constexpr (!DMM) dma_j1();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       p8_barrier();
       lora_mfma(acc_u[1], 0);
       VST_P8_QUAD(1, 1, fb1)
+      if constexpr (DMM) dma_j1();
       if constexpr (B1E) {
         if (t + 1 < ke) read_b(buf ^ 1, 1, fb1);  // B1(t + 1), waited by both groups in J0(t)
       }
       VST_P8_QUAD(1, 0, fb0)
       lora_mfma(acc_u[1], 1);
+      if constexpr (DMM) p8_interleave_dma<(2 + NJ1) * MQR * 2 + (LORA ? 2 : 0), (B1E ? NPB1 : 0) + NPA + 2>();
       if constexpr (B1E) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       p8_barrier();
     };
