@@ -26,6 +26,8 @@ sys.path.insert(0, ROOT)
 
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table; no sparsity)
 PEAK_HBM_GBS = 8000.0
+HBM_MEASURED_GBS = 6300.0       # vst_probe_hbm_read / MI355X_MICROARCH.md ("6.29 TB/s measured")
+MFMA_MEASURED_TFLOPS = 2440.0   # vst_probe_mfma
 
 KERNEL_OF_KIND = {  # non-GEMM kinds; GEMM/conv launches carry the library's own kernel name
     "spatial_attention": "spatial_attn_kernel",
@@ -172,10 +174,11 @@ def _roofline_from(rec, step_ms=None):
     for kind, sym, fl, nb, ms, shape in rec:
         sym = sym or KERNEL_OF_KIND.get(kind, kind)
         if shape is not None:
-            d = shapes.setdefault(f"{kind} {shape[0]}x{shape[1]}x{shape[2]} {sym}", [0, 0.0, 0.0])
+            d = shapes.setdefault(f"{kind} {shape[0]}x{shape[1]}x{shape[2]} {sym}", [0, 0.0, 0.0, 0.0])
             d[0] += 1
             d[1] += ms
             d[2] += fl
+            d[3] += nb
         d = by.setdefault(sym, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
         d["launches"] += 1
         d["ms"] += ms
@@ -184,15 +187,30 @@ def _roofline_from(rec, step_ms=None):
     total_ms = sum(d["ms"] for d in by.values())
     scale = min(1.0, step_ms / total_ms) if step_ms else 1.0
     if os.environ.get("VST_BENCH_SHAPES"):
-        for key, (n, ms, fl) in sorted(shapes.items(), key=lambda kv: -kv[1][1]):
+        for key, (n, ms, fl, nb) in sorted(shapes.items(), key=lambda kv: -kv[1][1]):
             print(f"[shape] {ms:8.3f} ms {n:4d}x {fl / (ms * 1e-3) / 1e12:7.1f} TF  {key}", file=sys.stderr)
-    # north-star view: the fused base + UnZipLoRA projection GEMMs (q/k/v, out, cross q) per shape
+    # north-star view: the fused base + UnZipLoRA projection GEMMs (q/k/v, out) and attn2 (to_q + UnZipLoRA + the
+    # text attention) per shape.  frac is against the 2.5 PF MFMA peak (the north star's measure); each entry also
+    # carries its roofline bound: the MFMA time floor (flops / 2.5 PF) against the HBM floor (algorithmic bytes /
+    # 8 TB/s, and at the measured 6.3 TB/s) -- the 32^2 out-projection moves more bytes than its flops cover
     lora = {}
-    for key, (n, ms, fl) in shapes.items():
-        if key.startswith("gemm_lora "):
-            lora[key.split()[1]] = {"launches": n, "ms_per_step": round(ms, 3),
-                                   "tflops": round(fl / (ms * 1e-3) / 1e12, 1),
-                                   "frac": round(fl / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4)}
+    for key, (n, ms, fl, nb) in shapes.items():
+        kind = key.split()[0]
+        if kind in ("gemm_lora", "gemm_xattn"):
+            per = ms / n * 1e3  # us per launch
+            t_mfma = fl / n / (PEAK_BF16_TFLOPS * 1e12) * 1e6
+            t_hbm = nb / n / (PEAK_HBM_GBS * 1e9) * 1e6
+            t_hbm_meas = nb / n / (HBM_MEASURED_GBS * 1e9) * 1e6
+            name = key.split()[1] + (" xattn" if kind == "gemm_xattn" else "")
+            lora[name] = {"launches": n, "ms_per_step": round(ms, 3), "us_per_launch": round(per, 2),
+                          "tflops": round(fl / (ms * 1e-3) / 1e12, 1),
+                          "frac": round(fl / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
+                          "alg_mb_per_launch": round(nb / n / 1e6, 1),
+                          "bound": "mfma" if t_mfma >= t_hbm else "hbm",
+                          "floor_us": round(max(t_mfma, t_hbm), 2),
+                          "roof_frac": round(max(t_mfma, t_hbm) / per, 4),
+                          "roof_frac_measured_hbm": round(max(t_mfma * PEAK_BF16_TFLOPS / MFMA_MEASURED_TFLOPS,
+                                                              t_hbm_meas) / per, 4)}
     dom_sym, dom = max(by.items(), key=lambda kv: kv[1]["ms"])
     mfma = dom["flops"] > 0
     if mfma:
