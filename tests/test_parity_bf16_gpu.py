@@ -183,6 +183,63 @@ def test_configs2_sdxl_f16_per_layer(cuda, sdxl_r8, exact_fp32):
     _gate_layers(cuda, R.rec, P, "configs[2]")
 
 
+def test_configs2_motion_attention_fused_vs_two_launches(cuda, sdxl_r8, exact_fp32):
+    """the motion modules' frame attention runs inside its q/k/v GEMM (vst_gemm_temporal_attention) by
+    default.  At configs[2]'s shapes (16 frames, 64x64 latent: the 64^2 and 32^2 motion levels fuse) every motion
+    module is run twice on its own recorded bf16 input -- fused (VST_TATTN=1) and as q/k/v GEMM + vst_temporal_attention
+    (VST_TATTN=0) -- and both are replayed through the bf16 emulation: each path within the per-layer motion gate
+    (max(1e-3, 3 x the reassociation floor)), and fused vs two launches within the kernel tolerance 2e-3."""
+    from oracle import unet as O
+    from video_style_transfer_amd import kernels as K
+    from video_style_transfer_amd import unet_motion as U
+    cfg, unet, P = sdxl_r8
+    lat, enc, pooled, tids = _inputs(cfg, 1, 16, 64, 37)
+    t = torch.tensor([401.0])
+    kw = dict(added_cond_kwargs={"text_embeds": pooled.to(cuda), "time_ids": tids.to(cuda)})
+    with _Recorder(unet) as R:
+        unet(lat.to(cuda), t.to(cuda), enc.to(cuda), **kw)
+    mods = dict(unet.named_modules())
+    Pd = _on(cuda, P)
+    fails, n_fused = [], 0
+    floors = {}
+    saved = os.environ.get("VST_TATTN")
+    try:
+        with torch.no_grad():
+            for kind, name, a, y_fused in R.rec:
+                if kind != "motion":
+                    continue
+                mod, HW = mods[name], a["HW"]
+                H = W = int(round(HW ** 0.5))
+                x = a["x"].to(cuda, BF)
+                ctx = U.FwdCtx(B=a["nclip"], F=a["F"], emb_silu=None, enc=None, cross_kwargs={})
+                with K.row_invariant():  # (as forward_tokens runs it)
+                    os.environ["VST_TATTN"] = "0"
+                    y_two = mod.run(x, a["nclip"] * a["F"], H, W, ctx).float().cpu()
+                    os.environ["VST_TATTN"] = "1"
+                    y_re = mod.run(x, a["nclip"] * a["F"], H, W, ctx).float().cpu()
+                assert torch.equal(y_re, y_fused), name  # (the recorded forward ran the default path)
+                ad = _on(cuda, a)
+                ref = _replay(Pd, "motion", name, ad, O.LoRAState())
+                key = y_fused.shape[1]
+                if key not in floors:
+                    floors[key] = _floor(lambda: _replay(Pd, "motion", name, ad, O.LoRAState()))[1]
+                gate = max(1e-3, 3 * floors[key])
+                e_f, e_t, e_ft = rel(y_fused, ref)[0], rel(y_two, ref)[0], rel(y_fused, y_two)[0]
+                fused = not torch.equal(y_fused, y_two)
+                n_fused += fused
+                log(f"[tattn] {name:40s} HW={HW:5d} fused vs emulation {e_f:.2e} | two launches {e_t:.2e} | "
+                    f"fused vs two {e_ft:.2e} (gate {gate:.2e}, floor {floors[key]:.2e}, paths differ: {fused})")
+                if e_f > gate or e_t > gate or e_ft > 2e-3:
+                    fails.append((name, e_f, e_t, e_ft, gate))
+    finally:
+        if saved is None:
+            os.environ.pop("VST_TATTN", None)
+        else:
+            os.environ["VST_TATTN"] = saved
+    assert n_fused == 10, n_fused  # the five 64^2 and five 32^2 motion modules take the fused path
+    assert not fails, fails
+
+
 def _gate_layers(cuda, rec, P, tag, report_only=()):
     """Replay every recorded layer through the emulation on its own bf16 input; a layer passes when rel_l2 <=
     max(1e-3, 3 x the fixed-probe floor of the first layer of its kind and width that exceeds 1e-3), rel_max <= 1.6e-2.

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Same-box A/B of the whole denoise step over library builds (round 5): bash tools/gpu_r5_stepab.sh base new xu ...
+# "new" = the in-tree .so, any other name = abl/libvst_<name>.so.  Builds alternate in the order given.
+set -o pipefail
+export TMPDIR=/tmp PYTHONUNBUFFERED=1
+mkdir -p gpurun_out
+i=0
+for tag in "$@"; do
+  i=$((i+1))
+  if [ "$tag" = new ]; then unset VST_LIB_AB; else export VST_LIB_AB=abl/libvst_$tag.so; fi
+  timeout -k 10 300 python -u bench.py --steps 15 --warmup 3 --no-cpu-baseline --no-peaks --no-vae \
+    > gpurun_out/stepab_${i}_$tag.json 2> gpurun_out/stepab_${i}_$tag.err || { tail -20 gpurun_out/stepab_${i}_$tag.err; exit 1; }
+  python - "gpurun_out/stepab_${i}_$tag.json" "$tag" <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+k = d["kernels"]
+print(sys.argv[2], "ms/step", d["ms_per_step"], "|", "  ".join(f"{n} {v['ms_per_step']:.2f}" for n, v in list(k.items())[:8]), flush=True)
+print("   fused:", {s: v["us_per_launch"] for s, v in d["roofline"]["fused_lora_gemms"].items()}, flush=True)
+PY
+done

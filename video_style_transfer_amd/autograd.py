@@ -330,21 +330,19 @@ class TemporalAttentionFn(torch.autograd.Function):
 
 class GroupNormFn(torch.autograd.Function):
     """GroupNorm (+SiLU) over `nsamples` groups of `rows_per_sample` token rows (the motion module's clip-wide GN:
-    rows_per_sample = F*H*W, frames = F; per-frame GN: H*W) with the HIP forward (vst_groupnorm, or for a clip-wide
-    GN the inference path's per-frame partials, vst_groupnorm_frame_partials / _apply_partials) and backward
-    (vst_groupnorm_bwd)."""
+    rows_per_sample = F*H*W, frames = F; per-frame GN: H*W) with the HIP forward (vst_groupnorm) and backward
+    (vst_groupnorm_bwd), which compute the same statistics."""
 
     @staticmethod
     def forward(ctx, x2d, gamma, beta, nsamples: int, rows_per_sample: int, groups: int, eps: float, silu: bool,
                 frames: int = 1):
         x2d = x2d.to(BF16).contiguous()
         g32, b32 = gamma.detach().float().contiguous(), beta.detach().float().contiguous()
-        if frames > 1 and not silu:
-            hw = rows_per_sample // frames
-            part = K.group_norm_frame_partials(x2d, nsamples * frames, hw, groups)
-            y = K.group_norm_apply_partials(x2d, nsamples, frames, hw, groups, eps, g32, b32, part, 1)
-        else:
-            y = K.group_norm(x2d, nsamples, rows_per_sample, groups, eps, g32, b32, silu=silu)
+        # vst_groupnorm for every GroupNorm here, the clip-wide motion GN included: its statistics are those
+        # vst_groupnorm_bwd recomputes, so forward output and backward agree to the bit on mean / rstd (ADVICE r4; the
+        # per-frame partials of the inference path, which a frame-sharded forward needs, merge in another order).
+        # `frames` is kept for the call signature.
+        y = K.group_norm(x2d, nsamples, rows_per_sample, groups, eps, g32, b32, silu=silu)
         ctx.save_for_backward(x2d, gamma, beta)
         ctx.cfg = (nsamples, rows_per_sample, groups, eps, silu)
         return y
