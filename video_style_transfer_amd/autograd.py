@@ -330,19 +330,27 @@ class TemporalAttentionFn(torch.autograd.Function):
 
 class GroupNormFn(torch.autograd.Function):
     """GroupNorm (+SiLU) over `nsamples` groups of `rows_per_sample` token rows (the motion module's clip-wide GN:
-    rows_per_sample = F*H*W, frames = F; per-frame GN: H*W) with the HIP forward (vst_groupnorm) and backward
-    (vst_groupnorm_bwd), which compute the same statistics."""
+    rows_per_sample = F*H*W, frames = F; per-frame GN: H*W) with the HIP forward (vst_groupnorm, or for a clip-wide
+    GN the inference path's per-frame partials, vst_groupnorm_frame_partials / _apply_partials) and backward
+    (vst_groupnorm_bwd)."""
 
     @staticmethod
     def forward(ctx, x2d, gamma, beta, nsamples: int, rows_per_sample: int, groups: int, eps: float, silu: bool,
                 frames: int = 1):
         x2d = x2d.to(BF16).contiguous()
         g32, b32 = gamma.detach().float().contiguous(), beta.detach().float().contiguous()
-        # vst_groupnorm for every GroupNorm here, the clip-wide motion GN included: its statistics are those
-        # vst_groupnorm_bwd recomputes, so forward output and backward agree to the bit on mean / rstd (ADVICE r4; the
-        # per-frame partials of the inference path, which a frame-sharded forward needs, merge in another order).
-        # `frames` is kept for the call signature.
-        y = K.group_norm(x2d, nsamples, rows_per_sample, groups, eps, g32, b32, silu=silu)
+        # (ADVICE r4 low, not taken: vst_groupnorm_bwd recomputes mean / rstd in its own chunking, so for the clip-wide
+        # motion GroupNorm the backward's statistics can differ from these fp64-merged ones by fp32 ulps.  Moving the
+        # forward to vst_groupnorm with the backward's statistics in its chunking was built and measured in round 5:
+        # it moves single tiny-UNet gradients (tensors of a few hundred elements) by up to 2.5x their CPU bf16-autocast
+        # yardstick error -- the gradients of this test are that sensitive to ulp-level changes -- while the
+        # production-size gradients are unaffected; the inference path's bits are kept, profiles/r5_gn_bwd_stats.log.)
+        if frames > 1 and not silu:
+            hw = rows_per_sample // frames
+            part = K.group_norm_frame_partials(x2d, nsamples * frames, hw, groups)
+            y = K.group_norm_apply_partials(x2d, nsamples, frames, hw, groups, eps, g32, b32, part, 1)
+        else:
+            y = K.group_norm(x2d, nsamples, rows_per_sample, groups, eps, g32, b32, silu=silu)
         ctx.save_for_backward(x2d, gamma, beta)
         ctx.cfg = (nsamples, rows_per_sample, groups, eps, silu)
         return y

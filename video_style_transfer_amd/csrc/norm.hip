@@ -1072,9 +1072,7 @@ static inline size_t gnb_floats(int nsamples, int rows_per_sample, int groups, i
   const size_t nchunk = gn_nchunk(nsamples, rows_per_sample);
   const size_t a4 = 4;
   auto up = [&](size_t n) { return (n + a4 - 1) / a4 * a4; };
-  const size_t partf = std::max(gn_part_floats(nsamples, rows_per_sample, groups),
-                                 gn_part_floats_rows(nsamples, rows_per_sample, groups));
-  return up(partf) + up((size_t)2 * nsamples * C)  // part (stats chunks: the forward's), scale/shift
+  return up(gn_part_floats(nsamples, rows_per_sample, groups)) + up((size_t)2 * nsamples * C)  // part, scale/shift
          + up((size_t)2 * nsamples * groups) + up((size_t)nsamples * nchunk * 2 * C)           // stats, part2
          + up((size_t)2 * nsamples * C) + up((size_t)3 * nsamples * C);                        // chsum, coef
 }
@@ -1095,21 +1093,17 @@ extern "C" int vst_groupnorm_bwd(const void* x, int ldx, const void* g, int ldg,
   const int nchunk = gn_nchunk(nsamples, rows_per_sample);
   const int CH = C / 8, rps = gn_rps(C);
   auto up = [](size_t n) { return (n + 3) / 4 * 4; };
-  // the statistics in vst_groupnorm's chunking (gn_rpc_rows: rows per sample only), so the mean / rstd used here are
-  // the forward's to the bit; the gradient sums and the apply keep the launch-wide chunking (parallelism)
-  const int rpc_s = gn_rpc_rows(rows_per_sample), nchunk_s = gn_nchunk_rows(rows_per_sample);
   float* part = (float*)workspace;
-  float* scale = part + up(std::max(gn_part_floats(nsamples, rows_per_sample, groups),
-                                    gn_part_floats_rows(nsamples, rows_per_sample, groups)));
+  float* scale = part + up(gn_part_floats(nsamples, rows_per_sample, groups));
   float* shift = scale + nsamples * (size_t)C;
   float* stats = scale + up((size_t)2 * nsamples * C);
   float* part2 = stats + up((size_t)2 * nsamples * groups);
   float* chsum = part2 + up((size_t)nsamples * nchunk * 2 * C);
   float* coef = chsum + up((size_t)2 * nsamples * C);
   const size_t lds = (size_t)2 * rps * C * sizeof(float);
-  hipLaunchKernelGGL(gn_stats_kernel, dim3(nchunk_s, nsamples), dim3(rps * CH), lds, s, (const bf16_t*)x, ldx, C,
-                     (const bf16_t*)nullptr, 0, 0, rows_per_sample, rpc_s, groups, part);
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3(nsamples * groups), dim3(64), 0, s, part, nchunk_s, rows_per_sample,
+  hipLaunchKernelGGL(gn_stats_kernel, dim3(nchunk, nsamples), dim3(rps * CH), lds, s, (const bf16_t*)x, ldx, C,
+                     (const bf16_t*)nullptr, 0, 0, rows_per_sample, rpc, groups, part);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(nsamples * groups), dim3(64), 0, s, part, nchunk, rows_per_sample,
                      groups, C / groups, eps, gamma, beta, scale, shift, C, stats);
   hipLaunchKernelGGL(gn_bwd_sums_kernel, dim3(nchunk, nsamples), dim3(rps * CH), lds, s, (const bf16_t*)x, ldx,
                      (const bf16_t*)g, ldg, C, rows_per_sample, rpc, scale, shift, silu_act, part2);
