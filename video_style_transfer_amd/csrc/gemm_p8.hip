@@ -589,7 +589,10 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   // bare MFMAs and 100-185 in a segment that carries 16 ds_read_b128, MI355X_MICROARCH.md constants table; the loop
   // ablations put the load segments, not the MFMAs, on the critical path).  Same DMAs in the same order per wave, so
   // every counted wait keeps its count; the slots they refill were read one interval earlier still.
-#ifdef VST_P8_DMM
+  // Off: in isolation the LoRA kernels gained 1-2 % per launch with it and the plain GEMMs lost 1-22 %
+  // (profiles/r5_ab_dma_in_mfma_negative.txt); on the LoRA kernels alone the whole step was 0.2 ms slower in two
+  // alternations (profiles/r5_ab_dma_in_mfma_lora_negative.txt).  VST_P8_DMM builds it everywhere (A/B).
+#if defined(VST_P8_DMM)
   constexpr bool DMM = true;
 #else
   constexpr bool DMM = false;
