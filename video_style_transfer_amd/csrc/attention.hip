@@ -243,6 +243,200 @@ __global__ __launch_bounds__(256, 2) void spatial_attn_kernel(
 }
 
 // ---------------------------------------------------------------------------------
+// Self-attention over long key ranges (the 16x16 and 32x32 levels: 256 / 1024 keys), the default for
+// vst_spatial_attention's self-attention: spatial_attn_kernel<0>'s arithmetic (S^T = K.Q^T with the query on the lane,
+// online softmax against the running max, P rounded to bf16 unnormalised, O^T = V^T.P^T from transposed V reads, K/V
+// tiles double-buffered through registers, 4 waves x 32 queries) without its causal mask, whose code spilled 31 SGPRs
+// into VGPR lanes (~29 v_readlane / v_writelane per 64-key tile).  32x32: 148-156 -> 145-147 us, 16x16: 26.2-26.6 ->
+// 25.4 us (profiles/r5_ab_sa_self.txt).  At head_dim 64 the softmax VALU, not the MFMA, bounds the loop (per tile and
+// wave 32 MFMAs = 512 cycles against ~700-1,100 cycles of vector issue).  Not kept (same file):
+//  - a deferred rescale (the running max moves only when a tile's max exceeds it by 2^8; the alpha exp2s and the 32 O
+//    multiplies skipped): 32x32 135-142 us, but a row's largest P is then exp2(d), 0 < d <= 8, rounded to bf16
+//    instead of an exact 1.0, and peaked rows lose accuracy (a configs[2] block rel_max 1.13e-2 -> 1.70e-2 against the
+//    1.6e-2 gate, rel_l2 2.43e-3 -> 2.99e-3);
+//  - 8 waves x 32 queries (one K/V fill per 256 queries): 128 VGPRs with spills, or one workgroup per CU; 16x16 31 us;
+//  - S_{t+1} issued before tile t's softmax (software pipelining inside the wave): 208 VGPRs, 2 waves per SIMD, 32x32
+//    169 us.
+template <int NW>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(3))) void sa_self_kernel(
+    const bf16_t* __restrict__ Q, int ldq, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V, int ldkv,
+    bf16_t* __restrict__ O, int ldo, int nbatch, int heads, int Nq, int Nk, float scale_log2, uint32_t q_bytes,
+    uint32_t kv_bytes) {
+  constexpr int NCH = 512 / (NW * 64);  // 16-B chunks per thread and operand per tile (64 rows x 8 chunks)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nqb = (Nq + NW * 32 - 1) / (NW * 32);
+  const int wg = xcd_remap(blockIdx.x, nqb * heads * nbatch);
+  const int qblk = wg % nqb;
+  const int bh = wg / nqb;
+  const int h = bh % heads, b = bh / heads;
+  const int fr = lane & 15, g = lane >> 4;
+
+  const auto rq = make_rsrc(Q, q_bytes);
+  const auto rk = make_rsrc(K, kv_bytes);
+  const auto rv = make_rsrc(V, kv_bytes);
+
+  bf16x8 qf[2][2];
+  const int qbase = qblk * (NW * 32) + wid * 32;
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int q = qbase + qb * 16 + fr;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int off = q < Nq ? ((b * Nq + q) * ldq + h * 64 + kk * 32 + g * 8) * 2 : kOOB;
+      qf[qb][kk] = __builtin_bit_cast(bf16x8, buf_load16(rq, off));
+    }
+  }
+
+  const int sc = tid & 7, sr = tid >> 3;  // rows sr + NW * 8 * i
+  u32x4 kreg[NCH], vreg[NCH];
+  const int kvrow0 = b * Nk;
+  auto load_kv = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int key = t * SA_KT + sr + NW * 8 * i;
+      const int off = key < Nk ? ((kvrow0 + key) * ldkv + h * 64 + sc * 8) * 2 : kOOB;
+      kreg[i] = buf_load16(rk, off);
+      vreg[i] = buf_load16(rv, off);
+    }
+  };
+  auto store_kv = [&](int buf) {
+    char* Ks = smem + buf * 2 * SA_TILE;
+    char* Vs = Ks + SA_TILE;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int row = sr + NW * 8 * i;
+      *reinterpret_cast<u32x4*>(Ks + k_off(row, sc)) = kreg[i];
+      *reinterpret_cast<u32x4*>(Vs + v_off(row, sc)) = vreg[i];
+    }
+  };
+
+  f32x4 o[4][2];
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) o[d][qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float mrun[2] = {-INFINITY, -INFINITY};
+  float mb[2] = {0.f, 0.f};  // mrun * scale_log2
+  float lrun[2] = {0.f, 0.f};
+
+  const int nt = (Nk + SA_KT - 1) / SA_KT;
+  int voff[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) {
+    const int li = lane & 15, r0 = g * 4 + (li >> 2), col = db * 16 + (li & 3) * 4;
+    voff[db] = v_off(r0, col >> 3) + (col & 7) * 2;
+  }
+  load_kv(0);
+  store_kv(0);
+  __syncthreads();
+
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nt) load_kv(t + 1);
+    const char* Ks = smem + cur * 2 * SA_TILE;
+    const char* Vs = Ks + SA_TILE;
+
+    f32x4 s[4][2];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      bf16x8 kf[2];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        kf[kk] = *reinterpret_cast<const bf16x8*>(Ks + k_off(kt * 16 + fr, kk * 4 + g));
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        f32x4 a{0.f, 0.f, 0.f, 0.f};
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[0], qf[qb][0], a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[1], qf[qb][1], a, 0, 0, 0);
+        s[kt][qb] = a;
+      }
+    }
+    if ((t + 1) * SA_KT > Nk) {
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bool dead = t * SA_KT + kt * 16 + g * 4 + i >= Nk;
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb)
+            if (dead) s[kt][qb][i] = -INFINITY;
+        }
+    }
+    float mx[2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      float m = s[0][qb][0];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) m = fmaxf(m, s[kt][qb][i]);
+      mx[qb] = group_max(m);
+    }
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const float mnew = fmaxf(mrun[qb], mx[qb]);
+      const float alpha = fast_exp2((mrun[qb] - mnew) * scale_log2);
+      mrun[qb] = mnew;
+      mb[qb] = mnew * scale_log2;
+      lrun[qb] *= alpha;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) o[d][qb] *= alpha;
+    }
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      float ls = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float pv = fast_exp2(fmaf(s[kt][qb][i], scale_log2, -mb[qb]));
+          s[kt][qb][i] = pv;
+          ls += pv;
+        }
+      lrun[qb] += ls;
+    }
+    bf16x8 pf[2][2];
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+        pf[st][qb] = pack_p8(s[2 * st][qb][0], s[2 * st][qb][1], s[2 * st][qb][2], s[2 * st][qb][3],
+                             s[2 * st + 1][qb][0], s[2 * st + 1][qb][1], s[2 * st + 1][qb][2], s[2 * st + 1][qb][3]);
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const char* vp = Vs + voff[db];
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const bf16x8 vf = cat_tr(ds_read_tr(vp + st * 4096), ds_read_tr(vp + st * 4096 + 2048));
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+          o[db][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[st][qb], o[db][qb], 0, 0, 0);
+      }
+    }
+    if (t + 1 < nt) store_kv(cur ^ 1);
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    float l = lrun[qb];
+    l += __shfl_xor(l, 16);
+    l += __shfl_xor(l, 32);
+    const float inv = 1.0f / l;
+    const int q = qbase + qb * 16 + fr;
+    if (q >= Nq) continue;
+    bf16_t* orow = O + (size_t)(b * Nq + q) * ldo + h * 64;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const f32x4 v = o[db][qb] * inv;
+      u32x2 w{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+      *reinterpret_cast<u32x2*>(orow + db * 16 + g * 4) = w;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
 // Temporal attention.  NT = number of 16-frame tiles (1: F<=16, 2: F<=32); D = head dim.
 // A workgroup holds `blockDim.x / 64` consecutive units, i.e. all heads of one (clip, pixel) when they fit: the
 // heads' 16-B q/k/v/o segments of a token row then meet in one CU's L1 instead of splitting cache lines
@@ -971,6 +1165,21 @@ extern "C" int vst_spatial_attention(const void* q, int ldq, const void* k, cons
 #define VST_SA_LAUNCH(P)                                                                                         \
   hipLaunchKernelGGL(spatial_attn_kernel<P>, grid, dim3(256), lds, st, (const bf16_t*)q, ldq, (const bf16_t*)k, \
                      (const bf16_t*)v, ldkv, (bf16_t*)o, ldo, nbatch, heads, Nq, Nk, kv_div, sl2, qb, kvb_v, lse)
+  static int self_env = -1;  // VST_SA_SELF=0: the long self-attention on spatial_attn_kernel<0> (A/B diagnostics)
+  if (self_env < 0) {
+    const char* e = getenv("VST_SA_SELF");
+    self_env = e ? atoi(e) : 1;
+  }
+  // inference only (no logsumexp requested): the training forward stays on spatial_attn_kernel<0>, the kernel its
+  // gradient gates were fixed against -- an ulp-level change of this forward (fma contraction) moved the SDXL
+  // gradient error median 4.18e-2 -> 5.21e-2 against the same fp32 reference (test_training_gpu.py, r5)
+  if (pre == 0 && kv_div == 1 && self_env && !lse) {
+    const dim3 g2(((Nq + 127) / 128) * heads * nbatch);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(sa_self_kernel<4>), g2, dim3(256), SA_LDS, st, (const bf16_t*)q, ldq,
+                       (const bf16_t*)k, (const bf16_t*)v, ldkv, (bf16_t*)o, ldo, nbatch, heads, Nq, Nk, sl2, qb,
+                       kvb_v);
+    return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+  }
   switch (pre) {
     case 1: VST_SA_LAUNCH(1); break;
     case 2: VST_SA_LAUNCH(2); break;
