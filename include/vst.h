@@ -116,6 +116,13 @@ int vst_conv3x3_ex(const void* x1, int C1, const void* x2, int C2, int nimg, int
                    const void* Wt, int Cout, const float* bias, const float* row_bias, int row_bias_div,
                    int ld_row_bias, const void* R, int ldr, void* out, int ldc, int tile, int splits, void* workspace,
                    size_t ws_bytes, void* stream);
+/* + the GroupNorm column statistics of the stored output, colstat [ceil(M/128)][Cout][2] fp32 (sum, sum of squares
+ * per 128-row tile and channel) for vst_groupnorm_colstat; returns 3 (unsupported, nothing launched) unless the
+ * conv runs on the 8-phase kernel's 128x320 tiles (Cout % 320 == 0). */
+int vst_conv3x3_colstat(const void* x1, int C1, const void* x2, int C2, int nimg, int H, int W, int stride,
+                        int upsample, const void* Wt, int Cout, const float* bias, const float* row_bias,
+                        int row_bias_div, int ld_row_bias, const void* R, int ldr, void* out, int ldc,
+                        float* colstat, void* stream);
 
 /* Spatial SDPA, head_dim 64: replaces F.scaled_dot_product_attention in
  * AnimateDiffAttnProcessor2_0.__call__ (animatediff/attention_processor.py:78-80).  K/V row
@@ -148,6 +155,15 @@ size_t vst_groupnorm_workspace_bytes(int nsamples, int rows_per_sample, int grou
 int vst_groupnorm(const void* x1, int ld1, int C1, const void* x2, int ld2, int C2, int nsamples,
                   int rows_per_sample, int groups, float eps, const float* gamma, const float* beta, int silu_act,
                   void* y, int ldy, void* workspace, void* stream);
+/* Column statistics of x [M, C] (C % 8 == 0) in the arithmetic of vst_conv3x3_colstat's epilogue, cs
+ * [ceil(M/128)][C][2] fp32: for a GroupNorm input whose producer did not write them (same bits if it had). */
+int vst_colstat(const void* x, int ldx, int M, int C, float* cs, void* stream);
+/* vst_groupnorm with its statistics from the column statistics the producing conv wrote (vst_conv3x3_colstat;
+ * cs2 for x2's channels), so the GroupNorm does not read x for them: rows_per_sample % 128 == 0. */
+int vst_groupnorm_colstat(const void* x1, int ld1, int C1, const float* cs1, const void* x2, int ld2, int C2,
+                          const float* cs2, int nsamples, int rows_per_sample, int groups, float eps,
+                          const float* gamma, const float* beta, int silu_act, void* y, int ldy, void* workspace,
+                          void* stream);
 
 /* GroupNorm (+SiLU) over NHWC samples of rows_per_sample rows; a frame's statistics depend only on its own rows
  * (the chunking is a function of rows_per_sample, not of how many samples share the launch). */

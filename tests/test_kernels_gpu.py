@@ -515,6 +515,54 @@ def test_group_norm(cuda, K, ns, rps, C1, C2, silu):
     check(out, ref, name="groupnorm")
 
 
+def test_conv_colstat_groupnorm(cuda, K, monkeypatch):
+    """GroupNorm statistics from the producing convs' epilogues (vst_conv3x3_colstat -> vst_groupnorm_colstat):
+    the conv output is the same bits with or without the statistics; the column statistics equal fp64 sums of the
+    stored bf16 output per 128-row tile and vst_colstat's bit for bit; the GroupNorm over [x1 | x2] (an up block's
+    concat, groups straddling the seam) matches the statistics-pass GroupNorm to within one bf16 rounding and torch
+    fp32."""
+    monkeypatch.setenv("VST_GN_COLSTAT", "1")  # (opt-in in the step)
+    g = torch.Generator().manual_seed(5)
+    n, H, W = 32, 32, 32  # 32768 rows: the 8-phase 128x320 conv path
+    outs, stats = [], []
+    xin = rnd(n * H * W, 320, gen=g).to(cuda)
+    r = rnd(n * H * W, 640, gen=g).to(cuda)
+    for Co, res in ((640, r), (320, None)):
+        w = rnd(Co, 320, 3, 3, scale=(9 * 320) ** -0.5, gen=g)
+        b = torch.randn(Co, generator=g) * 0.1
+        wd, bd = wflat(w).to(cuda), b.to(cuda)
+        plain = K.conv3x3(xin, n, H, W, wd, bd, residual=res)
+        y = K.conv3x3(xin, n, H, W, wd, bd, residual=res, colstat=True)
+        assert torch.equal(y, plain), Co
+        cs = K.colstat_of(y)
+        assert cs is not None and cs.shape == (n * H * W // 128, Co, 2)
+        yt = y.double().view(-1, 128, Co)
+        ref = torch.stack([yt.sum(1), (yt * yt).sum(1)], -1)
+        torch.testing.assert_close(cs.double(), ref, rtol=1e-5, atol=1e-3)
+        outs.append(y)
+        stats.append(cs)
+    x1, x2 = outs
+    C = 960
+    gam = (torch.rand(C, generator=g) + 0.5).to(cuda)
+    bet = (torch.randn(C, generator=g) * 0.1).to(cuda)
+    want = K.group_norm(x1, n, H * W, 32, 1e-5, gam, bet, silu=True, x2=x2)
+    got = K.group_norm(x1, n, H * W, 32, 1e-5, gam, bet, silu=True, x2=x2, colstat=(stats[0], stats[1]))
+    d = (got.float() - want.float()).abs()
+    assert (d <= want.float().abs() * 2 ** -7 + 1e-6).all(), d.max()
+    assert (got == want).float().mean() > 0.98
+    xs = torch.cat([x1, x2], 1).float().cpu().view(n, H * W, C).permute(0, 2, 1)
+    ref = F.silu(F.group_norm(xs, 32, gam.cpu(), bet.cpu(), 1e-5)).permute(0, 2, 1).reshape(-1, C)
+    check(got.cpu(), ref, name="groupnorm_colstat")
+    # vst_colstat restates the epilogue's arithmetic: the same bits as the conv wrote
+    for y, c in zip(outs, stats):
+        assert torch.equal(K.colstat(y), c)
+    # a tensor modified after its conv loses its statistics
+    x2.add_(0)
+    assert K.colstat_of(x2) is None and K.colstat_of(x1) is not None
+    K.colstat_reset()
+    assert K.colstat_of(x1) is None
+
+
 @pytest.mark.parametrize("P,nclip,Fr,HW,C", [(1, 2, 16, 256, 1280), (2, 2, 16, 256, 1280), (4, 2, 16, 64, 320),
                                               (8, 1, 32, 576, 640), (2, 3, 4, 100, 64)])
 def test_group_norm_frame_partials_sharded(cuda, K, P, nclip, Fr, HW, C):

@@ -47,6 +47,10 @@ SIGNATURES = {
     "vst_groupnorm_apply_partials": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _I, _F, _P, _P, _I, _P, _I, _P, _P]),
     "vst_permute_rows": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "vst_groupnorm": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _F, _P, _P, _I, _P, _I, _P, _P]),
+    "vst_colstat": (_I, [_P, _I, _I, _I, _P, _P]),
+    "vst_groupnorm_colstat": (_I, [_P, _I, _I, _P, _P, _I, _I, _P, _I, _I, _I, _F, _P, _P, _I, _P, _I, _P, _P]),
+    "vst_conv3x3_colstat": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _I, _P, _I, _P, _I, _P,
+                                 _P]),
     "vst_layernorm_lora": (_I, [_P, _I, _I, _I, _P, _P, _F, _P, _I, _P, _I, _P, _I, _P]),
     "vst_layernorm": (_I, [_P, _I, _I, _I, _P, _P, _F, _P, _I, _I, _P, _I, _P]),
     "vst_add_row_table": (_I, [_P, _I, _I, _I, _P, _I, _I, _P, _I, _P]),

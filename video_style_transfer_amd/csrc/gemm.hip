@@ -1096,7 +1096,7 @@ extern "C" int vst_gemm(const void* A, int lda, const void* A2, int lda2, int K1
 static int conv3x3_impl(const void* x1, int C1, const void* x2, int C2, int nimg, int H, int W, int stride,
                         int upsample, int pad0, const void* Wt, int Cout, const float* bias, const float* row_bias,
                         int row_bias_div, int ld_row_bias, const void* R, int ldr, void* out, int ldc, int tile,
-                        int splits, void* workspace, size_t ws_bytes, void* stream) {
+                        int splits, void* workspace, size_t ws_bytes, void* stream, float* colstat = nullptr) {
   if (!x1 || !Wt || !out || nimg <= 0 || H <= 0 || W <= 0 || Cout <= 0) return VST_ERR_ARG;
   if (pad0 && (stride != 2 || H < 2 || W < 2)) return VST_ERR_ARG;
   if (stride != 1 && stride != 2) return VST_ERR_ARG;
@@ -1128,8 +1128,13 @@ static int conv3x3_impl(const void* x1, int C1, const void* x2, int C2, int nimg
   if (!vec) { tile = 2; splits = 1; }
   // 3x3 convs with both sources a multiple of 64 channels run on the 8-phase kernel (implicit im2col; 128x320 tiles
   // where Cout is a multiple of 320, else the projection policy's width); VST_P8_CONV=0 restores the ring kernel
-  if (vec && tile == 0 && splits <= 1 && p8_conv_env() && !(C1 & 63) && !((x2 ? C2 : 0) & 63) && !(a.N & 63) &&
-      p8_auto(a.M, a.N, a.K, false)) {
+  const bool p8 = vec && tile == 0 && splits <= 1 && p8_conv_env() && !(C1 & 63) && !((x2 ? C2 : 0) & 63) &&
+                  !(a.N & 63) && p8_auto(a.M, a.N, a.K, false);
+  if (colstat) {  // column statistics come from the 128x320 tiles' epilogue only
+    if (!p8 || a.N % 320) return VST_ERR_UNSUPPORTED;
+    a.colstat = colstat;
+  }
+  if (p8) {
     a.splits = 1;
     a.ablate = 0;
     a.group_m = gemm_group_env();
@@ -1146,6 +1151,19 @@ extern "C" int vst_conv3x3_ex(const void* x1, int C1, const void* x2, int C2, in
                               int splits, void* workspace, size_t ws_bytes, void* stream) {
   return conv3x3_impl(x1, C1, x2, C2, nimg, H, W, stride, upsample, 0, Wt, Cout, bias, row_bias, row_bias_div,
                       ld_row_bias, R, ldr, out, ldc, tile, splits, workspace, ws_bytes, stream);
+}
+
+// vst_conv3x3_ex + the GroupNorm column statistics of the output for a following vst_groupnorm_colstat:
+// colstat [ceil(M / 128)][Cout][2] fp32 = (sum, sum of squares) over each 128-row output tile of the stored bf16
+// values.  VST_ERR_UNSUPPORTED (nothing launched) unless the conv runs on the 8-phase kernel's 128x320 tiles
+// (Cout % 320 == 0, both sources multiples of 64 channels, default policy).
+extern "C" int vst_conv3x3_colstat(const void* x1, int C1, const void* x2, int C2, int nimg, int H, int W, int stride,
+                                   int upsample, const void* Wt, int Cout, const float* bias, const float* row_bias,
+                                   int row_bias_div, int ld_row_bias, const void* R, int ldr, void* out, int ldc,
+                                   float* colstat, void* stream) {
+  if (!colstat) return VST_ERR_ARG;
+  return conv3x3_impl(x1, C1, x2, C2, nimg, H, W, stride, upsample, 0, Wt, Cout, bias, row_bias, row_bias_div,
+                      ld_row_bias, R, ldr, out, ldc, 0, 1, nullptr, 0, stream, colstat);
 }
 
 // 3x3 stride-2 conv with padding (0,1,0,1): diffusers Downsample2D(padding=0) = F.pad(x, (0, 1, 0, 1)) + conv(k3, s2,

@@ -43,6 +43,9 @@ struct GemmArgs {
   // (p.C / p.ldc) is written in (clip, frame, pixel) rows
   int ta_hw, ta_heads, ta_d;
   float ta_scale_log2;
+  // GroupNorm column statistics of the stored output (tile_epilogue EPI 0 on 128x320 tiles, vst_conv3x3_colstat):
+  // colstat[m_tile][N] = (sum, sum of squares) over the tile's rows of the bf16 values written to C, fp32
+  float* colstat;
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) {

@@ -36,15 +36,35 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, char* smem, con
   constexpr int TOT = BM * CPR;
   constexpr int ITEMS = (TOT + Cfg::THREADS - 1) / Cfg::THREADS;
   const auto rr = make_rsrc(p.R ? p.R : p.Wt, p.R ? p.r_bytes : 0u);
+  // GroupNorm column statistics (128x320 conv tiles, p.colstat; gn_colstat_kernel restates the same arithmetic):
+  // the store pass then maps thread t to one 8-channel column (t mod 40) and rows t / 40 + 12 j, sums the stored bf16
+  // values and their squares in registers (fixed order), and the 12 row groups are added in order through the LDS.
+  constexpr bool CSTAT = EPI == 0 && BM == 128 && BN == 320;
+  constexpr int CS_RG = Cfg::THREADS / CPR, CS_RPT = (BM + CS_RG - 1) / CS_RG;  // 12 row groups, 11 rows each
+  constexpr int NIT = CSTAT && CS_RPT > ITEMS ? CS_RPT : ITEMS;
+  const bool cs = CSTAT && p.colstat;
+  // store-pass item k -> (tile row, 16-B chunk); false past the tile
+  auto item = [&](int k, int& row, int& cc) {
+    if (CSTAT && cs) {
+      cc = tid % CPR;
+      row = tid / CPR + CS_RG * k;
+      return tid / CPR < CS_RG && row < BM;
+    }
+    const int idx = tid + k * Cfg::THREADS;
+    row = idx / CPR;
+    cc = idx - row * CPR;
+    return k < ITEMS && idx < TOT;
+  };
   // residual chunks are fetched first (the fragment registers are dead now): their HBM latency
   // overlaps the bias add and the LDS staging below instead of stalling the store pass.
-  u32x4 res[EPI == 0 ? ITEMS : 1];
+  u32x4 res[EPI == 0 ? NIT : 1];
   if (EPI == 0 && p.R) {
 #pragma unroll
-    for (int k = 0; k < ITEMS; ++k) {
-      const int idx = tid + k * Cfg::THREADS;
-      const int row = idx / CPR, n = n0 + (idx - row * CPR) * 8, m = m0 + row;
-      res[k] = buf_load16(rr, (idx < TOT && m < p.M && n + 8 <= p.N) ? (m * p.ldr + n) * 2 : kOOB);
+    for (int k = 0; k < NIT; ++k) {
+      int row, cc;
+      const bool ok = item(k, row, cc);
+      const int n = n0 + cc * 8, m = m0 + row;
+      res[k] = buf_load16(rr, (ok && m < p.M && n + 8 <= p.N) ? (m * p.ldr + n) * 2 : kOOB);
     }
   }
   if (p.bias) {
@@ -125,13 +145,18 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, char* smem, con
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if constexpr (EPI == 0 || EPI == 3) {
+    float csa[CSTAT ? 8 : 1], csq[CSTAT ? 8 : 1];
+    if constexpr (CSTAT) {
 #pragma unroll
-    for (int k = 0; k < ITEMS; ++k) {
-      const int idx = tid + k * Cfg::THREADS;
-      const int row = idx / CPR, cc = idx - row * CPR;
+      for (int e = 0; e < 8; ++e) csa[e] = csq[e] = 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      int row, cc;
+      const bool ok = item(k, row, cc);
       const int m = m0 + row, n = n0 + cc * 8;
       const int nv = min(8, p.N - n);
-      if (idx >= TOT || m >= p.M || nv <= 0) continue;
+      if (!ok || m >= p.M || nv <= 0) continue;
       float v[8];
       unpack8(*reinterpret_cast<const u32x4*>(smem + row * LROW + cc * 16), v);
       if (EPI == 0 && p.rbias) {
@@ -152,12 +177,45 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, char* smem, con
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += r8[e];
         }
-        *reinterpret_cast<u32x4*>(p.C + (size_t)m * p.ldc + n) = pack8(v);
+        const u32x4 w = pack8(v);
+        *reinterpret_cast<u32x4*>(p.C + (size_t)m * p.ldc + n) = w;
+        if (CSTAT && cs) {  // the stored bits
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float lo = __uint_as_float(w[e] << 16), hi = __uint_as_float(w[e] & 0xffff0000u);
+            csa[2 * e] += lo;
+            csq[2 * e] = fmaf(lo, lo, csq[2 * e]);
+            csa[2 * e + 1] += hi;
+            csq[2 * e + 1] = fmaf(hi, hi, csq[2 * e + 1]);
+          }
+        }
       } else {
         for (int e = 0; e < nv; ++e) {
           float x = v[e];
           if (EPI == 0 && p.R) x += bf2f(p.R[(size_t)m * p.ldr + n + e]);
           p.C[(size_t)m * p.ldc + n + e] = f2bf(x);
+        }
+      }
+    }
+    if constexpr (CSTAT) {
+      if (cs) {
+        float* part = reinterpret_cast<float*>(smem);  // [CS_RG][BN][2], over the staged tile once every wave read it
+        static_assert(CS_RG * BN * 8 <= BM * LROW, "column partials over the staged tile");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        const int cc = tid % CPR, rg = tid / CPR;
+        if (rg < CS_RG) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            *reinterpret_cast<f32x2*>(part + (rg * BN + cc * 8 + e) * 2) = f32x2{csa[e], csq[e]};
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (tid < BN && n0 + tid < p.N) {
+          f32x2 t = *reinterpret_cast<const f32x2*>(part + tid * 2);
+#pragma unroll
+          for (int g = 1; g < CS_RG; ++g) t += *reinterpret_cast<const f32x2*>(part + (g * BN + tid) * 2);
+          *reinterpret_cast<f32x2*>(p.colstat + ((size_t)(m0 / BM) * p.N + n0 + tid) * 2) = t;
         }
       }
     }

@@ -140,6 +140,91 @@ __global__ __launch_bounds__(64) void gn_finalize_kernel(const float* __restrict
   }
 }
 
+// Column statistics of a bf16 tensor x [M, C] in the arithmetic of the 128x320 conv tiles' epilogue
+// (gemm_epilogue.h, p.colstat): per 128-row chunk and channel, 12 row groups (rows g, g + 12, ...) summed in row order
+// (sum += x, sumsq = fma(x, x, sumsq) in fp32), then the 12 groups added in order -- so a GroupNorm gets the same
+// statistics bits whether its input's producer wrote them or this kernel did.  Workgroup: 128 rows x 320 channels.
+__global__ __launch_bounds__(512) void gn_colstat_kernel(const bf16_t* __restrict__ x, int ldx, int M, int C,
+                                                         float* __restrict__ cs) {
+  constexpr int CPR = 40, RG = 12, RPT = 11;
+  __shared__ f32x2 part[RG][320];
+  const int tid = threadIdx.x, cc = tid % CPR, rg = tid / CPR;
+  const int m0 = blockIdx.x * 128, n0 = blockIdx.y * 320, n = n0 + cc * 8;
+  float a[8], q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = q[e] = 0.f;
+  if (rg < RG && n < C) {
+    u32x4 v[RPT];
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+      const int row = rg + RG * j, m = m0 + row;
+      v[j] = row < 128 && m < M ? *reinterpret_cast<const u32x4*>(x + (size_t)m * ldx + n) : u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+      const int row = rg + RG * j;
+      if (row >= 128 || m0 + row >= M) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float lo = __uint_as_float(v[j][e] << 16), hi = __uint_as_float(v[j][e] & 0xffff0000u);
+        a[2 * e] += lo;
+        q[2 * e] = fmaf(lo, lo, q[2 * e]);
+        a[2 * e + 1] += hi;
+        q[2 * e + 1] = fmaf(hi, hi, q[2 * e + 1]);
+      }
+    }
+  }
+  if (rg < RG) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) part[rg][cc * 8 + e] = f32x2{a[e], q[e]};
+  }
+  __syncthreads();
+  if (tid < 320 && n0 + tid < C) {
+    f32x2 t = part[0][tid];
+#pragma unroll
+    for (int g = 1; g < RG; ++g) t += part[g][tid];
+    *reinterpret_cast<f32x2*>(cs + ((size_t)blockIdx.x * C + n0 + tid) * 2) = t;
+  }
+}
+
+// GroupNorm statistics from the producing conv's column statistics (vst_conv3x3_colstat: per 128-row output tile and
+// channel, the sum and sum of squares of the stored bf16 values), so the GroupNorm's own statistics pass over x
+// disappears.  One 64-thread block per (sample, group) merges the sample's nchunk tiles x Cg channels in double,
+// in a fixed order (lane-strided, then the xor butterfly), and emits the same per-channel affine as
+// gn_finalize_kernel.  x2 (the channel concat of an up block): channels >= C1 read cs2.
+__global__ __launch_bounds__(64) void gn_finalize_colstat_kernel(const float* __restrict__ cs1, int C1,
+                                                                 const float* __restrict__ cs2, int C2, int nchunk,
+                                                                 int rows_per_sample, int groups, int Cg, float eps,
+                                                                 const float* __restrict__ gamma,
+                                                                 const float* __restrict__ beta,
+                                                                 float* __restrict__ scale, float* __restrict__ shift) {
+  const int s = blockIdx.x / groups, gi = blockIdx.x - s * groups;
+  const int lane = threadIdx.x;
+  const int C = C1 + C2;
+  double a = 0.0, q = 0.0;
+  for (int e = lane; e < nchunk * Cg; e += 64) {
+    const int ck = e / Cg, c = gi * Cg + e - ck * Cg;
+    const int row = s * nchunk + ck;
+    const float* p = c < C1 ? cs1 + ((size_t)row * C1 + c) * 2 : cs2 + ((size_t)row * C2 + c - C1) * 2;
+    a += p[0];
+    q += p[1];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o);
+    q += __shfl_xor(q, o);
+  }
+  const double n = (double)rows_per_sample * Cg;
+  const double mean = a / n;
+  const double var = fmax(q / n - mean * mean, 0.0);
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  for (int c = gi * Cg + lane; c < (gi + 1) * Cg; c += 64) {
+    const float sc = rstd * gamma[c];
+    scale[(size_t)s * C + c] = sc;
+    shift[(size_t)s * C + c] = beta[c] - (float)mean * sc;
+  }
+}
+
 // ---- GroupNorm backward (training path) ----
 // z = x * scale + shift (the forward's affine, recomputed), dz = g (or g * silu'(z) with the fused SiLU).
 // Pass 1 (gn_bwd_sums): per (sample, chunk) and channel, sum dz and dz * x (same geometry as gn_stats).
@@ -854,6 +939,40 @@ extern "C" int vst_groupnorm(const void* x1, int ld1, int C1, const void* x2, in
                      groups, C / groups, eps, gamma, beta, scale, shift, C);
   hipLaunchKernelGGL(gn_apply_kernel, dim3(nchunk, nsamples), dim3(rps * CH), 0, s, (const bf16_t*)x1, ld1, C1,
                      (const bf16_t*)x2, ld2, C2, rows_per_sample, rpc, scale, shift, silu_act, (bf16_t*)y, ldy);
+  return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+}
+
+// Column statistics of x [M, C] (C % 8 == 0) as the 128x320 conv epilogue writes them: cs [ceil(M / 128)][C][2].
+extern "C" int vst_colstat(const void* x, int ldx, int M, int C, float* cs, void* stream) {
+  if (!x || !cs || M <= 0 || C <= 0 || C % 8 || (ldx & 7)) return VST_ERR_ARG;
+  hipLaunchKernelGGL(gn_colstat_kernel, dim3((M + 127) / 128, (C + 319) / 320), dim3(512), 0, (hipStream_t)stream,
+                     (const bf16_t*)x, ldx, M, C, cs);
+  return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
+}
+
+// vst_groupnorm with the statistics from column statistics of x1 (and x2) written by the producing conv
+// (vst_conv3x3_colstat, 128-row tiles): rows_per_sample % 128 == 0.  workspace: vst_groupnorm_workspace_bytes.
+extern "C" int vst_groupnorm_colstat(const void* x1, int ld1, int C1, const float* cs1, const void* x2, int ld2, int C2,
+                                     const float* cs2, int nsamples, int rows_per_sample, int groups, float eps,
+                                     const float* gamma, const float* beta, int silu_act, void* y, int ldy,
+                                     void* workspace, void* stream) {
+  const int C = C1 + (x2 ? C2 : 0);
+  if (!x1 || !cs1 || !y || !workspace || !gamma || !beta || nsamples <= 0 || rows_per_sample <= 0 || groups <= 0)
+    return VST_ERR_ARG;
+  if ((x2 && !cs2) || rows_per_sample % 128) return VST_ERR_ARG;
+  if (C % groups || C % 8 || C1 % 8 || (ld1 & 7) || (ldy & 7) || (x2 && (ld2 & 7))) return VST_ERR_ARG;
+  if (C > 4096) return VST_ERR_ARG;
+  if (!x2) C2 = 0;
+  hipStream_t s = (hipStream_t)stream;
+  const int rpc = gn_rpc_rows(rows_per_sample);
+  const int nchunk = gn_nchunk_rows(rows_per_sample);
+  float* scale = (float*)workspace + gn_part_floats_rows(nsamples, rows_per_sample, groups);
+  float* shift = scale + (size_t)nsamples * C;
+  hipLaunchKernelGGL(gn_finalize_colstat_kernel, dim3(nsamples * groups), dim3(64), 0, s, cs1, C1, cs2, C2,
+                     rows_per_sample / 128, rows_per_sample, groups, C / groups, eps, gamma, beta, scale, shift);
+  hipLaunchKernelGGL(gn_apply_kernel, dim3(nchunk, nsamples), dim3(gn_rps(C) * (C / 8)), 0, s, (const bf16_t*)x1,
+                     ld1, C1, (const bf16_t*)x2, ld2, C2, rows_per_sample, rpc, scale, shift, silu_act, (bf16_t*)y,
+                     ldy);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 

@@ -7,6 +7,9 @@ No CPU fallback exists: a CPU tensor or a missing library raises.
 """
 from __future__ import annotations
 
+import os
+import weakref
+
 import torch
 
 from . import _lib
@@ -421,12 +424,68 @@ def linear_temporal_attention(x: torch.Tensor, w_t: torch.Tensor, b_t: torch.Ten
     return out
 
 
+# GroupNorm column statistics of conv outputs (vst_conv3x3_colstat -> vst_groupnorm_colstat): output data_ptr ->
+# (weakref to the output, its version counter at the conv, colstat [ceil(M/128), Cout, 2] fp32).  Filled by
+# conv3x3(colstat=True) and read by colstat_of(); an entry is valid only for the very tensor the conv wrote, not
+# modified since (version), still alive (weakref).  colstat_reset() at the start of each UNet forward.
+_COLSTAT: dict = {}
+
+
+def colstat_enabled() -> bool:
+    """VST_GN_COLSTAT=1: the UNet's GroupNorms take their statistics from column statistics (opt-in).  Measured in
+    the denoise step (profiles/r5_ab_gn_colstat.txt): GroupNorm 2.22 -> 2.00 ms, the convs that write the statistics
+    10.80 -> 10.92 ms (the epilogue's two extra barriers and row-group sums), net -0.08 ms per step, within the
+    run-to-run spread; and every GroupNorm's statistics change bits (another summation order), which moved one
+    configs[2] block's max-element error past its gate (1.76e-2 against 1.6e-2, rel_l2 unchanged)."""
+    return os.environ.get("VST_GN_COLSTAT", "0") == "1"
+
+
+def colstat_reset() -> None:
+    _COLSTAT.clear()
+
+
+def colstat_of(t: torch.Tensor | None):
+    """The column statistics a conv3x3(colstat=True) registered for exactly this tensor, else None."""
+    if t is None:
+        return None
+    e = _COLSTAT.get(t.data_ptr())
+    if e is None:
+        return None
+    base = e[0]()
+    if base is None or base.shape != t.shape or base.stride() != t.stride() or t._version != e[1]:
+        return None
+    return e[2]
+
+
+def colstat(x: torch.Tensor) -> torch.Tensor:
+    """Column statistics of x [M, C] in the conv epilogue's arithmetic (vst_colstat): [ceil(M/128), C, 2] fp32."""
+    _dev(x, BF16, "x")
+    M, C = x.shape
+    cs = torch.empty(((M + 127) // 128, C, 2), dtype=F32, device=x.device)
+    with _Rec("groupnorm", 0.0, 2.0 * M * C):
+        _lib.call("vst_colstat", _p(x), _ld(x), M, C, _p(cs), _stream())
+    return cs
+
+
+def group_norm_stats(x1, x2=None):
+    """(cs1, cs2) for group_norm(colstat=...): each source's column statistics from its producing conv when it wrote
+    them (colstat_of), else from vst_colstat -- the same bits either way."""
+    c1 = colstat_of(x1)
+    c1 = colstat(x1) if c1 is None else c1
+    if x2 is None:
+        return c1, None
+    c2 = colstat_of(x2)
+    return c1, colstat(x2) if c2 is None else c2
+
+
 def conv3x3(x1: torch.Tensor, nimg: int, H: int, W: int, w: torch.Tensor, bias: torch.Tensor | None, *,
             x2: torch.Tensor | None = None, stride: int = 1, upsample: bool = False,
             row_bias: torch.Tensor | None = None, row_bias_div: int = 1, residual: torch.Tensor | None = None,
-            out: torch.Tensor | None = None) -> torch.Tensor:
+            out: torch.Tensor | None = None, colstat: bool = False) -> torch.Tensor:
     """NHWC 3x3 conv (pad 1).  x1: [nimg*H*W, C1] (+ x2: [nimg*H*W, C2] concatenated on channels).
-    w: [Cout, 9*(C1+C2)] laid out (ky, kx, ci).  Returns [nimg*OH*OW, Cout]."""
+    w: [Cout, 9*(C1+C2)] laid out (ky, kx, ci).  Returns [nimg*OH*OW, Cout].
+    colstat: also write the GroupNorm column statistics of the output where the 128x320 8-phase tiles run it
+    (vst_conv3x3_colstat), registered for colstat_of(out)."""
     _dev(x1, BF16, "x1")
     C1 = x1.shape[1]
     C2 = 0
@@ -460,6 +519,18 @@ def conv3x3(x1: torch.Tensor, nimg: int, H: int, W: int, w: torch.Tensor, bias: 
     kind = "conv3x3" if (C1 + C2) % 64 == 0 else "conv3x3_small_cin"
     with _Rec(kind, 2.0 * M * Cout * kreal, 2.0 * (nimg * H * W * (C1 + C2) + Cout * kreal + M * Cout),
               lambda: gemm_kernel_name(M, Cout, w.shape[1], 2 if kind == "conv3x3" else 3), (M, Cout, w.shape[1])):
+        if colstat and colstat_enabled() and Cout % 320 == 0 and out.is_contiguous() and GEMM_POLICY["tile"] == 0 \
+                and _splits() <= 1:
+            cs = torch.empty(((M + 127) // 128, Cout, 2), dtype=F32, device=x1.device)
+            rc = _lib.load().vst_conv3x3_colstat(
+                _p(x1), C1, _p(x2), C2, nimg, H, W, stride, 1 if upsample else 0, _p(w), Cout, _p(bias),
+                _p(row_bias), row_bias_div, 0 if row_bias is None else _ld(row_bias), _p(residual),
+                0 if residual is None else _ld(residual), _p(out), _ld(out), _p(cs), _stream())
+            if rc == 0:
+                _COLSTAT[out.data_ptr()] = (weakref.ref(out), out._version, cs)
+                return out
+            if rc != 3:
+                raise _lib.VstError(f"vst_conv3x3_colstat failed with status {rc}")
         ws = _workspace(x1.device)
         _lib.call("vst_conv3x3_ex", _p(x1), C1, _p(x2), C2, nimg, H, W, stride, 1 if upsample else 0, _p(w), Cout,
                   _p(bias), _p(row_bias), row_bias_div, 0 if row_bias is None else _ld(row_bias), _p(residual), 0 if residual is None else _ld(residual),
@@ -547,7 +618,10 @@ def motion_attention_block(x, nclip, F, HW, heads, gamma, beta, eps, pe, wqkv, b
     return out
 
 
-def group_norm(x1, nsamples, rows_per_sample, groups, eps, gamma, beta, *, silu=False, x2=None, out=None):
+def group_norm(x1, nsamples, rows_per_sample, groups, eps, gamma, beta, *, silu=False, x2=None, out=None,
+               colstat=None):
+    """colstat: (cs1, cs2 or None) column statistics of x1 / x2 from their producing convs (colstat_of):
+    the statistics pass over x is skipped (vst_groupnorm_colstat)."""
     _dev(x1, BF16, "x1")
     C = x1.shape[1] + (0 if x2 is None else x2.shape[1])
     if x2 is not None:
@@ -558,6 +632,14 @@ def group_norm(x1, nsamples, rows_per_sample, groups, eps, gamma, beta, *, silu=
         out = torch.empty((x1.shape[0], C), dtype=BF16, device=x1.device)
     ws_bytes = _lib.load().vst_groupnorm_workspace_bytes(nsamples, rows_per_sample, groups, C)
     ws = torch.empty((ws_bytes + 3) // 4, dtype=F32, device=x1.device)
+    if colstat is not None:
+        cs1, cs2 = colstat
+        with _Rec("groupnorm", 0.0, 2.0 * 2 * x1.shape[0] * C):  # one read + one write
+            _lib.call("vst_groupnorm_colstat", _p(x1), _ld(x1), x1.shape[1], _p(cs1), _p(x2),
+                      0 if x2 is None else _ld(x2), 0 if x2 is None else x2.shape[1], _p(cs2), nsamples,
+                      rows_per_sample, groups, float(eps), _p(gamma), _p(beta), 1 if silu else 0, _p(out), _ld(out),
+                      _p(ws), _stream())
+        return out
     with _Rec("groupnorm", 0.0, 2.0 * 3 * x1.shape[0] * C):  # two reads + one write
         _lib.call("vst_groupnorm", _p(x1), _ld(x1), x1.shape[1], _p(x2), 0 if x2 is None else _ld(x2),
                   0 if x2 is None else x2.shape[1], nsamples, rows_per_sample, groups, float(eps), _p(gamma),

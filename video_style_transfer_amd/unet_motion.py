@@ -59,8 +59,12 @@ f32 = _F32Cache.get
 
 class GroupNorm(nn.GroupNorm):
     def run(self, x1, nsamples, rows_per_sample, *, silu=False, x2=None, out=None):
+        # statistics from column statistics (128-row chunks): the producing conv's epilogue wrote them
+        # (K.conv3x3(colstat=True)) or vst_colstat makes them, the same bits either way, so a frame shard (whose convs
+        # may run on other tiles) normalises exactly as the whole clip does
+        cs = K.group_norm_stats(x1, x2) if rows_per_sample % 128 == 0 and K.colstat_enabled() else None
         return K.group_norm(x1, nsamples, rows_per_sample, self.num_groups, self.eps, f32(self.weight), f32(self.bias),
-                            silu=silu, x2=x2, out=out)
+                            silu=silu, x2=x2, out=out, colstat=cs)
 
 
 class LayerNorm(nn.LayerNorm):
@@ -96,9 +100,11 @@ class Conv3x3(nn.Conv2d):
             self.__dict__["_vst_w"] = c
         return c[1]
 
-    def run(self, x1, nimg, H, W, *, x2=None, upsample=False, row_bias=None, row_bias_div=1, residual=None):
+    def run(self, x1, nimg, H, W, *, x2=None, upsample=False, row_bias=None, row_bias_div=1, residual=None,
+            colstat=False):
         return K.conv3x3(x1, nimg, H, W, self.kernel_weight(), f32(self.bias), x2=x2, stride=self.stride[0],
-                         upsample=upsample, row_bias=row_bias, row_bias_div=row_bias_div, residual=residual)
+                         upsample=upsample, row_bias=row_bias, row_bias_div=row_bias_div, residual=residual,
+                         colstat=colstat)
 
 
 class Conv1x1(nn.Conv2d):
@@ -339,10 +345,10 @@ class ResnetBlock2D(nn.Module):
             temb = ctx.temb[self]  # view of the one batched projection (UNetMotionModel.batched_temb)
         else:
             temb = self.time_emb_proj.run(ctx.emb_silu).float()  # [B, cout]; bf16-rounded like the reference
-        h = self.conv1.run(h, nimg, H, W, row_bias=temb, row_bias_div=ctx.F * HW)
+        h = self.conv1.run(h, nimg, H, W, row_bias=temb, row_bias_div=ctx.F * HW, colstat=True)
         h = self.norm2.run(h, nimg, HW, silu=True)
         sc = self.conv_shortcut.run(x1, x2) if self.conv_shortcut is not None else x1
-        return self.conv2.run(h, nimg, H, W, residual=sc)
+        return self.conv2.run(h, nimg, H, W, residual=sc, colstat=True)
 
 
 class Downsample2D(nn.Module):
@@ -351,7 +357,7 @@ class Downsample2D(nn.Module):
         self.conv = Conv3x3(C, C, stride=2)
 
     def run(self, x, nimg, H, W):
-        return self.conv.run(x, nimg, H, W), (H + 1) // 2, (W + 1) // 2
+        return self.conv.run(x, nimg, H, W, colstat=True), (H + 1) // 2, (W + 1) // 2
 
 
 class Upsample2D(nn.Module):
@@ -360,7 +366,7 @@ class Upsample2D(nn.Module):
         self.conv = Conv3x3(C, C)
 
     def run(self, x, nimg, H, W):
-        return self.conv.run(x, nimg, H, W, upsample=True), 2 * H, 2 * W
+        return self.conv.run(x, nimg, H, W, upsample=True, colstat=True), 2 * H, 2 * W
 
 
 class DownBlock(nn.Module):
@@ -548,6 +554,7 @@ class UNetMotionModel(nn.Module):
         if fusion_world is None:
             fusion_world = shard.world if shard is not None else 1
         # no split-K: a row's bits do not depend on the launch's row count (frame shards)
+        K.colstat_reset()
         with K.row_invariant(), K.fusion_world(fusion_world):
             ctx = FwdCtx(B, F, emb_silu, enc, cross_kwargs or {}, shard, self.batched_temb(emb_silu))
             nimg = B * F
