@@ -188,7 +188,12 @@ def _roofline_from(rec, step_ms=None):
     scale = min(1.0, step_ms / total_ms) if step_ms else 1.0
     if os.environ.get("VST_BENCH_SHAPES"):
         for key, (n, ms, fl, nb) in sorted(shapes.items(), key=lambda kv: -kv[1][1]):
-            print(f"[shape] {ms:8.3f} ms {n:4d}x {fl / (ms * 1e-3) / 1e12:7.1f} TF  {key}", file=sys.stderr)
+            # the shape's own roofline floor: MFMA (flops / 2.5 PF) or HBM (algorithmic bytes / 8 TB/s), whichever is
+            # longer, and the fraction of it this launch reaches
+            t_mfma, t_hbm = fl / (PEAK_BF16_TFLOPS * 1e12), nb / (PEAK_HBM_GBS * 1e9)
+            print(f"[shape] {ms:8.3f} ms {n:4d}x {fl / (ms * 1e-3) / 1e12:7.1f} TF {nb / (ms * 1e-3) / 1e9:7.1f} GB/s "
+                  f"{'mfma' if t_mfma >= t_hbm else 'hbm ':4s} roof {max(t_mfma, t_hbm) / (ms * 1e-3):.3f}  {key}",
+                  file=sys.stderr)
     # north-star view: the fused base + UnZipLoRA projection GEMMs (q/k/v, out) and attn2 (to_q + UnZipLoRA + the
     # text attention) per shape.  frac is against the 2.5 PF MFMA peak (the north star's measure); each entry also
     # carries its roofline bound: the MFMA time floor (flops / 2.5 PF) against the HBM floor (algorithmic bytes /
