@@ -58,10 +58,42 @@ CASES = [
     (8192, 1280, 1, 1280, 16, 32, True, True, 192),    # to_out + UnZipLoRA r=8 at the 16x16 level (+ bias, residual)
     (8192, 1280, 3, 1280, 16, 64, False, False, 256),  # attn1 q/k/v stacked
     (8192, 1280, 1, 1280, 16, 32, False, False, 192),  # attn2 q
-    (32768, 640, 1, 640, 16, 32, True, True, 192),     # to_out at the 32x32 level
+    (32768, 640, 1, 640, 16, 32, True, True, 320),     # to_out at the 32x32 level (the persistent LoRA grid)
+    (32768, 640, 3, 640, 16, 64, False, False, 320),   # attn1 q/k/v at the 32x32 level (persistent, 6 rounds)
     (8192, 1280, 3, 1280, 8, 32, False, False, 256),   # content-only (r = 8 per projection: 8-column groups)
     (7000, 1000, 1, 1280, 16, 32, True, True, 192),    # M tail (7000 = 27 x 256 + 88), K tail (1000 = 15 x 64 + 40)
 ]
+
+
+@pytest.mark.parametrize("M,Kd,nproj,n_per,r_per,P", [(32768, 640, 1, 640, 16, 32), (32768, 640, 3, 640, 16, 64)])
+def test_gemm_lora_persistent_bitwise(cuda, K, monkeypatch, M, Kd, nproj, n_per, r_per, P):
+    """The persistent LoRA grid (128x320 tiles, each tile's fill under the previous tile's epilogue) gives the bits of
+    the one-workgroup-per-tile launches (VST_P8_LORA_PERSIST=0 in a child process: the switch is read once)."""
+    import subprocess
+    import sys
+    g = torch.Generator().manual_seed(M + nproj)
+    x, A, W = _operands(M, Kd, nproj, n_per, r_per, P, g, cuda)
+    N = W.shape[0]
+    b = (torch.randn(N, generator=g) * 0.1).to(cuda)
+    r = rnd(M, N, gen=g).to(cuda)
+    assert K.gemm_lora_tile(M, N, Kd, P, n_per, r_per) == 320
+    out = K.linear_lora(x, W, A, n_per, r_per, b, residual=r)
+    import os
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        torch.save({"x": x.cpu(), "A": A.cpu(), "W": W.cpu(), "b": b.cpu(), "r": r.cpu()}, os.path.join(d, "in.pt"))
+        code = (
+            "import sys, torch; sys.path.insert(0, %r)\n"
+            "from video_style_transfer_amd import kernels as K\n"
+            "t = torch.load(%r, weights_only=True)\n"
+            "c = {k: v.cuda() for k, v in t.items()}\n"
+            "y = K.linear_lora(c['x'], c['W'], c['A'], %d, %d, c['b'], residual=c['r'])\n"
+            "torch.save(y.cpu(), %r)\n" % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                             os.path.join(d, "in.pt"), n_per, r_per, os.path.join(d, "out.pt")))
+        env = dict(os.environ, VST_P8_LORA_PERSIST="0")
+        subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=240)
+        ref = torch.load(os.path.join(d, "out.pt"), weights_only=True)
+    assert torch.equal(out.cpu(), ref)
 
 
 @pytest.mark.parametrize("M,Kd,nproj,n_per,r_per,P,use_bias,use_res,bn", CASES)

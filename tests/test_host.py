@@ -42,15 +42,17 @@ def test_bad_arguments_rejected_without_gpu():
 
 def test_gemm_lora_policy_without_gpu():
     """vst_gemm_lora_supported (host policy, no launch): the SDXL UnZipLoRA r=8 projections run the down-projection
-    inside the 8-phase GEMM, whatever M is (the decision is shape-only, so a frame-sharded rank takes the unsharded
-    forward's path); a shape where every tile width straddles two u blocks, or a rank wider than one block, is
-    refused."""
+    inside the 8-phase GEMM, whatever M is (whether the in-GEMM path is taken is shape-only, so a frame-sharded rank
+    takes the unsharded forward's path; the tile width it returns may follow the grid's rounds); a shape where every
+    tile width straddles two u blocks, or a rank wider than one block, is refused."""
     from video_style_transfer_amd import _lib
     lib = _lib.load()
     q = lib.vst_gemm_lora_supported
     assert q(8192, 1280, 1280, 32, 1280, 16) == 192   # to_out / attn2 q at 16x16
     assert q(8192, 3840, 1280, 64, 1280, 16) == 256   # attn1 q/k/v at 16x16
-    assert q(32768, 640, 640, 32, 640, 16) == 192     # to_out at 32x32
+    assert q(32768, 640, 640, 32, 640, 16) == 320     # to_out at 32x32: two rounds -> the persistent 128x320 grid
+    #   (the tile width may follow M; the k order, and so the bits, do not -- test_gemm_lora_persistent_bitwise)
+    assert q(16384, 640, 640, 32, 640, 16) == 192     # ... one round at a 2-way frame shard: one workgroup per tile
     assert q(32768, 1920, 640, 64, 640, 16) == 320    # q/k boundary inside a 256-wide tile: 128x320 tiles
     assert q(32768, 1800, 640, 64, 600, 16) == 0      # every width straddles (600 wide, not a multiple of 320)
     assert q(8192, 1280, 1280, 32, 1280, 32) == 0     # r = 16 UnZipLoRA: 32 u columns per projection

@@ -7,11 +7,12 @@ mkdir -p gpurun_out
 i=0
 for tag in "$@"; do
   i=$((i+1))
-  unset VST_P8_320 VST_SA_SELF VST_GN_COLSTAT
+  unset VST_P8_320 VST_SA_SELF VST_GN_COLSTAT VST_P8_LORA_PERSIST
   base=$tag
   if [ "$tag" = new320 ]; then export VST_P8_320=1; base=new; fi  # 128x320 tiles where their rounds win (opt-in)
   if [ "$tag" = sa0 ]; then export VST_SA_SELF=0; base=new; fi  # self-attention on spatial_attn_kernel<0>
   if [ "$tag" = gn1 ]; then export VST_GN_COLSTAT=1; base=new; fi  # GroupNorm statistics from conv column statistics
+  if [ "$tag" = lp0 ]; then export VST_P8_LORA_PERSIST=0; base=new; fi  # in-GEMM LoRA one workgroup per tile
   if [ "$tag" = n320 ]; then export VST_P8_320N=1; base=new; fi  # 128x320 tiles for the narrow 32x32 / 64x64 GEMMs
   if [ "$base" = new ]; then unset VST_LIB_AB; else export VST_LIB_AB=abl/libvst_$base.so; fi
   timeout -k 10 300 python -u bench.py --steps 15 --warmup 3 --no-cpu-baseline --no-peaks --no-vae \

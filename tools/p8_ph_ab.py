@@ -3,7 +3,7 @@ denoise step's GEMM shapes, in isolation: each schedule runs in its own child pr
 process), alternated `passes` times; the children also hash their outputs, which must be equal (same k order).
 python tools/p8_ph_ab.py [passes] [variant ...]  -> one JSON line per shape with us per launch and TF/s per variant.
 A variant is the schedule, optionally '+320' for the 128x320 tile policy (VST_P8_320=1) and '+persist' for the persistent
-grid (VST_P8_PERSIST=1), '+bn320' / '+bn192' to force the tile width (VST_P8_BN): e.g. 3 2 3+320 2+320 2+persist."""
+grid (VST_P8_PERSIST=1), '+bn320' / '+bn192' to force the tile width (VST_P8_BN), '+lp' for the persistent LoRA kernels (VST_P8_LORA_PERSIST=1): e.g. 3 2 3+320 2+320 2+persist."""
 import hashlib
 import json
 import os
@@ -103,6 +103,7 @@ def main():
             env = dict(os.environ, VST_P8_PH=ph.split("+")[0], VST_PH_CHILD="1", VST_P8_320="1" if "+320" in ph else "0",
                        VST_P8_PERSIST="1" if "+persist" in ph else "0",
                        VST_P8_BN="320" if "+bn320" in ph else "192" if "+bn192" in ph else "0",
+                       VST_P8_LORA_PERSIST="1" if "+lp" in ph else "0",
                        )
             r = subprocess.run([sys.executable, os.path.abspath(__file__)], env=env, capture_output=True, text=True,
                                timeout=300)

@@ -635,6 +635,7 @@ static void choose(int M, int N, int K, int geglu, int conv, size_t ws_bytes, in
 int launch_gemm_ring(const GemmArgs& a, int amode, int epi, int tile, int splits, hipStream_t s);
 int launch_gemm_p8(const GemmArgs& a, int epi, int bn, hipStream_t s);
 bool p8_persist_applies(int M, int N, int K, int epi, int bn);
+bool p8_lora_persist_on();
 int launch_gemm_p8_tattn(const GemmArgs& a, hipStream_t s);
 int launch_gemm_p8_lora(const GemmArgs& a, int bn, hipStream_t s);
 int launch_gemm_p8_xattn(const GemmArgs& a, hipStream_t s);
@@ -867,9 +868,19 @@ static int lora_ingemm_bn(int M, int N, int K, int P, int gn, int gr, int force_
     return 0;
   if (force_bn) return lora_tiles_ok(N, P, gn, gr, force_bn) && (force_bn != 320 || N % 320 == 0) ? force_bn : 0;
   const int cand[4] = {p8_bn(M, N, false), 192, 256, 320};
-  for (int bn : cand)
-    if ((bn != 320 || N % 320 == 0) && lora_tiles_ok(N, P, gn, gr, bn)) return bn;
-  return 0;
+  int bn = 0;
+  for (int c : cand)
+    if ((c != 320 || N % 320 == 0) && lora_tiles_ok(N, P, gn, gr, c)) {
+      bn = c;
+      break;
+    }
+  // a multi-round grid of 256-row tiles (the 32x32 out-projection) moves to the persistent LoRA grid, which runs
+  // 128x320 tiles only (gemm_p8.hip, p8_lora_persist_env); a grid under two rounds keeps its tiles (the 16x16 q/k/v:
+  // 480 tiles of 256x256, 76 us against 89 on 128x320 persistent, profiles/r5_ab_lora_persist.txt)
+  if (bn && bn != 320 && p8_lora_persist_on() && N % 320 == 0 && lora_tiles_ok(N, P, gn, gr, 320) &&
+      (long)((M + 255) / 256) * ((N + bn - 1) / bn) >= 2L * device_cus() && p8_persist_applies(M, N, K, 0, 320))
+    bn = 320;
+  return bn;
 }
 
 extern "C" int vst_gemm_lora_supported(int M, int N, int K, int P, int group_n, int group_r) {

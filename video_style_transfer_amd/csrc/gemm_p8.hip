@@ -58,6 +58,10 @@ struct P8Cfg {  // the epilogue's view of the tile (same wave tiling as RingCfg<
   static constexpr int LDS_LORA = LORA_END > EPI_BYTES ? LORA_END : EPI_BYTES;
   // PERSIST: the epilogue stages through the LDS past the ring (the ring holds the next tile's first k-tiles)
   static constexpr int EPI_OFF = 2 * BUF, EPI_REGION = 160 * 1024 - 2 * BUF;
+  // PERSIST + LORA (128x320 tiles): u exchanged at U_OFF past V; the epilogue stages over V and U (both dead once the
+  // tile's u . V step is done), never over the Acat slots, which hold the next tile's first two k-tiles by then
+  static constexpr int U_OFF = LORA_END, U_END = U_OFF + BM * 32;
+  static constexpr int EPI_OFF_L = V_OFF, EPI_REGION_L = 160 * 1024 - V_OFF;
   static_assert((BM == 256 && (BN == 256 || BN == 192)) || (BM == 128 && BN == 320), "tile shape");
   static_assert(LDS <= 160 * 1024 && LDS_LORA <= 160 * 1024, "LDS budget");
 };
@@ -313,36 +317,39 @@ __device__ __forceinline__ void xattn_epilogue(const GemmArgs& p, char* smem, co
 // chunks get out-of-range offsets), so every wave issues exactly p8_epi_stores<Cfg, EPI>() of them.  pre() runs after
 // the bias add (the caller's next-tile DMAs, issued before any store).  GEGLU reads its bias from R, where the k-loop
 // brought it by LDS-DMA.
-template <class Cfg, int EPI>
+template <class Cfg, int EPI, int REGION = Cfg::EPI_REGION>
 constexpr int p8_epi_ipp() {  // 16-row accumulator blocks per staged pass (both wave rows)
-  constexpr int ROWB = (EPI == 1 ? Cfg::BN / 2 : Cfg::BN) * 2, REGION = Cfg::EPI_REGION, MI = Cfg::MI;
+  constexpr int ROWB = (EPI == 1 ? Cfg::BN / 2 : Cfg::BN) * 2, MI = Cfg::MI;
   return (MI >= 8 && 256 * ROWB <= REGION) ? 8
          : (MI >= 4 && 128 * ROWB <= REGION) ? 4
          : (MI >= 2 && 64 * ROWB <= REGION) ? 2 : 1;
 }
-template <class Cfg, int EPI>
+template <class Cfg, int EPI, int REGION = Cfg::EPI_REGION>
 constexpr int p8_epi_items() {  // 16-B output chunks per thread per staged pass
-  return 32 * p8_epi_ipp<Cfg, EPI>() * ((EPI == 1 ? Cfg::BN / 2 : Cfg::BN) / 8) / Cfg::THREADS;
+  return 32 * p8_epi_ipp<Cfg, EPI, REGION>() * ((EPI == 1 ? Cfg::BN / 2 : Cfg::BN) / 8) / Cfg::THREADS;
 }
-template <class Cfg, int EPI>
+template <class Cfg, int EPI, int REGION = Cfg::EPI_REGION>
 constexpr int p8_epi_stores() {
 #ifdef VST_ABL_NOEPI
   return 0;
 #else
-  return EPI == 1 ? 2 * Cfg::MI : p8_epi_items<Cfg, EPI>() * (Cfg::MI / p8_epi_ipp<Cfg, EPI>());
+  return EPI == 1 ? 2 * Cfg::MI : p8_epi_items<Cfg, EPI, REGION>() * (Cfg::MI / p8_epi_ipp<Cfg, EPI, REGION>());
 #endif
 }
 
-template <class Cfg, int EPI, class Pre>
+// ROT (the in-GEMM LoRA kernels): acc[mq MQR + i] holds row block (i + wc) mod MQR of quadrant mq (p8_acc_row), so a
+// pass stages whole quadrants (IPP == MQR) and each wave writes its blocks at their rotated rows.
+template <class Cfg, int EPI, int REGION = Cfg::EPI_REGION, bool ROT = false, class Pre>
 __device__ __forceinline__ void p8_epilogue_passes(const GemmArgs& p, char* R, const int m0, const int n0,
                                                    f32x4 (&acc)[Cfg::MI][Cfg::NJ], const int wr, const int wc,
                                                    Pre&& pre) {
   constexpr int MI = Cfg::MI, NJ = Cfg::NJ, WM = Cfg::WM, THREADS = Cfg::THREADS;
   constexpr int OC = EPI == 1 ? Cfg::BN / 2 : Cfg::BN;  // output columns of the tile
-  constexpr int ROWB = OC * 2, REGION = Cfg::EPI_REGION;
-  constexpr int IPP = p8_epi_ipp<Cfg, EPI>();
+  constexpr int ROWB = OC * 2;
+  constexpr int IPP = p8_epi_ipp<Cfg, EPI, REGION>();
   constexpr int PR = 32 * IPP, NPASS = MI / IPP, CPR = OC / 8, ITEMS = PR * CPR / THREADS;
-  static_assert(ITEMS == p8_epi_items<Cfg, EPI>(), "store count");
+  static_assert(ITEMS == p8_epi_items<Cfg, EPI, REGION>(), "store count");
+  static_assert(!ROT || IPP == Cfg::MQR, "rotated row blocks: one quadrant per pass");
   static_assert(PR * ROWB <= REGION && (PR * CPR) % THREADS == 0 && CPR % 8 == 0 && MI % IPP == 0, "pass split");
   static_assert(EPI != 1 || (Cfg::WN == 64 && NJ == 4), "GEGLU: [32 hidden | 32 gate] per wave column");
   const int tid = threadIdx.x, lane = tid & 63, fr = lane & 15, fq = lane >> 4;
@@ -415,7 +422,7 @@ __device__ __forceinline__ void p8_epilogue_passes(const GemmArgs& p, char* R, c
     }
 #pragma unroll
     for (int ii = 0; ii < IPP; ++ii) {
-      const int i = q * IPP + ii, lr = wr * 16 * IPP + ii * 16 + fr;
+      const int i = q * IPP + ii, lr = wr * 16 * IPP + (ROT ? ((ii + wc) & (Cfg::MQR - 1)) : ii) * 16 + fr;
       {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
@@ -570,7 +577,9 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   static_assert(!CONV || (!LORA && EPI == 0), "conv: plain epilogue");
   static_assert(EPI != 1 || BN == 256, "GEGLU needs 64-column [hidden | gate] blocks");
   static_assert(!LORA || EPI != 1, "in-GEMM LoRA: linear epilogue");
-  static_assert(!PERSIST || (!LORA && !CONV && EPI != 4 && EPI != 5 && PH == 2), "persistent tiles: plain / GEGLU / GELU, PH 2");
+  static_assert(!PERSIST || (!CONV && EPI != 4 && EPI != 5 && PH == 2 && (!LORA || (EPI == 0 && BN == 320))),
+                "persistent tiles: plain / GEGLU / GELU, and the in-GEMM LoRA on 128x320 tiles; PH 2");
+  static_assert(!(PERSIST && LORA) || Cfg::U_END <= 160 * 1024, "LoRA persistent LDS");
   static_assert(EPI != 5 || (BN == 256 && BM == 256 && !LORA && !CONV), "temporal attention epilogue: 256x256 tiles");
   static_assert(EPI != 4 || (BN == 192 && BM == 256), "cross-attention epilogue: 256 x 192 tiles (3 heads)");
   // LORA: the Acat DMA of a k-tile is issued by waves 0-1 only (one 1-KiB piece each), so their counted vmcnt waits
@@ -783,11 +792,11 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   };
 
   // LORA: Acat columns of k-tile kt into its slot (buffer kt & 1), by waves 0-1 (the others issue nothing)
-  auto dma_lora = [&](int kt, int kend, bool checked) {
+  auto dma_lora = [&](int kt, int kend, bool checked, int kbase) {
     if ((abl & 1) && kt > 1) return;
     if constexpr (LORA) {
       if (wid >= 2) return;
-      char* dst = smem + Cfg::LORA_OFF + (kt & 1) * 2048 + wid * 1024;
+      char* dst = smem + Cfg::LORA_OFF + ((kbase + kt) & 1) * 2048 + wid * 1024;
       const int k0 = kt * 64;
       const bool kin = !checked || (kt < kend && k0 + lc8 < p.K);
       p8_dma16(rl, dst, kin ? (int)(lbase + (uint32_t)k0 * 2u) : kOOB);
@@ -873,8 +882,8 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
                    row2 < BN && n2 < p.N ? (int)(((uint32_t)n2 * p.ldw + p.K + ub0 + 8 * (lane & 1)) * 2u) : kOOB);
       }
     }
-    dma_slot(0, kb, ke, 0); dma_lora(kb, ke, true); dma_slot(2, kb, ke, 0); dma_slot(3, kb, ke, 0);
-    dma_slot(1, kb, ke, 0); dma_slot(3, kb + 1, ke, 0); dma_slot(0, kb + 1, ke, 0); dma_lora(kb + 1, ke, true);
+    dma_slot(0, kb, ke, 0); dma_lora(kb, ke, true, 0); dma_slot(2, kb, ke, 0); dma_slot(3, kb, ke, 0);
+    dma_slot(1, kb, ke, 0); dma_slot(3, kb + 1, ke, 0); dma_slot(0, kb + 1, ke, 0); dma_lora(kb + 1, ke, true, 0);
     dma_slot(2, kb + 1, ke, 0);
     VST_P8_VMWAIT_LX(2 * NPA + 2 + NPB1);  // A0, (Acat,) B0, B1 of kb landed
     p8_barrier();
@@ -913,7 +922,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       read_b(buf ^ 1, 1, fb1);
       if (!(abl & 4)) p8_vmwait<NPA + NPB1>();  // A0(t+1), B0(t+1) landed
       dma(0, t + 2);
-      dma_lora(t + 2, ke, !FAST);
+      dma_lora(t + 2, ke, !FAST, 0);
       dma(2, t + 2);
       p8_barrier();
       VST_P8_QUAD(1, 0, fb0)
@@ -966,10 +975,10 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
     // J0(kb + 1) (B1E: B1(kb + 2) is younger) / J1(kb + 1)
     const bool handed = PERSIST && !first;
     if (!PERSIST || first) {
-      dma_slot(0, kb, ke, kofs); dma_lora(kb, ke, true); dma_slot(2, kb, ke, kofs); dma_slot(3, kb, ke, kofs);
+      dma_slot(0, kb, ke, kofs); dma_lora(kb, ke, true, kofs); dma_slot(2, kb, ke, kofs); dma_slot(3, kb, ke, kofs);
       dma_slot(1, kb, ke, kofs);
       if constexpr (B1E) dma_slot(3, kb + 1, ke, kofs);
-      dma_slot(0, kb + 1, ke, kofs); dma_lora(kb + 1, ke, true); dma_slot(2, kb + 1, ke, kofs);
+      dma_slot(0, kb + 1, ke, kofs); dma_lora(kb + 1, ke, true, kofs); dma_slot(2, kb + 1, ke, kofs);
       // A0, (Acat,) B0, B1 of kb landed; A1(kb), (B1,) A0, B0 of kb + 1 in flight
       VST_P8_VMWAIT_LX(2 * NPA + (B1E ? NPB1 : 0) + 2);
     }
@@ -1032,13 +1041,18 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       // (DMM: the Acat piece, issued by waves 0-1 only, stays in the load segment, ahead of A0 / B0: a wave-dependent
       // branch inside the MFMA segment would split it; every wait that counts it counts A0 and B0 as well)
       static_assert(!(DMM && LORA && B1E), "DMM + LoRA: the Acat piece must stay younger than B1");
+      // the Acat piece of k-tile t + 2: past this tile's end (PERSIST) the next tile's first two (bases switched above)
+      auto dma_l = [&] {
+        if (PERSIST && !FAST && t + 2 >= ke && has_next) dma_lora(t + 2 - ke, ke, true, kofs + ke);
+        else dma_lora(t + 2, ke, !FAST, kofs);
+      };
       auto dma_j1 = [&] {
         if constexpr (B1E) dma(3, t + 2);
         dma(0, t + 2);
-        if constexpr (!DMM) dma_lora(t + 2, ke, !FAST);
+        if constexpr (!DMM) dma_l();
         dma(2, t + 2);
       };
-      if constexpr (DMM) dma_lora(t + 2, ke, !FAST);
+      if constexpr (DMM) dma_l();
       if constexpr (!DMM) dma_j1();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       p8_barrier();
@@ -1069,8 +1083,38 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
 #undef VST_P8_QUAD
 #undef VST_P8_VMWAIT_LX
 
+  // LORA: u (bf16) -> LDS [BM rows][16 columns] at U, then acc += u . V^T over the 32-wide window (columns 16-31
+  // zero: the [x | u] k-tile's second u half), V = W[n][K + ub0 ...]
+  auto lora_post = [&](char* U) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      u32x2 v;
+      v[0] = pack2bf(acc_u[q][0], acc_u[q][1]);
+      v[1] = pack2bf(acc_u[q][2], acc_u[q][3]);
+      if (wc < MQR) *reinterpret_cast<u32x2*>(U + (wr * Cfg::WM + q * HALF + wc * 16 + fr) * 32 + fq * 8) = v;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const bf16x8 zero8 = {};
+    bf16x8 fv[Cfg::NJ];
+#pragma unroll
+    for (int j = 0; j < Cfg::NJ; ++j) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + Cfg::V_OFF + (wc * Cfg::WN + j * 16 + fr) * 32 + (fq & 1) * 16);
+      fv[j] = fq < 2 ? v : zero8;
+    }
+#pragma unroll
+    for (int i = 0; i < Cfg::MI; ++i) {
+      bf16x8 fu = *reinterpret_cast<const bf16x8*>(U + (wr * Cfg::WM + p8_acc_row<Cfg, true>(i, wc) + fr) * 32 + (fq & 1) * 16);
+      fu = fq < 2 ? fu : zero8;
+#pragma unroll
+      for (int j = 0; j < Cfg::NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fv[j], fu, acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's u reads done before the epilogue stages the tile over them
+  };
   int m0, n0;
   VST_P8_STAMP(0)
+  constexpr int EREG = LORA ? Cfg::EPI_REGION_L : Cfg::EPI_REGION;  // PERSIST epilogue staging bytes
   if constexpr (PERSIST) {
     // gridDim.x (a multiple of 8) workgroups walk the tiles: the workgroups sharing an XCD (b % 8) take that XCD's
     // contiguous chunk of logical tiles in rounds, as the one-tile-per-workgroup launch places them.  Each tile's last
@@ -1103,7 +1147,9 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
         }
       }
 #else
-      p8_epilogue_passes<Cfg, EPI>(p, smem + Cfg::EPI_OFF, m0, n0, acc, wr, wc, [&] {
+      if constexpr (LORA) lora_post(smem + Cfg::U_OFF);  // (the ring holds the next tile's first k-tiles)
+      p8_epilogue_passes<Cfg, EPI, EREG, LORA>(p, smem + (LORA ? Cfg::EPI_OFF_L : Cfg::EPI_OFF), m0, n0, acc, wr, wc,
+                                               [&] {
         if (has_next) {  // A1 (!B1E: and B1) of the next tile's second k-tile (slots free: their last reads retired
                          // in the k-loop)
           if constexpr (!B1E) dma_slot(3, 1, nk, kofs + nk);
@@ -1112,7 +1158,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
       });
 #endif
       if (has_next) {  // the next tile's k-tiles landed; this wave's (exactly counted) stores may stay in flight
-        p8_vmwait<p8_epi_stores<Cfg, EPI>()>();
+        p8_vmwait<p8_epi_stores<Cfg, EPI, EREG>()>();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // no LDS-DMA outlives the workgroup
@@ -1131,36 +1177,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   if constexpr (PH == 2) run_segment2(0, nk, true);
   else run_segment(0, nk);
   VST_P8_STAMP(2)
-  if constexpr (LORA) {
-    // u (bf16) -> LDS [256 rows][16 columns] (the drained ring), then acc += u . V^T over the 32-wide window
-    // (columns 16-31 zero: the [x | u] k-tile's second u half), V = W[n][K + ub0 ...]
-    char* U = smem;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      u32x2 v;
-      v[0] = pack2bf(acc_u[q][0], acc_u[q][1]);
-      v[1] = pack2bf(acc_u[q][2], acc_u[q][3]);
-      if (wc < MQR) *reinterpret_cast<u32x2*>(U + (wr * Cfg::WM + q * HALF + wc * 16 + fr) * 32 + fq * 8) = v;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    const bf16x8 zero8 = {};
-    bf16x8 fv[Cfg::NJ];
-#pragma unroll
-    for (int j = 0; j < Cfg::NJ; ++j) {
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + Cfg::V_OFF + (wc * Cfg::WN + j * 16 + fr) * 32 + (fq & 1) * 16);
-      fv[j] = fq < 2 ? v : zero8;
-    }
-#pragma unroll
-    for (int i = 0; i < Cfg::MI; ++i) {
-      bf16x8 fu = *reinterpret_cast<const bf16x8*>(U + (wr * Cfg::WM + p8_acc_row<Cfg, true>(i, wc) + fr) * 32 + (fq & 1) * 16);
-      fu = fq < 2 ? fu : zero8;
-#pragma unroll
-      for (int j = 0; j < Cfg::NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fv[j], fu, acc[i][j], 0, 0, 0);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave's u reads done before the epilogue stages the tile over them
-  }
+  if constexpr (LORA) lora_post(smem);  // (the drained ring)
 #ifdef VST_ABL_NOEPI  // diagnostics build only: no epilogue of any kind (attention epilogues included)
   {
     float sink = 0.f;
@@ -1240,20 +1257,33 @@ bool p8_persist_applies(int M, int N, int K, int epi, int bn) {
   return tiles >= 2L * p8_cus() && K >= 128 && (K & 63) == 0 && (N % (epi == 1 ? 16 : 8)) == 0;
 }
 
-template <int EPI, int BN, int BM>
+template <int EPI, int BN, int BM, bool LORA = false>
 static int launch_p8_persist(const GemmArgs& a, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_p8_kernel<EPI, BN, false, 2, BM, false, true>,
+    (void)hipFuncSetAttribute((const void*)gemm_p8_kernel<EPI, BN, LORA, 2, BM, false, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
   const int ntiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   const int grid = ntiles < p8_cus() ? (ntiles & ~7) : p8_cus();
   if (grid < 8) return VST_ERR_ARG;
-  hipLaunchKernelGGL((gemm_p8_kernel<EPI, BN, false, 2, BM, false, true>), dim3(grid), dim3(512), 160 * 1024, s, a);
+  hipLaunchKernelGGL((gemm_p8_kernel<EPI, BN, LORA, 2, BM, false, true>), dim3(grid), dim3(512), 160 * 1024, s, a);
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
+
+// The in-GEMM LoRA kernels on the persistent grid (128x320 tiles only: a pass of the staged epilogue must hold whole
+// row quadrants of the rotated LoRA accumulators), wherever p8_persist_applies: the 32x32 level's q/k/v 123 -> 108 us
+// and out-projection 48 -> 43 us per launch, bitwise equal (profiles/r5_ab_lora_persist.txt).  VST_P8_LORA_PERSIST=0
+// restores one workgroup per tile (A/B).
+static int p8_lora_persist_env() {
+  static const int v = [] {
+    const char* e = getenv("VST_P8_LORA_PERSIST");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+bool p8_lora_persist_on() { return p8_persist_env() && p8_ph_env() == 2 && p8_lora_persist_env(); }
 
 // BN = 320 runs 128-row tiles (P8Cfg)
 template <int EPI, int BN, bool LORA = false>
@@ -1262,6 +1292,10 @@ static int launch_p8_epi(const GemmArgs& a, hipStream_t s) {
   if constexpr (!LORA && EPI != 4 && EPI != 5)
     if (!a.A2 && (size_t)a.M * a.ldc * 2 < 0x7fff0000u && p8_persist_applies(a.M, a.N, a.K, EPI, BN))
       return launch_p8_persist<EPI, BN, BM>(a, s);
+  if constexpr (LORA && EPI == 0 && BN == 320)
+    if (p8_lora_persist_on() && !a.A2 && (size_t)a.M * a.ldc * 2 < 0x7fff0000u &&
+        p8_persist_applies(a.M, a.N, a.K, EPI, BN))
+      return launch_p8_persist<EPI, BN, BM, true>(a, s);
   return p8_ph_env() == 2 ? launch_p8_ph<EPI, BN, LORA, 2, BM>(a, s) : launch_p8_ph<EPI, BN, LORA, 3, BM>(a, s);
 }
 
