@@ -213,3 +213,26 @@ def test_text_encoder_surface_cpu():
         assert ours == set(model.state_dict())
         with pytest.raises(_lib.VstError):
             model(torch.zeros(1, 77, dtype=torch.long))
+
+
+def test_colstat_registry_host_logic():
+    """kernels.colstat_of (the GroupNorm column-statistics hand-off, opt-in VST_GN_COLSTAT): an entry is valid only
+    for the very tensor its conv wrote -- same storage, shape and strides, not modified since, still alive -- and
+    colstat_reset() drops every entry (each UNet forward starts with it)."""
+    import weakref
+    from video_style_transfer_amd import kernels as K
+    K.colstat_reset()
+    out = torch.zeros(256, 320, dtype=torch.bfloat16)
+    cs = torch.zeros(2, 320, 2)
+    K._COLSTAT[out.data_ptr()] = (weakref.ref(out), out._version, cs)
+    assert K.colstat_of(out) is cs
+    assert K.colstat_of(out.view(128, 640)) is None          # another shape over the same storage
+    assert K.colstat_of(out[:, :160]) is None                # a column slice (other strides)
+    assert K.colstat_of(None) is None
+    out.add_(1)                                              # modified after the conv wrote it
+    assert K.colstat_of(out) is None
+    K._COLSTAT[out.data_ptr()] = (weakref.ref(out), out._version, cs)
+    assert K.colstat_of(out) is cs
+    K.colstat_reset()
+    assert K.colstat_of(out) is None
+    assert not K.colstat_enabled() or os.environ.get("VST_GN_COLSTAT") == "1"  # opt-in
