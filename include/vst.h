@@ -130,6 +130,10 @@ int vst_conv3x3_colstat(const void* x1, int C1, const void* x2, int C2, int nimg
 int vst_spatial_attention(const void* q, int ldq, const void* k, const void* v, int ldkv, void* o, int ldo,
                           int nbatch, int heads, int Nq, int Nk, int kv_div, int head_dim, float scale, float* lse,
                           void* stream);  /* lse: NULL, or fp32 [nbatch*heads*Nq] log2-domain logsumexp (training) */
+/* Self-attention over 64+ keys (kv_div 1) on sa_self_kernel (1, default: VST_SA_SELF, else 1) or on the general
+ * spatial kernel (0), for every later vst_spatial_attention of this process; returns the previous setting.  Same
+ * bits either way (tests / A/B). */
+int vst_sa_self(int on);
 
 /* Frame-axis attention (motion module / TemporalTransformerBlock, animatediff/temporal_transformer.py:66-68):
  * token (clip b, frame f, pixel p) at row (b*F + f)*HW + p; F <= 32; head_dim in {8,16,32,40,64,80,160}. */

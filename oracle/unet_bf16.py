@@ -80,16 +80,19 @@ def mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 
 
 def conv2d(img, w, b, stride):
-    """F.conv2d (pad 1) in fp32, input channels in two halves under split_k_reassociation, fp64 under
-    fp64_accumulation."""
-    c = img.shape[1]
-    if _FP64:
-        return F.conv2d(img.double(), w.double(), None if b is None else b.double(), stride=stride, padding=1).float()
-    if not _SPLIT_K or c < 2:
-        return F.conv2d(img, w, b, stride=stride, padding=1)
-    h = c // 2
-    return (F.conv2d(img[:, :h], w[:, :h], None, stride=stride, padding=1)
-            + F.conv2d(img[:, h:], w[:, h:], b, stride=stride, padding=1))
+    """3x3 conv (pad 1) in fp32 as an explicit im2col GEMM: the (channel, ky, kx) patch matrix of F.unfold times the
+    flattened weights through mm(), so the split_k_reassociation / fp64_accumulation probes apply to it like to every
+    other contraction (the split falls between the two channel halves).  Not F.conv2d: on the GPU that dispatches to
+    MIOpen, whose algorithm choice (and so the fp32 summation order) may differ from box to box (VERDICT r5 weak #1,
+    lead 2), and the emulation is the yardstick the HIP path is gated against."""
+    n, c, H, W = img.shape
+    co = w.shape[0]
+    OH, OW = (H - 1) // stride + 1, (W - 1) // stride + 1
+    cols = F.unfold(img, 3, padding=1, stride=stride)            # [n, c*9, OH*OW], rows ordered (c, ky, kx)
+    y = mm(cols.transpose(1, 2), w.reshape(co, c * 9).t())       # [n, OH*OW, co]
+    if b is not None:
+        y = y + b
+    return y.transpose(1, 2).reshape(n, co, OH, OW)
 
 
 def _w(P, k):

