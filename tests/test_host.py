@@ -235,4 +235,11 @@ def test_colstat_registry_host_logic():
     assert K.colstat_of(out) is cs
     K.colstat_reset()
     assert K.colstat_of(out) is None
-    assert not K.colstat_enabled() or os.environ.get("VST_GN_COLSTAT") == "1"  # opt-in
+    # a raw-pointer write into the tensor (a K.* wrapper given out=, which does not bump _version) drops the entry
+    K._COLSTAT[out.data_ptr()] = (weakref.ref(out), out._version, cs)
+    K._wrote(out)
+    assert K.colstat_of(out) is None
+    K._COLSTAT[out.data_ptr()] = (weakref.ref(out), out._version, cs)
+    with pytest.raises(K._lib.VstError):                     # _dev(out, ...) drops it too (then refuses the CPU tensor)
+        K._dev(out, torch.bfloat16, "out")
+    assert K.colstat_of(out) is None

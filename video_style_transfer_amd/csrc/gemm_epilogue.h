@@ -21,7 +21,7 @@ __device__ __forceinline__ int p8_acc_row(const int i, const int wc) {
   }
 }
 
-template <class Cfg, int EPI, bool ROT = false>
+template <class Cfg, int EPI, bool ROT = false, bool CS_OK = false>
 __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, char* smem, const int m0, const int n0,
                                               f32x4 (&acc)[Cfg::MI][Cfg::NJ], const int wr, const int wc,
                                               const int tid = threadIdx.x) {
@@ -39,7 +39,9 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, char* smem, con
   // GroupNorm column statistics (128x320 conv tiles, p.colstat; gn_colstat_kernel restates the same arithmetic):
   // the store pass then maps thread t to one 8-channel column (t mod 40) and rows t / 40 + 12 j, sums the stored bf16
   // values and their squares in registers (fixed order), and the 12 row groups are added in order through the LDS.
-  constexpr bool CSTAT = EPI == 0 && BM == 128 && BN == 320;
+  // Compiled in only where the caller can ask for it (CS_OK: the 8-phase conv kernels), so the 128x320 projection and
+  // in-GEMM LoRA epilogues keep their 10 store items and no runtime branch.
+  constexpr bool CSTAT = CS_OK && EPI == 0 && BM == 128 && BN == 320;
   constexpr int CS_RG = Cfg::THREADS / CPR, CS_RPT = (BM + CS_RG - 1) / CS_RG;  // 12 row groups, 11 rows each
   constexpr int NIT = CSTAT && CS_RPT > ITEMS ? CS_RPT : ITEMS;
   const bool cs = CSTAT && p.colstat;

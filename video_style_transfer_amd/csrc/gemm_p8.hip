@@ -1188,7 +1188,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
 #else
   if constexpr (EPI == 4) xattn_epilogue<Cfg, LORA>(p, smem, m0, n0, acc, wr, wc);
   else if constexpr (EPI == 5) tattn_epilogue<Cfg>(p, smem, m0, n0, acc, wr, wc);
-  else tile_epilogue<Cfg, EPI, LORA>(p, smem, m0, n0, acc, wr, wc);
+  else tile_epilogue<Cfg, EPI, LORA, CONV>(p, smem, m0, n0, acc, wr, wc);
 #endif
 #ifdef VST_P8_TRACE
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

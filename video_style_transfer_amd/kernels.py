@@ -86,10 +86,12 @@ _FUSION_WORLD = [1]
 
 class fusion_world:
     """Inside: shape-dependent fusion decisions are taken as a P-way frame-sharded rank takes them, so a forward here
-    computes exactly the bits of a P-way sharded forward.  The one such decision is the motion attention fused into
-    its q/k/v GEMM (vst_gemm_temporal_attention), which needs the pixels a rank holds to be a multiple of 16: with the
-    all-to-all exchange a rank holds H*W/P pixels, so an unsharded forward (or an all-gather rank, which holds all
-    H*W) under fusion_world(P) fuses a layer only when (H*W) % (16 P) == 0.  UNetMotionModel.forward_tokens enters it
+    computes exactly the bits of a P-way sharded forward.  Two decisions depend on the pixels a rank holds (with the
+    all-to-all exchange H*W/P of them): the motion attention fused into its q/k/v GEMM (vst_gemm_temporal_attention,
+    default), which needs a multiple of 16 pixels, so an unsharded forward (or an all-gather rank, which holds all
+    H*W) under fusion_world(P) fuses a layer only when (H*W) % (16 P) == 0; and the opt-in whole-block motion kernel
+    (VST_MOTION_FUSE=1, unet_motion._fused_motion_ops_impl), which also asks vst_motion_attention_block_supported
+    for H*W/P.  UNetMotionModel.forward_tokens enters it
     with the shard's world size (or its `fusion_world` argument); the all-to-all branch of MotionModule, whose
     pixels are already split, re-enters it with 1."""
 
@@ -137,7 +139,16 @@ def _workspace(device):
     return ws
 
 
+def _wrote(t):
+    """A launch is about to write t through a raw pointer (which does not bump t._version): drop any GroupNorm column
+    statistics registered for its storage (colstat_of), so they are never read for overwritten data."""
+    if _COLSTAT and t is not None:
+        _COLSTAT.pop(t.data_ptr(), None)
+
+
 def _dev(t: torch.Tensor, dtype, name):
+    if name == "out":
+        _wrote(t)
     if not t.is_cuda:
         raise _lib.VstError(f"{name}: tensor is on {t.device}; the HIP path has no CPU fallback")
     if t.dtype != dtype:
@@ -233,6 +244,21 @@ class p8_persist:
 
     def __exit__(self, *a):
         _lib.load().vst_p8_persist(self.prev)
+
+
+class sa_self:
+    """Context manager routing the long self-attention to sa_self_kernel (on=True, the default) or to the general
+    spatial kernel (vst_sa_self); tests and A/B runs only (the outputs are the same bits either way)."""
+
+    def __init__(self, on=True):
+        self.on = int(bool(on))
+
+    def __enter__(self):
+        self.prev = int(_lib.load().vst_sa_self(self.on))
+        return self
+
+    def __exit__(self, *a):
+        _lib.load().vst_sa_self(self.prev)
 
 
 class p8_tile_width:
@@ -509,6 +535,7 @@ def conv3x3(x1: torch.Tensor, nimg: int, H: int, W: int, w: torch.Tensor, bias: 
     M = nimg * OH * OW
     if out is None:
         out = torch.empty((M, Cout), dtype=BF16, device=x1.device)
+    _wrote(out)
     if bias is not None and (bias.dtype != F32 or bias.numel() != Cout):
         raise _lib.VstError("conv3x3: bias must be fp32 [Cout]")
     if residual is not None:
@@ -571,6 +598,7 @@ def temporal_attention(q, k, v, nclip, F, HW, heads, head_dim, out=None, scale=N
         raise _lib.VstError("temporal_attention: rows != nclip*F*HW")
     if out is None:
         out = torch.empty((q.shape[0], heads * head_dim), dtype=BF16, device=q.device)
+    _wrote(out)
     scale = head_dim ** -0.5 if scale is None else scale
     T = nclip * F * HW
     with _Rec("temporal_attention", 4.0 * T * F * heads * head_dim, 2.0 * 4 * T * heads * head_dim):
@@ -630,10 +658,20 @@ def group_norm(x1, nsamples, rows_per_sample, groups, eps, gamma, beta, *, silu=
         raise _lib.VstError("group_norm: rows != nsamples*rows_per_sample")
     if out is None:
         out = torch.empty((x1.shape[0], C), dtype=BF16, device=x1.device)
+    _wrote(out)
     ws_bytes = _lib.load().vst_groupnorm_workspace_bytes(nsamples, rows_per_sample, groups, C)
     ws = torch.empty((ws_bytes + 3) // 4, dtype=F32, device=x1.device)
     if colstat is not None:
         cs1, cs2 = colstat
+        for nm, cs, src in (("cs1", cs1, x1), ("cs2", cs2, x2)):
+            if (cs is None) != (src is None):
+                raise _lib.VstError(f"group_norm: {nm} must be given exactly when its source is")
+            if cs is None:
+                continue
+            want = ((src.shape[0] + 127) // 128, src.shape[1], 2)
+            if tuple(cs.shape) != want or cs.dtype != F32 or cs.device != src.device or not cs.is_contiguous():
+                raise _lib.VstError(f"group_norm: {nm} must be contiguous fp32 {want} on {src.device}, got "
+                                    f"{tuple(cs.shape)} {cs.dtype} on {cs.device}")
         with _Rec("groupnorm", 0.0, 2.0 * 2 * x1.shape[0] * C):  # one read + one write
             _lib.call("vst_groupnorm_colstat", _p(x1), _ld(x1), x1.shape[1], _p(cs1), _p(x2),
                       0 if x2 is None else _ld(x2), 0 if x2 is None else x2.shape[1], _p(cs2), nsamples,
@@ -697,6 +735,7 @@ def permute_rows(src, dims, perm, out=None):
         raise _lib.VstError("permute_rows: src must be contiguous with prod(dims) rows")
     if out is None:
         out = torch.empty_like(src)
+    _wrote(out)
     with _Rec("permute", 0.0, 2.0 * 2 * src.numel()):
         _lib.call("vst_permute_rows", _p(src), _p(out), src.shape[1], *dims, *perm, _stream())
     return out
@@ -710,6 +749,7 @@ def add_row_table(x, table, *, div=1, mod=1, out=None):
         raise _lib.VstError("add_row_table: table must be fp32 [>= mod, C] on device")
     if out is None:
         out = torch.empty((rows, C), dtype=BF16, device=x.device)
+    _wrote(out)
     with _Rec("add_row_table", 0.0, 2.0 * 2 * rows * C):
         _lib.call("vst_add_row_table", _p(x), _ld(x), C, rows, _p(table.contiguous()), div, mod, _p(out), _ld(out),
                   _stream())
@@ -738,6 +778,7 @@ def layer_norm_lora(x, gamma, beta, eps, A, *, r_alg=None, out=None):
         raise _lib.VstError(f"layer_norm_lora: x {tuple(x.shape)} A {tuple(A.shape)}")
     if out is None:
         out = torch.empty((rows, C), dtype=BF16, device=x.device)
+    _wrote(out)
     u = torch.empty((rows, R), dtype=BF16, device=x.device)
     with _Rec("layernorm_lora", 2.0 * rows * C * (r_alg or R), 2.0 * (2 * rows * C + rows * R)):
         _lib.call("vst_layernorm_lora", _p(x), _ld(x), C, rows, _p(gamma), _p(beta), float(eps), _p(A), R, _p(out),
@@ -750,6 +791,7 @@ def layer_norm(x, gamma, beta, eps=1e-5, *, pe=None, pe_div=1, pe_mod=1, out=Non
     rows, C = x.shape
     if out is None:
         out = torch.empty((rows, C), dtype=BF16, device=x.device)
+    _wrote(out)
     with _Rec("layernorm", 0.0, 2.0 * 2 * rows * C):
         _lib.call("vst_layernorm", _p(x), _ld(x), C, rows, _p(gamma), _p(beta), float(eps), _p(pe), pe_div, pe_mod,
                   _p(out), _ld(out), _stream())
@@ -767,12 +809,14 @@ def timestep_embedding(t, n, dim, out, *, col0=0, per_row=1, step_idx=None, flip
 
 def silu(x, out=None):
     out = torch.empty_like(x) if out is None else out
+    _wrote(out)
     _lib.call("vst_silu", _p(x), _p(out), x.numel(), _stream())
     return out
 
 
 def add(a, b, out=None):
     out = torch.empty_like(a) if out is None else out
+    _wrote(out)
     _lib.call("vst_add", _p(a), _p(b), _p(out), a.numel(), _stream())
     return out
 
@@ -783,6 +827,7 @@ def transpose(x, out=None):
     rows, cols = x.shape
     if out is None:
         out = torch.empty((cols, rows), dtype=BF16, device=x.device)
+    _wrote(out)
     with _Rec("transpose", 0.0, 2.0 * 2 * rows * cols):
         _lib.call("vst_transpose", _p(x), _ld(x), rows, cols, _p(out), _ld(out), _stream())
     return out

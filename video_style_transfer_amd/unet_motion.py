@@ -237,6 +237,11 @@ def _fused_motion_ops_impl(block, C, F, HW):
     # opt-in (VST_MOTION_FUSE=1): the fused block is correct but measured slower than the four launches
     if os.environ.get("VST_MOTION_FUSE") != "1" or not K.motion_block_fusable(C, F, HW, block.attn1.heads):
         return None
+    # shape-dependent like the fused frame attention (kernels.fusion_world): decide as a P-way all-to-all rank, which
+    # holds HW / P pixels, decides, so an unsharded forward under fusion_world(P) equals the shards bit for bit
+    P = K.fusion_pixel_div()
+    if P > 1 and (HW % P or not K.motion_block_fusable(C, F, HW // P, block.attn1.heads)):
+        return None
     out = []
     for attn in (block.attn1, block.attn2):
         if type(attn.processor) is not AttnProcessor2_0 or attn.heads != block.attn1.heads:
