@@ -65,6 +65,13 @@ def parse():
     ap.add_argument("--configs3", default="auto", choices=["auto", "on", "off"],
                     help="frames mode, N>1: also time BASELINE configs[3] (one --configs3-frames x --configs3-size^2 "
                          "clip frame-sharded over the ranks) under sub_records.configs3 (auto: at N=8)")
+    ap.add_argument("--gather-record", default="auto", choices=["auto", "on", "off"],
+                    help="frames mode, N>1, --exchange all_to_all: also time the headline workload with the north "
+                         "star's exchange (an all-gather of the clip before each motion module) under "
+                         "sub_records.all_gather (auto: whenever N>1)")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="frames mode, all_to_all: run each motion module's exchange as one blocking collective "
+                         "(default: the CFG pair in two halves whose all-to-alls overlap the other half's compute)")
     ap.add_argument("--configs3-frames", type=int, default=32)
     ap.add_argument("--configs3-size", type=int, default=768)
     ap.add_argument("--no-graph", action="store_true")
@@ -632,24 +639,31 @@ def main():
         plans = []
         if want_strong:
             plans.append(("strong_1clip", args.frames, args.size))
+        want_gather = args.exchange == "all_to_all" and (
+            args.gather_record == "on" or args.gather_record == "auto")
+        if want_gather:  # the north star's own exchange on the headline workload, next to the all-to-all headline
+            plans.append(("all_gather", args.frames, args.size, nclips, "all_gather"))
         if want_c3:
-            plans.append(("configs3", args.configs3_frames, args.configs3_size))
-        for name, fr, sz in plans:
+            plans.append(("configs3", args.configs3_frames, args.configs3_size, 1, args.exchange))
+        plans = [p if len(p) == 5 else p + (1, args.exchange) for p in plans]
+        for name, fr, sz, ncl, exch in plans:
             if fr % world:
                 subs[name] = {"skipped": f"{fr} frames do not split over {world} ranks"}
                 continue
-            r = timed_denoise(args, unet, cfg, world, rank, dev, rehearsal, frames=fr, size=sz, nclips=1,
-                              sharded=True)
+            r = timed_denoise(args, unet, cfg, world, rank, dev, rehearsal, frames=fr, size=sz, nclips=ncl,
+                              sharded=True, exchange=exch)
             subs[name] = {
                 "value": round(r["value"], 4), "unit": "frames/s", "ms_per_step": round(r["ms_per_step"], 3),
-                "n_gpus": world, "scaling": "strong", "frames": fr, "resolution": sz, "clips": 1,
-                "frames_per_gpu": fr // world, "graph": r["den"].graph is not None, "note": r["graph_note"],
+                "n_gpus": world, "scaling": "strong" if ncl < world else "weak", "frames": fr, "resolution": sz,
+                "clips": ncl, "frames_per_gpu": fr // world, "graph": r["den"].graph is not None,
+                "note": r["graph_note"], "exchange": exch, "overlap": r["overlap"],
                 "shard_preflight": r["preflight"],
                 "finite": bool(torch.isfinite(r["den"].lat).all().item()),
                 "workload": ("BASELINE configs[3]: " if name == "configs3" else "") +
-                            f"one {fr}x{sz}x{sz} clip + UnZipLoRA rank-{args.lora_rank}, CFG pair, frame-sharded "
-                            f"x{world} ({fr // world} frames/GPU, "
-                            + ("all-to-all" if args.exchange == "all_to_all" else "all-gather") + ")"}
+                            f"{ncl} {fr}x{sz}x{sz} clip(s) + UnZipLoRA rank-{args.lora_rank}, CFG pair, frame-sharded "
+                            f"x{world} ({fr // world} frames/clip/GPU, "
+                            + ("all-to-all" if exch == "all_to_all" else "all-gather of the clip before each motion "
+                                                                         "module (the north star's exchange)") + ")"}
             r["den"].graph = None
             del r
             torch.cuda.empty_cache()
@@ -678,7 +692,7 @@ def main():
                                        if sharded else
                                        f"replicas x{world}" if world > 1 else "single") + (
                                        f", {nclips} clips batched per GPU" if not sharded and nclips > 1 else ""),
-                       "graph": graphed,
+                       "graph": graphed, "exchange_overlap": head["overlap"],
                        "note": head["graph_note"]},
             "roofline": rl, "step_roofline": step, "vae_decode": vae_rec, "cpu_baseline": cpu, "kernels": table,
             "finite": ok, "shard_preflight": head["preflight"], "sub_records": subs or None,
@@ -691,7 +705,7 @@ def main():
         dist.destroy_process_group()  # (every HIP graph released above: a graph must not outlive the communicator)
 
 
-def timed_denoise(args, unet, cfg, world, rank, dev, rehearsal, *, frames, size, nclips, sharded):
+def timed_denoise(args, unet, cfg, world, rank, dev, rehearsal, *, frames, size, nclips, sharded, exchange=None):
     """One denoiser of `nclips` clips of `frames` x size^2 (frame-sharded over the ranks when `sharded`): preflight
     (sharded), capture (one HIP graph; piecewise at N > 1), --warmup untimed and --steps timed replays bracketed by
     barrier + synchronize, the max over ranks.  Returns the denoiser (for the roofline / VAE records) and the timing."""
@@ -699,7 +713,7 @@ def timed_denoise(args, unet, cfg, world, rank, dev, rehearsal, *, frames, size,
     shard = None
     if sharded:
         from video_style_transfer_amd.frame_shard import FrameShard
-        shard = FrameShard(exchange=args.exchange)
+        shard = FrameShard(exchange=exchange or args.exchange, overlap=not args.no_overlap)
     den = AnimateDiffDenoiser(unet, frames, size, size, num_inference_steps=args.num_inference_steps,
                               guidance_scale=args.guidance, device=dev, shard=shard, num_clips=nclips)
     seed_rank = 0 if shard is not None else rank  # sharded ranks hold frames of the SAME clips
@@ -769,7 +783,8 @@ def timed_denoise(args, unet, cfg, world, rank, dev, rehearsal, *, frames, size,
     # frames mode: nclips whole clips spread over all ranks; replicas: every rank denoises its own clip
     frames_total = frames * nclips if shard is not None else frames * nclips * world
     value = frames_total / (args.num_inference_steps * ms_step * 1e-3)
-    return {"den": den, "ms_per_step": ms_step, "value": value, "preflight": preflight, "graph_note": graph_note}
+    return {"den": den, "ms_per_step": ms_step, "value": value, "preflight": preflight, "graph_note": graph_note,
+            "overlap": None if shard is None else shard.overlap}
 
 
 if __name__ == "__main__":

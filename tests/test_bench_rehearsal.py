@@ -43,9 +43,12 @@ def test_bench_two_rank_frame_shard_rehearsal():
     # the sub-records the driver's N-GPU run adds: one clip split over the ranks (strong scaling) and configs[3]'s
     # shape class (here 8 frames at 256^2 so the rehearsal stays short), each with its own bitwise preflight
     subs = d["sub_records"]
-    for name in ("strong_1clip", "configs3"):
+    assert d["config"]["exchange_overlap"] is True  # the headline runs the overlapped all-to-all (CFG pair halves)
+    for name in ("strong_1clip", "configs3", "all_gather"):
         r = subs[name]
         print(f"[rehearsal] {name}: {r['ms_per_step']} ms/step, {r['frames_per_gpu']} frames/GPU, "
-              f"preflight {r['shard_preflight']}")
-        assert r["scaling"] == "strong" and r["finite"] and r["value"] > 0
+              f"exchange {r['exchange']} (overlap {r['overlap']}), preflight {r['shard_preflight']}")
+        assert r["scaling"] == ("weak" if name == "all_gather" else "strong") and r["finite"] and r["value"] > 0
         assert r["shard_preflight"]["bitwise_equal"], r["shard_preflight"]
+    # the north star's exchange on the headline workload (sub_records.all_gather): same clips, same bits
+    assert subs["all_gather"]["exchange"] == "all_gather" and subs["all_gather"]["clips"] == 2

@@ -65,6 +65,31 @@ def _cpu_worker(rank, world, port, q, F=4):
         gx = sh.gather_frames(x_loc, B, Fl, HW)
         assert torch.equal(gx, X.reshape(-1, C)), "gather_frames layout"
         assert torch.equal(sh.local_frames_of(gx, B, Fl, HW), x_loc), "local_frames_of(gather_frames(x)) != x"
+        # (b'') the overlapped schedule (FrameShard.pipelined: the batch in two halves, each half's exchange issued
+        # before the other half computes) gives the one-slice schedule's bits; mid() is a frame-axis op (a running sum
+        # over every frame of each pixel), so it only matches if each half really holds all frames of its pixels
+        def mid_op(h, nb):
+            return h.view(nb, F, hp, C).cumsum(1).reshape(-1, C) * 0.5
+
+        ref_all = sh.to_frames(mid_op(sh.to_pixels(x_loc * 3.0, B, Fl, HW), B), B, Fl, HW) + x_loc
+        nb, rows = B // 2, (B // 2) * Fl * HW
+        got = torch.empty_like(x_loc)
+        order = []
+
+        def pre(i):
+            order.append(("pre", i))
+            return x_loc[i * rows:(i + 1) * rows] * 3.0
+
+        def mid(i, h):
+            order.append(("mid", i))
+            return mid_op(h, nb)
+
+        def post(i, h):
+            order.append(("post", i))
+            got[i * rows:(i + 1) * rows] = h + x_loc[i * rows:(i + 1) * rows]
+        sh.pipelined(2, pre, mid, post, nb, Fl, HW)
+        assert torch.equal(got, ref_all), "pipelined exchange != one-slice exchange"
+        assert order == [("pre", 0), ("pre", 1), ("mid", 0), ("mid", 1), ("post", 0), ("post", 1)], order
         # (c) sharded motion module == oracle motion module
         P = {}
         g = torch.Generator().manual_seed(1)
@@ -312,6 +337,53 @@ def test_frame_shard_sdxl_cfg_pair_one_gpu(world, F, hw):
     res = _spawn(_gpu_worker_sdxl_cfg, world, F, hw)
     for rank, status, info in res:
         print(f"[shard] CFG pair rank {rank}: {status} {info}")
+        assert status == "ok", f"rank {rank}: {info}"
+
+
+def _gpu_worker_overlap(rank, world, port, q):
+    """The overlapped exchange (FrameShard(overlap=True): each motion module's CFG pair as two halves whose all-to-alls
+    run under the other half's compute) against the one-slice exchange and against the unsharded forward: the tiny
+    UNet, CFG pair, 8 frames over `world` ranks; all three bit-identical."""
+    try:
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        _init(rank, world, port)
+        from test_parity_gpu import _setup
+        from video_style_transfer_amd.frame_shard import FrameShard
+        from video_style_transfer_amd.utils import build_unet
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        F = 8
+        cfg, sd, lat, enc, pooled, tids = _setup("tiny", F, 16, seed=9, B=2)
+        unet = build_unet(cfg, state_dict=sd, device=dev)
+        kw = dict(added_cond_kwargs={"text_embeds": pooled.to(dev), "time_ids": tids.to(dev)})
+        t = torch.tensor([421.0, 421.0])
+        outs = {}
+        for ov in (True, False):
+            sh = FrameShard(overlap=ov)
+            Fl, f0 = sh.local_frames(F)
+            outs[ov] = unet(lat[:, :, f0:f0 + Fl].contiguous().to(dev), t.to(dev), enc.to(dev), frame_shard=sh,
+                            **kw).sample.float().cpu()
+        full = unet(lat.to(dev), t.to(dev), enc.to(dev), fusion_world=world, **kw).sample.float().cpu()
+        same_ov = torch.equal(outs[True], outs[False])
+        same_full = torch.equal(outs[True], full[:, :, f0:f0 + Fl])
+        q.put((rank, "ok" if same_ov and same_full else "fail",
+               f"overlapped == one-slice exchange: {same_ov}; == unsharded: {same_full}"))
+    except BaseException:  # noqa: BLE001
+        import traceback
+        q.put((rank, "fail", traceback.format_exc()[-2000:]))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_frame_shard_overlapped_exchange_two_ranks_one_gpu():
+    if torch.cuda.device_count() == 0:
+        pytest.skip("no HIP device")
+    res = _spawn(_gpu_worker_overlap, 2)
+    for rank, status, info in res:
+        print(f"[shard] overlap rank {rank}: {status} {info}")
         assert status == "ok", f"rank {rank}: {info}"
 
 

@@ -34,6 +34,7 @@ CPU) gets the same captured step as nccl (= RCCL).
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, Optional, Sequence
 
 import torch
@@ -123,12 +124,18 @@ class PiecewiseGraph:
 class FrameShard:
     EXCHANGES = ("all_to_all", "all_gather")
 
-    def __init__(self, group=None, permute: Optional[Permute] = None, exchange: str = "all_to_all"):
+    def __init__(self, group=None, permute: Optional[Permute] = None, exchange: str = "all_to_all",
+                 overlap: Optional[bool] = None):
+        """overlap (all_to_all only): run each motion module's batch as two halves whose exchanges overlap the other
+        half's compute (pipelined; same bits).  Default: VST_SHARD_OVERLAP, else on."""
         if not dist.is_initialized():
             raise RuntimeError("FrameShard needs an initialised torch.distributed process group")
         if exchange not in self.EXCHANGES:
             raise ValueError(f"exchange {exchange!r}: one of {self.EXCHANGES}")
         self.exchange = exchange
+        if overlap is None:
+            overlap = os.environ.get("VST_SHARD_OVERLAP", "1") != "0"
+        self.overlap = bool(overlap) and exchange == "all_to_all"
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -200,6 +207,28 @@ class FrameShard:
                 dist.all_to_all_single(out, inp, group=self.group)
         self._issue(op)
 
+    def _all_to_all_begin(self, out: torch.Tensor, inp: torch.Tensor):
+        """Issue the all-to-all without making the compute stream wait for it; returns the `wait` to call before `out`
+        is read.  nccl (RCCL): async_op=True -- the collective runs on RCCL's stream after the work already queued on
+        the current stream, so the kernels queued between begin and wait overlap it.  gloo (host-staged): done at
+        begin (no overlap; same result).  Under piecewise capture both halves are host items between graph pieces."""
+        slot = {}
+
+        def issue():
+            if self._staged(inp):
+                ho = torch.empty(out.shape, dtype=out.dtype)
+                dist.all_to_all_single(ho, inp.cpu(), group=self.group)
+                out.copy_(ho)
+            else:
+                slot["work"] = dist.all_to_all_single(out, inp, group=self.group, async_op=True)
+
+        def wait():
+            w = slot.pop("work", None)
+            if w is not None:
+                w.wait()  # the current stream waits for RCCL's (no host block)
+        self._issue(issue)
+        return lambda: self._issue(wait)
+
     # ---- layout exchange ------------------------------------------------------------------
     def to_pixels(self, h: torch.Tensor, B: int, Fl: int, HW: int) -> torch.Tensor:
         """rows (b, f_local, p) over this rank's frames -> rows (b, f_global, p') over pixel slab `rank`
@@ -240,4 +269,49 @@ class FrameShard:
         recv = torch.empty_like(send)
         self._all_to_all(recv, send)                             # (source slab q, b, f_local, p')
         return self._permute(recv, (P, B, Fl, hp), (1, 2, 0, 3))  # (b, f_local, q*hp + p')
+
+    # ---- the exchange overlapped with compute -------------------------------------------------
+    def _to_pixels_begin(self, h, B, Fl, HW):
+        P, hp = self.world, HW // self.world
+        send = self._permute(h, (B, Fl, P, hp), (2, 0, 1, 3))
+        recv = torch.empty_like(send)
+        wait = self._all_to_all_begin(recv, send)
+
+        def end():
+            wait()
+            return self._permute(recv, (P, B, Fl, hp), (1, 0, 2, 3))
+        return end, send  # (send is held until end: the collective reads it)
+
+    def _to_frames_begin(self, h, B, Fl, HW):
+        P, hp = self.world, HW // self.world
+        send = self._permute(h, (B, P, Fl, hp), (1, 0, 2, 3))
+        recv = torch.empty_like(send)
+        wait = self._all_to_all_begin(recv, send)
+
+        def end():
+            wait()
+            return self._permute(recv, (P, B, Fl, hp), (1, 2, 0, 3))
+        return end, send
+
+    def pipelined(self, nparts: int, pre, mid, post, B: int, Fl: int, HW: int) -> None:
+        """The all-to-all motion-module schedule over `nparts` equal slices of the batch (B = clips per slice), so
+        that each slice's exchange runs while the previous slice computes (the exchange overlapped with
+        compute):
+            pre(0) x0  pre(1) x1  w0 mid(0) x0'  w1 mid(1) x1'  w0' post(0)  w1' post(1)
+        pre(i) -> rows (b, f_local, p) of slice i (GroupNorm + proj_in); mid(i, h) on rows (b, f_global, p') of
+        pixel slab `rank` (the transformer block); post(i, h) consumes rows (b, f_local, p) (proj_out + residual).
+        x = an all-to-all issued (to_pixels / to_frames), w = its wait.  Every slice runs the same row-wise ops on
+        its own rows as the one-slice schedule, so the result is the same bits (test_frame_shard.py)."""
+        if self.world == 1 or HW % self.world:
+            raise ValueError(f"pipelined exchange: {HW} pixels over {self.world} ranks")
+        ends = []
+        for i in range(nparts):
+            ends.append(self._to_pixels_begin(pre(i), B, Fl, HW))
+        for i in range(nparts):
+            end, _send = ends[i]
+            ends[i] = self._to_frames_begin(mid(i, end()), B, Fl, HW)
+        for i in range(nparts):
+            end, _send = ends[i]
+            post(i, end())
+            ends[i] = None
 

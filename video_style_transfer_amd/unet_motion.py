@@ -313,6 +313,8 @@ class MotionModule(nn.Module):
         P = 1 if shard is None else shard.world
         if P > 1:
             part = shard.all_gather(part)
+            if shard.overlap and B % 2 == 0 and HW % P == 0:
+                return self._run_overlapped(x, B, ctx.F, HW, P, ctx, part)
         h = K.group_norm_apply_partials(x, B, ctx.F, HW, G, self.norm.eps, f32(self.norm.weight), f32(self.norm.bias),
                                         part, P)
         h = self.proj_in.run(h)
@@ -329,6 +331,36 @@ class MotionModule(nn.Module):
                 h = blk.run(h, B * Fl * P, HW // P, tctx)
         h = shard.to_frames(h, B, Fl, HW)
         return self.proj_out.run(h, residual=x)
+
+    def _run_overlapped(self, x, B, Fl, HW, P, ctx, part):
+        """The all-to-all branch with the batch in two halves (the CFG pair's uncond / cond clips), so each half's
+        exchange runs while the other half computes (FrameShard.pipelined): GroupNorm + proj_in of half 1 under half
+        0's frame -> pixel exchange, half 0's transformer block under half 1's, and so on.  Every op is row-wise on
+        its half's rows (the GroupNorm statistics are per clip, from the all-gathered partials), so the output is the
+        one-half schedule's bits (tests/test_frame_shard.py)."""
+        G, nb = self.norm.num_groups, B // 2
+        rows = nb * Fl * HW
+        out = torch.empty_like(x)
+        tctx = dataclasses.replace(ctx, F=Fl * P)
+        w, bias = f32(self.norm.weight), f32(self.norm.bias)
+
+        def pre(i):
+            xs = x[i * rows:(i + 1) * rows]
+            ps = part[:, i * nb * Fl:(i + 1) * nb * Fl].contiguous()  # [P, nb*Fl, chunks, G, 2]: this half's clips
+            h = K.group_norm_apply_partials(xs, nb, Fl, HW, G, self.norm.eps, w, bias, ps, P)
+            return self.proj_in.run(h)
+
+        def mid(i, h):
+            with K.fusion_world(1):  # (these HW // P pixels are this rank's share already)
+                for blk in self.transformer_blocks:
+                    h = blk.run(h, nb * Fl * P, HW // P, tctx)
+            return h
+
+        def post(i, h):
+            self.proj_out.run(h, residual=x[i * rows:(i + 1) * rows], out=out[i * rows:(i + 1) * rows])
+
+        ctx.shard.pipelined(2, pre, mid, post, nb, Fl, HW)
+        return out
 
 
 class ResnetBlock2D(nn.Module):
