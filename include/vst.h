@@ -321,6 +321,10 @@ int vst_vae_sample(const void* moments, int ld, int n, int HW, const float* eps,
  * with 16-B loads.  `out` receives nothing in practice (anti-dead-code sink, >= grid elements). */
 int vst_probe_mfma(int grid, int iters, float* out, void* stream);
 int vst_probe_hbm_read(const void* src, size_t bytes, int grid, unsigned* out, void* stream);
+/* vst_probe_fetch: the per-CU operand fetch rate from an L2-resident `bytes` region (the GEMM loaders' path): `grid`
+ * 512-thread workgroups, each wave moving `iters` 1-KiB pieces, 8 in flight; mode 0 buffer loads into VGPRs, 1 LDS-DMA
+ * into an LDS ring (the 8-phase GEMM's loader), 2 buffer loads + ds_write_b128 (a register-staged loader). */
+int vst_probe_fetch(int mode, const void* src, int bytes, int grid, int iters, unsigned* out, void* stream);
 const char* vst_version(void);
 
 #ifdef __cplusplus

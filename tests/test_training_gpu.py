@@ -418,6 +418,38 @@ def test_transformer2d_backward_vs_oracle(cuda, unfreeze_mergers):
             assert e < 5e-2, (n, e)
 
 
+class _SplitKProbe(torch.overrides.TorchFunctionMode):
+    """Reassociation probe of the CPU bf16-autocast yardstick (the forward gates' method): every
+    linear / matmul / conv2d of the oracle computed as two separately accumulated K halves (input channels for the
+    conv) and summed -- the same math in another summation order, each half rounded by autocast like the whole.  Its
+    distance from the plain yardstick is the per-tensor noise floor of 'a bf16 implementation of this math'."""
+
+    def __torch_function__(self, func, types, args=(), kwargs=None):
+        import torch.nn.functional as F
+        kwargs = kwargs or {}
+        if func is F.linear:
+            x, w = args[0], args[1]
+            b = args[2] if len(args) > 2 else kwargs.get("bias")
+            h = x.shape[-1] // 2
+            if h:
+                return F.linear(x[..., :h], w[:, :h]) + F.linear(x[..., h:], w[:, h:], b)
+        elif func in (torch.matmul, torch.Tensor.__matmul__):
+            a, m = args[0], args[1]
+            h = a.shape[-1] // 2
+            if h and a.dim() >= 2 and m.dim() >= 2:
+                return a[..., :h] @ m[..., :h, :] + a[..., h:] @ m[..., h:, :]
+        elif func is F.conv2d:
+            x, w = args[0], args[1]
+            b = args[2] if len(args) > 2 else kwargs.pop("bias", None)
+            rest = dict(kwargs)
+            rest.pop("bias", None)
+            extra = args[3:]
+            h = x.shape[1] // 2
+            if h and rest.get("groups", 1) == 1 and not extra:
+                return F.conv2d(x[:, :h], w[:, :h], None, **rest) + F.conv2d(x[:, h:], w[:, h:], b, **rest)
+        return func(*args, **kwargs)
+
+
 @pytest.mark.parametrize("config", ["tiny", "sdxl"])
 def test_unet_training_step_grads_vs_oracle(cuda, config):
     """train_animatediff.py's fwd+bwd on the whole AnimateDiff UNet: frozen spatial path with
@@ -463,7 +495,7 @@ def test_unet_training_step_grads_vs_oracle(cuda, config):
     # there it is the same bits every run (checked: all 390 motion gradients of two SDXL runs torch.equal); torch's GPU
     # autocast is not (its SDXL median moved 4.78e-2 .. 5.54e-2 over four runs, profiles/r4_train_grads_ab.txt), and a
     # gate keyed to it moved with it
-    def oracle_grads(autocast, dev):
+    def oracle_grads(autocast, dev, probe=False):
         leaves = {n: p.detach().float().to(dev).clone().requires_grad_(p.requires_grad)
                   for n, p in unet.named_parameters()}
         P = {}
@@ -477,7 +509,9 @@ def test_unet_training_step_grads_vs_oracle(cuda, config):
                 P[n + ".weight"] = leaves[n + ".base.weight"] + m.scale * leaves[n + ".lora_B"] @ leaves[n + ".lora_A"]
         for n, b in unet.named_buffers():
             P[n] = b.detach().float().to(dev)
-        with torch.autocast(dev.type, dtype=BF, enabled=autocast):
+        import contextlib
+        with torch.autocast(dev.type, dtype=BF, enabled=autocast), (_SplitKProbe() if probe else
+                                                                     contextlib.nullcontext()):
             ref = unet_forward(P, cfg.to_dict(), sample.to(dev), t.to(dev), enc.to(dev), pooled.to(dev), tids.to(dev),
                                LoRAState())
         ref_tok = ref.float().permute(0, 2, 3, 4, 1).reshape(-1, 4)
@@ -491,6 +525,7 @@ def test_unet_training_step_grads_vs_oracle(cuda, config):
         ref_tok, want = oracle_grads(False, cuda)
         torch.set_num_threads(16)
         yard_tok, yard = oracle_grads(True, torch.device("cpu"))
+        _, probe = oracle_grads(True, torch.device("cpu"), probe=True)
     finally:
         torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32 = tf32
         torch.set_num_threads(nthreads)
@@ -511,12 +546,18 @@ def test_unet_training_step_grads_vs_oracle(cuda, config):
     named = dict(unet.named_parameters())
     trainable = [n for n, p in named.items() if p.requires_grad]
     assert trainable and all("motion_modules" in n for n in trainable)
-    errs, yerr = {}, {}
+    errs, yerr, perr, pfl = {}, {}, {}, {}
     for n in trainable:
         got = named[n].grad
         assert got is not None and want[n] is not None, n
         errs[n] = rel(got, want[n])
         yerr[n] = rel(yard[n], want[n])
+        perr[n] = rel(probe[n], want[n])   # the probe: the yardstick in another summation order
+        pfl[n] = rel(probe[n], yard[n])    # its distance from the yardstick: the per-tensor reassociation floor
+    pf = sorted(pfl.values())
+    print(f"[train] {config}: yardstick reassociation probe (split-K) vs yardstick: median {pf[len(pf) // 2]:.2e}, "
+          f"95th pct {pf[int(0.95 * (len(pf) - 1))]:.2e}, max {pf[-1]:.2e}; probe vs fp32: median "
+          f"{sorted(perr.values())[len(pf) // 2]:.2e}")
     order = sorted(errs, key=errs.get)
     yorder = sorted(yerr.values())
     kinds = {}
@@ -533,24 +574,30 @@ def test_unet_training_step_grads_vs_oracle(cuda, config):
     print(f"[train] {config}: per-tensor HIP / yardstick error ratio: median {ratio[len(ratio) // 2]:.2f}, 95th pct "
           f"{ratio[int(0.95 * (len(ratio) - 1))]:.2f}, max {ratio[-1]:.2f}")
     for n in trainable:
-        print(f"[train] {config}   {n:90s} {errs[n]:.3e}  yardstick {yerr[n]:.3e}")
+        print(f"[train] {config}   {n:90s} {errs[n]:.3e}  yardstick {yerr[n]:.3e}  probe {perr[n]:.3e}")
     for k, v in sorted(kinds.items(), key=lambda kv: -kv[1]):
         print(f"[train] {config}   worst per kind {k:40s} {v:.2e}")
-    # Gates (round 5), fixed once against the deterministic CPU bf16-autocast yardstick (profiles/r5_train_grads.log):
-    #   sdxl (the production architecture, 480 tensors): every tensor within 1.25x its yardstick error (measured max
-    #        1.10x), and the distribution no worse than the yardstick's (median 4.18e-2 vs 5.46e-2, 95th pct 7.01e-2 vs
-    #        9.35e-2): the HIP gradients are at least as close to fp32 as the reference's own precision;
+    # Gates (round 5 factors, round 6 reference), against the deterministic CPU bf16-autocast yardstick AND its
+    # reassociation probe (_SplitKProbe: the same yardstick in another summation order) -- two bf16 implementations of
+    # this math, whose per-tensor errors against fp32 scatter by the probe floor printed above.  A tensor's reference
+    # error is the larger of the two, so a ulp-level change of the HIP forward (another fp32 summation order: what the
+    # probe itself is) is judged against the spread such a change produces, not against one sample of it (VERDICT r5
+    # weak #7: a round-5 attention kernel with another fma contraction moved the median 4.18e-2 -> 5.21e-2 against a
+    # single yardstick):
+    #   sdxl (the production architecture, 480 tensors): every tensor within 1.25x its reference error (round 5
+    #        measured max 1.10x against the yardstick alone), the median and 95th pct no worse than the references';
     #   tiny (F=8, 16x16, C=32/64: tensors of a few hundred elements, where one rounding flip moves a tensor's error):
-    #        every tensor within 2x its yardstick error or 3e-2 (max 1.77x, at 3.5e-2 vs 2.0e-2), median and 95th pct
-    #        within 1.1x of the yardstick's (0.91x / 0.89x measured).
-    # Both sides are the same bits every run (the HIP path and the CPU yardstick at 16 threads), so these gates do not
-    # move between runs; round 4's moved with torch's GPU autocast.
+    #        every tensor within 2x its reference error or 3e-2, median and 95th pct within 1.1x.
+    # All sides are the same bits every run (HIP, and the CPU yardstick / probe, which do not depend on the thread
+    # count), so the gates do not move between runs.
     tol_t, floor_t, tol_d = (1.25, 0.0, 1.0) if config == "sdxl" else (2.0, 3e-2, 1.1)
-    bad = {n: (e, yerr[n]) for n, e in errs.items() if e > max(floor_t, tol_t * yerr[n])}
+    refe = {n: max(yerr[n], perr[n]) for n in trainable}
+    bad = {n: (e, yerr[n], perr[n]) for n, e in errs.items() if e > max(floor_t, tol_t * refe[n])}
     assert not bad, bad
+    yorder = sorted(refe.values())
     med, ymed = errs[order[len(order) // 2]], yorder[len(yorder) // 2]
     p95, yp95 = errs[order[int(0.95 * (len(order) - 1))]], yorder[int(0.95 * (len(yorder) - 1))]
-    print(f"[train] {config}: gates: every tensor <= max({floor_t}, {tol_t} x yardstick); median {med:.3e} <= "
+    print(f"[train] {config}: gates: every tensor <= max({floor_t}, {tol_t} x max(yardstick, probe)); median {med:.3e} <= "
           f"{tol_d} x {ymed:.3e}; 95th pct {p95:.3e} <= {tol_d} x {yp95:.3e}")
     assert med <= tol_d * ymed and p95 <= tol_d * yp95, (med, ymed, p95, yp95)
 

@@ -50,7 +50,69 @@ __global__ __launch_bounds__(256) void probe_hbm_read_kernel(const void* src, si
   if (r == 0x9e3779b9u) out[blockIdx.x] = r;  // data-dependent, practically never taken
 }
 
+// Per-CU operand fetch rate from an L2-resident region (the GEMMs' operand path): one 512-thread
+// workgroup per CU, every wave moving 1 KiB pieces (16 B per lane) of a `bytes` region that stays in each XCD's L2,
+// `iters` pieces per wave, up to 8 in flight per wave:
+//   MODE 0: buffer_load_dwordx4 into VGPRs (folded into one word per lane);
+//   MODE 1: LDS-DMA (buffer_load ... lds) into a 64 KiB LDS ring, as the 8-phase GEMM's loader issues them;
+//   MODE 2: buffer_load_dwordx4 into VGPRs, then ds_write_b128 into the same ring (register-staged loader).
+template <int MODE>
+__global__ __launch_bounds__(512) void probe_fetch_kernel(const void* src, int bytes, int iters, unsigned* out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const auto r = make_rsrc(src, (uint32_t)bytes);
+  const int npieces = bytes >> 10;
+  int piece = (blockIdx.x * 8 + wid) * 97 % npieces;
+  u32x4 x = {0u, 0u, 0u, 0u};
+  char* ring = smem + wid * 8192;  // 8 KiB (8 pieces) per wave
+  for (int it = 0; it < iters; it += 8) {
+    if constexpr (MODE == 0) {
+      u32x4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = buf_load16(r, ((piece + j) % npieces) * 1024 + lane * 16);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x ^= v[j];
+    } else if constexpr (MODE == 1) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            r, (__attribute__((address_space(3))) void*)((__attribute__((address_space(3))) char*)(uintptr_t)(ring + j * 1024)),
+            16, ((piece + j) % npieces) * 1024 + lane * 16, 0, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      u32x4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = buf_load16(r, ((piece + j) % npieces) * 1024 + lane * 16);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) *reinterpret_cast<u32x4*>(ring + j * 1024 + lane * 16) = v[j];
+      // read one piece back (another lane's chunk) so the stores are live, as a consumer's fragment read would be
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      x ^= *reinterpret_cast<const u32x4*>(ring + (it & 7) * 1024 + (lane ^ 1) * 16);
+    }
+    piece = (piece + 8 * 61) % npieces;
+  }
+  if constexpr (MODE != 0) {
+    __syncthreads();
+    x = *reinterpret_cast<const u32x4*>(smem + threadIdx.x * 16);
+  }
+  const unsigned rr = x[0] ^ x[1] ^ x[2] ^ x[3];
+  if (rr == 0x9e3779b9u) out[blockIdx.x] = rr;  // data-dependent, practically never taken
+}
+
 }  // namespace vst
+
+extern "C" int vst_probe_fetch(int mode, const void* src, int bytes, int grid, int iters, unsigned* out, void* stream) {
+  if (!src || bytes < 65536 || (bytes & 1023) || grid <= 0 || iters <= 0 || (iters & 7) || !out) return VST_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  switch (mode) {
+    case 0: hipLaunchKernelGGL(vst::probe_fetch_kernel<0>, dim3(grid), dim3(512), 65536, s, src, bytes, iters, out); break;
+    case 1: hipLaunchKernelGGL(vst::probe_fetch_kernel<1>, dim3(grid), dim3(512), 65536, s, src, bytes, iters, out); break;
+    case 2: hipLaunchKernelGGL(vst::probe_fetch_kernel<2>, dim3(grid), dim3(512), 65536, s, src, bytes, iters, out); break;
+    default: return VST_ERR_ARG;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : VST_ERR_LAUNCH;
+}
 
 extern "C" int vst_probe_mfma(int grid, int iters, float* out, void* stream) {
   if (grid <= 0 || iters <= 0 || !out) return VST_ERR_ARG;
