@@ -908,7 +908,7 @@ extern "C" int vst_gemm_lora(const void* x, int ldx, const void* Acat, int ld_ac
   a.stride = 1; a.splits = 1;
   a.p8_bn = bn;
   a.ablate = gemm_ablate_env();  // (reaches the kernel in the diagnostics build only, -DVST_P8_TRACE)
-  a.group_m = 0;
+  a.group_m = gemm_group_env();
   return launch_gemm_p8_lora(a, bn, (hipStream_t)stream);
 }
 

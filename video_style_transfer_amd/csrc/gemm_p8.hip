@@ -621,8 +621,10 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
   const int fr = lane & 15, fq = lane >> 4;
   const int nbm = (p.M + BM - 1) / BM, nbn = (p.N + BN - 1) / BN;
   const int ntiles = nbm * nbn;
+  // grouped order: GROUP_M row panels sweep N together (p.group_m: VST_GEMM_GROUP_M, A/B only; default 8)
+  const int GROUP_M = p.group_m > 0 ? p.group_m : 8;
   auto tile_origin = [&](int t, int& m0, int& n0) {
-    const int GROUP_M = 8, in_group = GROUP_M * nbn;
+    const int in_group = GROUP_M * nbn;
     const int gid = t / in_group, first_m = gid * GROUP_M;
     const int gsize = min(nbm - first_m, GROUP_M);
     m0 = (first_m + (t - gid * in_group) % gsize) * BM;
