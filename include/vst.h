@@ -325,6 +325,10 @@ int vst_probe_hbm_read(const void* src, size_t bytes, int grid, unsigned* out, v
  * 512-thread workgroups, each wave moving `iters` 1-KiB pieces, 8 in flight; mode 0 buffer loads into VGPRs, 1 LDS-DMA
  * into an LDS ring (the 8-phase GEMM's loader), 2 buffer loads + ds_write_b128 (a register-staged loader). */
 int vst_probe_fetch(int mode, const void* src, int bytes, int grid, int iters, unsigned* out, void* stream);
+/* vst_probe_mix: what a loader costs an MFMA stream: `grid` 512-thread workgroups, each wave iterating {issue `pieces`
+ * (0, 2, 4, 8) one-KiB pieces, 32 register-operand 16x16x32 bf16 MFMAs, land the pieces}; mode 1 LDS-DMA, 2 buffer
+ * loads + ds_write_b128.  Time against pieces = 0 is the loader's cost to the matrix core. */
+int vst_probe_mix(int mode, int pieces, const void* src, int bytes, int grid, int iters, float* out, void* stream);
 const char* vst_version(void);
 
 #ifdef __cplusplus

@@ -91,6 +91,7 @@ SIGNATURES = {
     "vst_probe_mfma": (_I, [_I, _I, _P, _P]),
     "vst_probe_hbm_read": (_I, [_P, _S, _I, _P, _P]),
     "vst_probe_fetch": (_I, [_I, _P, _I, _I, _I, _P, _P]),
+    "vst_probe_mix": (_I, [_I, _I, _P, _I, _I, _I, _P, _P]),
     "vst_version": (ctypes.c_char_p, []),
 }
 

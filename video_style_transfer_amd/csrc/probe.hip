@@ -100,7 +100,88 @@ __global__ __launch_bounds__(512) void probe_fetch_kernel(const void* src, int b
   if (rr == 0x9e3779b9u) out[blockIdx.x] = rr;  // data-dependent, practically never taken
 }
 
+// What a loader costs an MFMA stream: one 512-thread workgroup per CU (2 waves per SIMD, as the 8-phase
+// GEMM), every wave iterating {issue P one-KiB pieces, 32 independent-chain v_mfma_f32_16x16x32_bf16 from registers,
+// land the pieces} over an L2-resident region:
+//   MODE 1: LDS-DMA (buffer_load ... lds), the pieces of iteration i waited for (counted vmcnt) one iteration later;
+//   MODE 2: buffer_load into VGPRs for iteration i + 1, ds_write_b128 of iteration i's (landed) registers.
+// P = 0 is the MFMA-only baseline; the difference per iteration is the loader's cost to the matrix core.
+template <int MODE, int P>
+__global__ __launch_bounds__(512) void probe_mix_kernel(const void* src, int bytes, int iters, float* out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const auto r = make_rsrc(src, (uint32_t)bytes);
+  const int npieces = bytes >> 10;
+  int piece = (blockIdx.x * 8 + wid) * 97 % npieces;
+  char* ring = smem + wid * 16384;  // 16 pieces per wave
+  bf16x8 fa, fb;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    fa[i] = (__bf16)(1e-3f * (lane + i));
+    fb[i] = (__bf16)(1e-3f * (lane - i));
+  }
+  f32x4 acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  u32x4 cur[P > 0 ? P : 1], nxt[P > 0 ? P : 1];
+  if constexpr (MODE == 2 && P > 0) {
+#pragma unroll
+    for (int j = 0; j < P; ++j) cur[j] = buf_load16(r, ((piece + j) % npieces) * 1024 + lane * 16);
+  }
+  for (int it = 0; it < iters; ++it) {
+    const int slot = (it & 1) * 8;
+    piece = (piece + 8 * 61) % npieces;
+    if constexpr (MODE == 1 && P > 0) {
+#pragma unroll
+      for (int j = 0; j < P; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            r, (__attribute__((address_space(3))) void*)((__attribute__((address_space(3))) char*)(uintptr_t)(ring + (slot + j) * 1024)),
+            16, ((piece + j) % npieces) * 1024 + lane * 16, 0, 0, 0);
+    }
+    if constexpr (MODE == 2 && P > 0) {
+#pragma unroll
+      for (int j = 0; j < P; ++j) nxt[j] = buf_load16(r, ((piece + j) % npieces) * 1024 + lane * 16);
+    }
+#pragma unroll
+    for (int m = 0; m < 32; ++m) acc[m & 7] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc[m & 7], 0, 0, 0);
+    if constexpr (MODE == 1 && P > 0) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");  // the previous iteration's pieces landed
+    }
+    if constexpr (MODE == 2 && P > 0) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");  // cur (issued one iteration ago) landed
+#pragma unroll
+      for (int j = 0; j < P; ++j) *reinterpret_cast<u32x4*>(ring + (slot + j) * 1024 + lane * 16) = cur[j];
+#pragma unroll
+      for (int j = 0; j < P; ++j) cur[j] = nxt[j];
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  float sacc = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sacc += acc[j][0] + acc[j][1] + acc[j][2] + acc[j][3];
+  if (P > 0) sacc += __uint_as_float(*reinterpret_cast<const uint32_t*>(ring + lane * 16) & 0x007fffffu);
+  if (sacc == 1234.5f) out[blockIdx.x] = sacc;  // never true in practice; keeps everything live
+}
+
 }  // namespace vst
+
+extern "C" int vst_probe_mix(int mode, int pieces, const void* src, int bytes, int grid, int iters, float* out,
+                             void* stream) {
+  if (!src || bytes < 65536 || (bytes & 1023) || grid <= 0 || iters <= 0 || !out) return VST_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+#define VST_MIX(M, P) \
+  hipLaunchKernelGGL((vst::probe_mix_kernel<M, P>), dim3(grid), dim3(512), 131072, s, src, bytes, iters, out)
+  if (mode == 0 || pieces == 0) VST_MIX(1, 0);
+  else if (mode == 1 && pieces == 2) VST_MIX(1, 2);
+  else if (mode == 1 && pieces == 4) VST_MIX(1, 4);
+  else if (mode == 1 && pieces == 8) VST_MIX(1, 8);
+  else if (mode == 2 && pieces == 2) VST_MIX(2, 2);
+  else if (mode == 2 && pieces == 4) VST_MIX(2, 4);
+  else if (mode == 2 && pieces == 8) VST_MIX(2, 8);
+  else return VST_ERR_ARG;
+#undef VST_MIX
+  return hipGetLastError() == hipSuccess ? 0 : VST_ERR_LAUNCH;
+}
 
 extern "C" int vst_probe_fetch(int mode, const void* src, int bytes, int grid, int iters, unsigned* out, void* stream) {
   if (!src || bytes < 65536 || (bytes & 1023) || grid <= 0 || iters <= 0 || (iters & 7) || !out) return VST_ERR_ARG;
