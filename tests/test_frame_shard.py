@@ -65,6 +65,11 @@ def _cpu_worker(rank, world, port, q, F=4):
         gx = sh.gather_frames(x_loc, B, Fl, HW)
         assert torch.equal(gx, X.reshape(-1, C)), "gather_frames layout"
         assert torch.equal(sh.local_frames_of(gx, B, Fl, HW), x_loc), "local_frames_of(gather_frames(x)) != x"
+        # the async form the overlapped all-gather exchange issues per CFG half: each half gathered on its own
+        nbh, rws = B // 2, (B // 2) * Fl * HW
+        halves = [sh.gather_frames_begin(x_loc[i * rws:(i + 1) * rws], nbh, Fl, HW) for i in range(2)]
+        got_g = torch.cat([end() for end, _src in halves])
+        assert torch.equal(got_g, X.reshape(-1, C)), "gather_frames_begin per half != gather_frames"
         # (b'') the overlapped schedule (FrameShard.pipelined: the batch in two halves, each half's exchange issued
         # before the other half computes) gives the one-slice schedule's bits; mid() is a frame-axis op (a running sum
         # over every frame of each pixel), so it only matches if each half really holds all frames of its pixels
@@ -341,9 +346,9 @@ def test_frame_shard_sdxl_cfg_pair_one_gpu(world, F, hw):
 
 
 def _gpu_worker_overlap(rank, world, port, q):
-    """The overlapped exchange (FrameShard(overlap=True): each motion module's CFG pair as two halves whose all-to-alls
-    run under the other half's compute) against the one-slice exchange and against the unsharded forward: the tiny
-    UNet, CFG pair, 8 frames over `world` ranks; all three bit-identical."""
+    """The overlapped exchanges (FrameShard(overlap=True): each motion module's CFG pair as two halves whose all-to-alls
+    -- or, for the north star's all-gather, whose gathers -- run under the other half's compute) against the one-slice
+    exchange and against the unsharded forward: the tiny UNet, CFG pair, 8 frames over `world` ranks; bit-identical."""
     try:
         sys.path.insert(0, ROOT)
         sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -358,17 +363,20 @@ def _gpu_worker_overlap(rank, world, port, q):
         unet = build_unet(cfg, state_dict=sd, device=dev)
         kw = dict(added_cond_kwargs={"text_embeds": pooled.to(dev), "time_ids": tids.to(dev)})
         t = torch.tensor([421.0, 421.0])
-        outs = {}
-        for ov in (True, False):
-            sh = FrameShard(overlap=ov)
-            Fl, f0 = sh.local_frames(F)
-            outs[ov] = unet(lat[:, :, f0:f0 + Fl].contiguous().to(dev), t.to(dev), enc.to(dev), frame_shard=sh,
-                            **kw).sample.float().cpu()
         full = unet(lat.to(dev), t.to(dev), enc.to(dev), fusion_world=world, **kw).sample.float().cpu()
-        same_ov = torch.equal(outs[True], outs[False])
-        same_full = torch.equal(outs[True], full[:, :, f0:f0 + Fl])
-        q.put((rank, "ok" if same_ov and same_full else "fail",
-               f"overlapped == one-slice exchange: {same_ov}; == unsharded: {same_full}"))
+        msgs, ok = [], True
+        for exchange in ("all_to_all", "all_gather"):
+            outs = {}
+            for ov in (True, False):
+                sh = FrameShard(exchange=exchange, overlap=ov)
+                Fl, f0 = sh.local_frames(F)
+                outs[ov] = unet(lat[:, :, f0:f0 + Fl].contiguous().to(dev), t.to(dev), enc.to(dev), frame_shard=sh,
+                                **kw).sample.float().cpu()
+            same_ov = torch.equal(outs[True], outs[False])
+            same_full = torch.equal(outs[True], full[:, :, f0:f0 + Fl])
+            ok = ok and same_ov and same_full
+            msgs.append(f"{exchange}: overlapped == one-slice: {same_ov}; == unsharded: {same_full}")
+        q.put((rank, "ok" if ok else "fail", "; ".join(msgs)))
     except BaseException:  # noqa: BLE001
         import traceback
         q.put((rank, "fail", traceback.format_exc()[-2000:]))

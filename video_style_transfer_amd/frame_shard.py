@@ -126,8 +126,9 @@ class FrameShard:
 
     def __init__(self, group=None, permute: Optional[Permute] = None, exchange: str = "all_to_all",
                  overlap: Optional[bool] = None):
-        """overlap (all_to_all only): run each motion module's batch as two halves whose exchanges overlap the other
-        half's compute (pipelined; same bits).  Default: VST_SHARD_OVERLAP, else on."""
+        """overlap: run each motion module's batch as two halves whose exchanges overlap the other half's compute
+        (all_to_all: pipelined; all_gather: half 1's gather under half 0's module; same bits either way).  Default:
+        VST_SHARD_OVERLAP, else on."""
         if not dist.is_initialized():
             raise RuntimeError("FrameShard needs an initialised torch.distributed process group")
         if exchange not in self.EXCHANGES:
@@ -135,7 +136,7 @@ class FrameShard:
         self.exchange = exchange
         if overlap is None:
             overlap = os.environ.get("VST_SHARD_OVERLAP", "1") != "0"
-        self.overlap = bool(overlap) and exchange == "all_to_all"
+        self.overlap = bool(overlap)
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -206,6 +207,37 @@ class FrameShard:
             else:
                 dist.all_to_all_single(out, inp, group=self.group)
         self._issue(op)
+
+    def _all_gather_begin(self, out: torch.Tensor, src: torch.Tensor):
+        """all_gather_into_tensor(out [world * rows, C], src [rows, C]) issued like _all_to_all_begin; returns its wait."""
+        slot = {}
+
+        def issue():
+            if self.backend != "nccl":  # gloo: list all-gather through host memory (done at issue)
+                parts = [torch.empty(src.shape, dtype=src.dtype) for _ in range(self.world)]
+                dist.all_gather(parts, src.cpu(), group=self.group)
+                out.copy_(torch.cat(parts))
+            else:
+                slot["work"] = dist.all_gather_into_tensor(out, src, group=self.group, async_op=True)
+
+        def wait():
+            w = slot.pop("work", None)
+            if w is not None:
+                w.wait()
+        self._issue(issue)
+        return lambda: self._issue(wait)
+
+    def gather_frames_begin(self, h: torch.Tensor, B: int, Fl: int, HW: int):
+        """gather_frames issued without waiting: returns end() -> rows (b, f_global, p) of the whole clip (the all-gather
+        runs on RCCL's stream until end() makes the compute stream wait for it)."""
+        src = h.contiguous()
+        g = torch.empty((self.world * src.shape[0], src.shape[1]), dtype=src.dtype, device=src.device)
+        wait = self._all_gather_begin(g, src)
+
+        def end():
+            wait()
+            return self._permute(g, (self.world, B, Fl, HW), (1, 0, 2, 3))
+        return end, src
 
     def _all_to_all_begin(self, out: torch.Tensor, inp: torch.Tensor):
         """Issue the all-to-all without making the compute stream wait for it; returns the `wait` to call before `out`

@@ -295,18 +295,31 @@ class MotionModule(nn.Module):
         shard = ctx.shard
         B, G = nimg // ctx.F, self.norm.num_groups
         if shard is not None and shard.world > 1 and shard.exchange == "all_gather":
-            # north-star exchange (frame_shard.py): the whole clip on every rank, this rank's frames kept at the end
+            # north-star exchange (frame_shard.py): the whole clip on every rank, this rank's frames kept at the end.
+            # With overlap, the batch's two halves (the CFG pair) are gathered by two async all-gathers issued up front,
+            # so half 1's gather runs under half 0's module (the gather overlapped with compute)
             Fl, P = ctx.F, shard.world
-            xf = shard.gather_frames(x, B, Fl, HW)
             F = Fl * P
-            part = K.group_norm_frame_partials(xf, B * F, HW, G)
-            h = K.group_norm_apply_partials(xf, B, F, HW, G, self.norm.eps, f32(self.norm.weight),
-                                            f32(self.norm.bias), part, 1)
-            h = self.proj_in.run(h)
             tctx = dataclasses.replace(ctx, F=F)
-            for blk in self.transformer_blocks:
-                h = blk.run(h, B * F, HW, tctx)
-            return self.proj_out.run(shard.local_frames_of(h, B, Fl, HW), residual=x)
+            halves = 2 if shard.overlap and B % 2 == 0 else 1
+            nb, rows = B // halves, (B // halves) * Fl * HW
+            ends = [shard.gather_frames_begin(x[i * rows:(i + 1) * rows], nb, Fl, HW) for i in range(halves)]
+            out = torch.empty_like(x) if halves > 1 else None
+            for i in range(halves):
+                end, _src = ends[i]
+                xf = end()
+                part = K.group_norm_frame_partials(xf, nb * F, HW, G)
+                h = K.group_norm_apply_partials(xf, nb, F, HW, G, self.norm.eps, f32(self.norm.weight),
+                                                f32(self.norm.bias), part, 1)
+                h = self.proj_in.run(h)
+                for blk in self.transformer_blocks:
+                    h = blk.run(h, nb * F, HW, tctx)
+                ends[i] = None
+                if halves == 1:
+                    return self.proj_out.run(shard.local_frames_of(h, nb, Fl, HW), residual=x)
+                self.proj_out.run(shard.local_frames_of(h, nb, Fl, HW), residual=x[i * rows:(i + 1) * rows],
+                                  out=out[i * rows:(i + 1) * rows])
+            return out
         # GroupNorm statistics over every frame of a clip, from per-frame partials merged in one fixed frame order:
         # the same bits whether this process holds the whole clip or a frame shard of it
         part = K.group_norm_frame_partials(x, nimg, HW, G)
