@@ -30,7 +30,7 @@ def timeit(fn, iters=30):
 def main():
     dev = torch.device("cuda")
     g = torch.Generator(device="cpu").manual_seed(0)
-    var = os.environ.get("VST_SA_SELF", "0")
+    var = os.environ.get("SA_LABEL", os.environ.get("VST_SA_SELF", "0"))  # SA_LABEL: a build's name (VST_LIB_AB A/B)
     only = sys.argv[1:]
     for name, nb, heads, N in SHAPES:
         if only and name not in only:

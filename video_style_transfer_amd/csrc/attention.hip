@@ -383,8 +383,15 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(3))) vo
       alpha[qb] = fast_exp2((mrun[qb] - mnew) * scale_log2);
       mrun[qb] = mnew;
       mb[qb] = mnew * scale_log2;
+#ifdef VST_SA_SCALAR
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[d][qb][e] = o[d][qb][e] * alpha[qb];
+#else
 #pragma unroll
       for (int d = 0; d < 4; ++d) o[d][qb] *= alpha[qb];
+#endif
     }
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
