@@ -360,6 +360,26 @@ def test_conv3x3_8phase_bitwise_equals_ring(cuda, K, n, C1, C2, Co, H, W, stride
     check(p8, to_nhwc(ref), name="conv p8")
 
 
+@pytest.mark.parametrize("n,Ci,Co,H,W", [(2, 128, 128, 128, 128), (4, 512, 512, 64, 64), (2, 256, 128, 128, 128)])
+def test_conv3x3_vae_ring128(cuda, K, n, Ci, Co, H, W):
+    """The VAE's Cout = 128 / 512 convs that the 8-phase policy would put on 192-wide tiles run on the ring kernel's
+    256x128 tiles (gemm.hip conv_ring128): the same bits as the 256x256 ring tiles, and fp32 torch's values."""
+    g = torch.Generator().manual_seed(n + Ci + Co + H)
+    x = rnd(n, Ci, H, W, gen=g)
+    w = rnd(Co, Ci, 3, 3, scale=(9 * Ci) ** -0.5, gen=g)
+    b = torch.randn(Co, generator=g) * 0.1
+    args = (to_nhwc(x).to(cuda), n, H, W, wflat(w).to(cuda), b.to(cuda))
+    assert K.gemm_kernel_name(n * H * W, Co, 9 * Ci, 2) == "gemm_ring<256x128,conv>"
+    out = K.conv3x3(*args)
+    K.GEMM_POLICY.update(tile=3, splits=1)
+    try:
+        ring256 = K.conv3x3(*args)
+    finally:
+        K.GEMM_POLICY.update(tile=0, splits=0)
+    assert torch.equal(out, ring256)
+    check(out, to_nhwc(conv_ref(x.float(), w.float(), b)), name="conv ring128")
+
+
 @pytest.mark.parametrize("M,N,Kd", [(2, 1280, 320), (2, 1280, 2816), (2, 13760, 1280), (1, 8, 8), (3, 104, 40),
                                     (5, 640, 1288), (8, 336, 4096)])
 @pytest.mark.parametrize("epi", ["bias", "residual", "gelu", "rowbias"])

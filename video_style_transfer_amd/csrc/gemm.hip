@@ -727,6 +727,13 @@ static int p8_bn(int M, int N, bool geglu) {
   return p8_bn320(M, N, geglu) ? 320 : p8_bn192(M, N, geglu) ? 192 : 256;
 }
 
+
+// Convs whose Cout is a multiple of 128 (not of 320) on which the 8-phase policy would take 192-wide tiles -- the VAE's
+// Cout = 128 convs at 512^2 (a third of every 192-wide tile padding) and its Cout = 512 convs at 64^2 (256x128 tiles fill
+// exactly one round of 256 CUs) -- run on the ring kernel's 256x128 tiles: same k order, same bits, 10-12 % faster
+// per launch (tools/vae_conv_ab.py, profiles/r6_vae_conv_ab.txt).  No UNet conv qualifies (Cout 320 / 640 / 1280 / 4).
+static bool conv_ring128(int M, int N) { return N % 128 == 0 && N % 320 != 0 && p8_bn(M, N, false) == 192; }
+
 }  // namespace vst
 
 // Force the 8-phase kernel's tile width for every later GEMM of this process (256 / 192 / 320 where legal; 0 = the
@@ -1016,6 +1023,7 @@ extern "C" const char* vst_gemm_kernel_name(int M, int N, int K, int kind, int t
   if (kind == 3) return "gemm_kernel<conv_in>";
   if (kind == 2 && tile == 0 && splits <= 1 && p8_conv_env() && K % 576 == 0 && N % 64 == 0 &&
       p8_auto(M, N, K, false)) {
+    if (conv_ring128(M, N)) return "gemm_ring<256x128,conv>";
     const int bn = N % 320 == 0 ? 320 : p8_bn(M, N, false) == 192 ? 192 : 256;
     return bn == 320 ? "gemm_p8<128x320,conv>" : bn == 192 ? "gemm_p8<256x192,conv>" : "gemm_p8<256x256,conv>";
   }
@@ -1104,6 +1112,7 @@ extern "C" int vst_gemm(const void* A, int lda, const void* A2, int lda2, int K1
 // 3x3 conv, padding 1, NHWC.  x1: [nimg,H,W,C1], optional x2: [nimg,H,W,C2] concatenated
 // on channels.  Wt: [Cout][3][3][C1+C2].  stride 1 or 2; upsample=1 applies nearest 2x to
 // the input first (output 2H x 2W).  Output [nimg, OH, OW, Cout] with row stride ldc.
+
 static int conv3x3_impl(const void* x1, int C1, const void* x2, int C2, int nimg, int H, int W, int stride,
                         int upsample, int pad0, const void* Wt, int Cout, const float* bias, const float* row_bias,
                         int row_bias_div, int ld_row_bias, const void* R, int ldr, void* out, int ldc, int tile,
@@ -1139,8 +1148,13 @@ static int conv3x3_impl(const void* x1, int C1, const void* x2, int C2, int nimg
   if (!vec) { tile = 2; splits = 1; }
   // 3x3 convs with both sources a multiple of 64 channels run on the 8-phase kernel (implicit im2col; 128x320 tiles
   // where Cout is a multiple of 320, else the projection policy's width); VST_P8_CONV=0 restores the ring kernel
-  const bool p8 = vec && tile == 0 && splits <= 1 && p8_conv_env() && !(C1 & 63) && !((x2 ? C2 : 0) & 63) &&
-                  !(a.N & 63) && p8_auto(a.M, a.N, a.K, false);
+  bool p8 = vec && tile == 0 && splits <= 1 && p8_conv_env() && !(C1 & 63) && !((x2 ? C2 : 0) & 63) &&
+            !(a.N & 63) && p8_auto(a.M, a.N, a.K, false);
+  if (p8 && !colstat && conv_ring128(a.M, a.N)) {
+    p8 = false;
+    tile = 4;
+    splits = 1;
+  }
   if (colstat) {  // column statistics come from the 128x320 tiles' epilogue only
     if (!p8 || a.N % 320) return VST_ERR_UNSUPPORTED;
     a.colstat = colstat;
