@@ -28,6 +28,11 @@ SHAPES = [  # name, M, N, K1, K2, geglu, residual, bias
     ("mm320_ff2", 131072, 320, 1280, 0, False, True, True),
 ]
 TILES = [(0, 0), (8, 1), (3, 1), (6, 1), (7, 1)]  # (tile, splits), 0 = auto
+# VST_TILE_AB_TILES="0:0,1:1,9:1" / VST_TILE_AB_SHAPES="sp1280_out_lora,sp1280_ff2": another tile set / shape subset
+if os.environ.get("VST_TILE_AB_TILES"):
+    TILES = [tuple(int(v) for v in t.split(":")) for t in os.environ["VST_TILE_AB_TILES"].split(",")]
+if os.environ.get("VST_TILE_AB_SHAPES"):
+    SHAPES = [s for s in SHAPES if s[0] in os.environ["VST_TILE_AB_SHAPES"].split(",")]
 
 
 def run(x, x2, w, b, r, geglu, tile):
