@@ -108,6 +108,63 @@ print("rccl whole-graph ok")
 """
 
 
+CHILD_ASYNC = r"""
+import os, sys, time
+t0 = time.time()
+def log(m):
+    print(f"[rccl child {time.time() - t0:6.1f}s] {m}", flush=True)
+import torch, torch.distributed as dist
+sys.path.insert(0, os.environ["VST_ROOT"])
+from video_style_transfer_amd.frame_shard import FrameShard, PiecewiseGraph
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+sh = FrameShard(exchange="all_to_all")
+assert sh.backend == "nccl" and not sh._staged(torch.zeros(1, device=dev))
+n = 1 << 22
+a = torch.zeros(n, device=dev); b = torch.zeros(n, device=dev); c = torch.zeros(3, 5, device=dev)
+ta = torch.empty(n, device=dev); g2 = torch.empty(3, 5, device=dev)
+def step():
+    # FrameShard's overlapped exchange primitives: the collective issued async on RCCL's stream, kernels queued
+    # between the issue and the wait, then the compute stream waits for RCCL's
+    b.mul_(2.0)
+    w1 = sh._all_to_all_begin(ta, b)
+    c.add_(1.0)
+    for _ in range(4):
+        a.mul_(1.0)
+    w1()
+    ta.mul_(3.0)
+    w2 = sh._all_gather_begin(g2, c)
+    a.mul_(2.0)
+    w2()
+    g2.mul_(0.5)
+x = torch.randn(n, device=dev); y = torch.randn(n, device=dev); z = torch.randn(3, 5, device=dev)
+a.copy_(x); b.copy_(y); c.copy_(z)
+step(); torch.cuda.synchronize()
+assert torch.equal(ta, y * 2 * 3) and torch.equal(g2, (z + 1) * 0.5) and torch.equal(a, x * 2)
+log("eager async step ok")
+s = torch.cuda.Stream()
+s.wait_stream(torch.cuda.current_stream())
+pw = PiecewiseGraph()
+pw.capture(step, [sh], s)
+assert pw.num_graphs == 5 and len(pw.items) == 9, (pw.num_graphs, len(pw.items))
+log("captured piecewise: 5 graphs, 2 async issues + 2 waits")
+for it in range(3):
+    x = torch.randn(n, device=dev); y = torch.randn(n, device=dev); z = torch.randn(3, 5, device=dev)
+    a.copy_(x); b.copy_(y); c.copy_(z)
+    pw.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(ta, y * 2 * 3), "async all_to_all_single between graphs"
+    assert torch.equal(g2, (z + 1) * 0.5), "async all_gather_into_tensor between graphs"
+    assert torch.equal(a, x * 2)
+    log(f"replay {it} ok")
+pw.items.clear()
+dist.destroy_process_group()
+log("process group destroyed")
+print("rccl async piecewise ok")
+"""
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -146,3 +203,22 @@ def test_rccl_world1_collectives_captured_then_graph_released_first():
     text = open(out).read()
     print(text[-3000:])
     assert r.returncode == 0 and "rccl whole-graph ok" in text, text[-3000:]
+
+
+@pytest.mark.gpu
+def test_rccl_world1_async_exchange_between_graph_replays():
+    """FrameShard's overlapped-exchange primitives (_all_to_all_begin / _all_gather_begin: async_op=True on RCCL's
+    stream, the wait as a later host item) under piecewise capture with the nccl backend at world 1: the exact code the
+    N-GPU overlapped motion-module schedule runs between its graph pieces, on RCCL before any 8-GPU run."""
+    if torch.cuda.device_count() == 0:
+        pytest.skip("no HIP device")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), VST_ROOT=ROOT,
+               HSA_ENABLE_IPC_MODE_LEGACY="0")
+    out = os.path.join(ROOT, "gpurun_out", "rccl_child_async.log")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    with open(out, "w") as f:
+        r = subprocess.run([sys.executable, "-u", "-c", CHILD_ASYNC], env=env, stdout=f, stderr=subprocess.STDOUT,
+                           timeout=150)
+    text = open(out).read()
+    print(text[-3000:])
+    assert r.returncode == 0 and "rccl async piecewise ok" in text, text[-3000:]
