@@ -33,7 +33,9 @@ int vst_gemm(const void* A, int lda, const void* A2, int lda2, int K1, const voi
              void* C, int ldc, int epilogue, void* stream);
 /* Same, with the tile (0 auto, 1 = 128x128, 2 = 128x64, 3 = 256x256, 4 = 256x128, 5 = skinny N <= 64
  * without epilogue: the UnZipLoRA down-projection) and split-K (0 auto, >= 1 forced) choice and a
- * caller-owned fp32 workspace for split-K slabs (NULL / too small disables split-K). */
+ * caller-owned fp32 workspace for split-K slabs (NULL / too small disables split-K).  An A / A2 / R / C
+ * whose byte extent passes 2^31 - 1 (the kernels' 32-bit buffer offsets) is run as equal row chunks, each row
+ * with the bits of one launch. */
 int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int K1, const void* W, int ldw, int M, int N, int K,
                 const float* bias, const float* row_bias, int row_bias_div, int ld_row_bias, const void* R, int ldr,
                 void* C, int ldc, int epilogue, int tile, int splits, void* workspace, size_t ws_bytes,
@@ -111,7 +113,9 @@ int vst_conv3x3(const void* x1, int C1, const void* x2, int C2, int nimg, int H,
                 const void* Wt, int Cout, const float* bias, const float* row_bias, int row_bias_div, const void* R,
                 int ldr, void* out, int ldc, void* stream);
 /* _ex: + tile / split-K policy and workspace (as vst_gemm_ex) and the row stride of row_bias (0 = Cout), so
- * the time-embedding projections of every ResnetBlock2D can come from ONE batched GEMM output. */
+ * the time-embedding projections of every ResnetBlock2D can come from ONE batched GEMM output.  Inputs /
+ * outputs past 2^31 - 1 bytes run as chunks of whole images (row_bias then must be per image: row_bias_div =
+ * OH * OW; VST_ERR_UNSUPPORTED otherwise). */
 int vst_conv3x3_ex(const void* x1, int C1, const void* x2, int C2, int nimg, int H, int W, int stride, int upsample,
                    const void* Wt, int Cout, const float* bias, const float* row_bias, int row_bias_div,
                    int ld_row_bias, const void* R, int ldr, void* out, int ldc, int tile, int splits, void* workspace,

@@ -761,3 +761,43 @@ def test_ceiling_probes(cuda, K):
     gbs = K.probe_hbm_read_gbs(cuda, nbytes=1 << 30, reps=1)
     assert 500.0 < tf < 3000.0, tf
     assert 1000.0 < gbs < 9000.0, gbs
+
+
+def test_gemm_rows_past_2gb(cuda, K):
+    """An A operand of 2.3 GB (the 64^2 ff.net.2 of an 8-clip CFG batch reads 2.7 GB): the kernels' buffer descriptors
+    take 32-bit byte offsets, so vst_gemm_ex runs such a call as row chunks (gemm.hip row_chunk).  The rows past
+    2 GiB are checked against fp32 torch and bitwise against a launch over those rows alone."""
+    M, Kd, N = 900_000, 1280, 320
+    g = torch.Generator(device=cuda).manual_seed(5)
+    x = torch.randn(M, Kd, generator=g, device=cuda).to(torch.bfloat16)
+    w = (torch.randn(N, Kd, generator=g, device=cuda) * Kd ** -0.5).to(torch.bfloat16)
+    b = torch.randn(N, generator=g, device=cuda) * 0.1
+    r = torch.randn(M, N, generator=g, device=cuda).to(torch.bfloat16)
+    assert (M - 1) * Kd * 2 > 2 ** 31
+    out = K.linear(x, w, b, residual=r)
+    tail = slice(M - 65536, M)
+    alone = K.linear(x[tail].contiguous(), w, b, residual=r[tail].contiguous())
+    torch.cuda.synchronize()
+    assert torch.equal(out[tail], alone)
+    ref = x[tail].float() @ w.float().t() + b + r[tail].float()
+    check(out[tail], ref, name="gemm rows past 2 GiB")
+    head = slice(0, 4096)
+    check(out[head], x[head].float() @ w.float().t() + b + r[head].float(), name="gemm first rows")
+
+
+def test_conv3x3_images_past_2gb(cuda, K):
+    """A conv input of 2.2 GB: vst_conv3x3_ex runs it as chunks of whole images; the last images (past 2 GiB) equal a
+    conv of those 8 images alone (both on the 8-phase kernel), and fp32 torch on the last one."""
+    n, Ci, Co, H, W = 42, 1024, 64, 160, 160
+    g = torch.Generator(device=cuda).manual_seed(6)
+    x = torch.randn(n * H * W, Ci, generator=g, device=cuda).to(torch.bfloat16)
+    w = (torch.randn(Co, Ci, 3, 3, generator=g, device=cuda) * (9 * Ci) ** -0.5).to(torch.bfloat16)
+    b = torch.randn(Co, generator=g, device=cuda) * 0.1
+    assert x.numel() * 2 > 2 ** 31
+    wf = wflat(w.cpu()).to(cuda)
+    out = K.conv3x3(x, n, H, W, wf, b)
+    alone = K.conv3x3(x[(n - 8) * H * W:].contiguous(), 8, H, W, wf, b)
+    torch.cuda.synchronize()
+    assert torch.equal(out[(n - 8) * H * W:], alone)
+    xi = x[(n - 1) * H * W:].float().view(1, H, W, Ci).permute(0, 3, 1, 2)
+    check(out[(n - 1) * H * W:], to_nhwc(conv_ref(xi, w.float(), b)), name="conv image past 2 GiB")

@@ -1051,6 +1051,22 @@ extern "C" const char* vst_gemm_kernel_name(int M, int N, int K, int kind, int t
   return names[tile - 1][kind == 2 ? 2 : kind];
 }
 
+// The kernels address A, A2 and the residual through buffer descriptors with 32-bit byte offsets (clamp_bytes): an
+// operand whose byte extent passes 2^31 - 1 would read zeros past that point.  Such a call (e.g. the motion modules'
+// ff.net.2 at the 64^2 level of an 8-clip CFG batch, A = 1M x 1280 bf16 = 2.7 GB) runs as equal row chunks with
+// offset pointers instead.  The kernels' per-row k order does not depend on M, and chunks this large take the same
+// kernels (no split-K), so every row gets the bits of one launch (test_kernels_gpu.py::test_gemm_rows_past_2gb).
+static size_t row_extent(size_t rows, int ld, int cols) { return ((rows - 1) * (size_t)ld + (size_t)cols) * 2; }
+static int row_chunk(int M, size_t row_bytes, int align) {  // balanced rows per chunk (a multiple of align), 0: none
+  const size_t lim = 0x7fffffffULL;
+  const size_t fit = (lim / row_bytes) / (size_t)align * (size_t)align;
+  if (fit == 0) return 0;
+  const size_t n = ((size_t)M + fit - 1) / fit;
+  const size_t rows = (((size_t)M + n - 1) / n + align - 1) / align * align;
+  return rows <= fit ? (int)rows : (int)fit;
+}
+static int gcd_int(int a, int b) { return b ? gcd_int(b, a % b) : a; }
+
 extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int K1, const void* W, int ldw, int M,
                            int N, int K, const float* bias, const float* row_bias, int row_bias_div, int ld_row_bias,
                            const void* R, int ldr, void* C, int ldc, int epilogue, int tile, int splits,
@@ -1067,6 +1083,28 @@ extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int
   if (epilogue == 2 && (R || row_bias)) return VST_ERR_ARG;  // GELU: bias only
   if (R && (ldr & 7)) return VST_ERR_ARG;
   if (row_bias && row_bias_div <= 0) return VST_ERR_ARG;
+  {
+    const int nout = epilogue == 1 ? N / 2 : N;
+    const size_t lim = 0x7fffffffULL;
+    if (row_extent(M, lda, K1) > lim || (A2 && row_extent(M, lda2, K - K1) > lim) ||
+        (R && row_extent(M, ldr, nout) > lim) || row_extent(M, ldc, nout) > lim) {
+      const int wide = max(max(lda, A2 ? lda2 : 0), max(R ? ldr : 0, ldc));
+      const int align = row_bias ? 256 / gcd_int(256, row_bias_div) * row_bias_div : 256;
+      const int rows = align > 0 ? row_chunk(M, (size_t)wide * 2, align) : 0;
+      if (rows <= 0) return VST_ERR_ARG;
+      const int ldrb = ld_row_bias ? ld_row_bias : N;
+      for (int m0 = 0; m0 < M; m0 += rows) {
+        const int mc = min(rows, M - m0);
+        const int st = vst_gemm_ex(
+            (const char*)A + (size_t)m0 * lda * 2, lda, A2 ? (const char*)A2 + (size_t)m0 * lda2 * 2 : nullptr, lda2,
+            A2 ? K1 : 0, W, ldw, mc, N, K, bias, row_bias ? row_bias + (size_t)(m0 / row_bias_div) * ldrb : nullptr,
+            row_bias_div, ld_row_bias, R ? (const char*)R + (size_t)m0 * ldr * 2 : nullptr, ldr,
+            (char*)C + (size_t)m0 * ldc * 2, ldc, epilogue, tile, splits, workspace, ws_bytes, stream);
+        if (st != VST_OK) return st;
+      }
+      return VST_OK;
+    }
+  }
   if (tile < 0 || tile > 10 || splits < 0) return VST_ERR_ARG;
   if ((tile == 8 || tile == 9 || tile == 10) && !p8_applies(M, N, K1, A2 != nullptr)) return VST_ERR_ARG;
   if ((tile == 9 || tile == 10) && epilogue == 1) return VST_ERR_ARG;  // GEGLU needs the 256-wide tiles
@@ -1128,6 +1166,28 @@ static int conv3x3_impl(const void* x1, int C1, const void* x2, int C2, int nimg
   GemmArgs a{};
   a.OH = upsample ? 2 * H : pad0 ? (H - 2) / 2 + 1 : (stride == 2 ? (H + 1) / 2 : H);
   a.OW = upsample ? 2 * W : pad0 ? (W - 2) / 2 + 1 : (stride == 2 ? (W + 1) / 2 : W);
+  {  // byte extents past the 32-bit buffer offsets (vst_gemm_ex): chunks of whole images (a 3x3 tap never leaves its
+     // image), equal in size
+    const size_t lim = 0x7fffffffULL, hw = (size_t)H * W, ohw = (size_t)a.OH * a.OW;
+    const size_t img_bytes = max(max(hw * C1, x2 ? hw * C2 : 0), max(R ? ohw * ldr : 0, ohw * ldc)) * 2;
+    if ((size_t)nimg * img_bytes > lim) {
+      if (colstat || (row_bias && row_bias_div != (int)ohw)) return VST_ERR_UNSUPPORTED;
+      const int per = (int)(lim / img_bytes);
+      if (per <= 0) return VST_ERR_ARG;
+      const int nch = (nimg + per - 1) / per, ipc = (nimg + nch - 1) / nch;
+      const int ldrb = ld_row_bias ? ld_row_bias : Cout;
+      for (int i0 = 0; i0 < nimg; i0 += ipc) {
+        const int ni = min(ipc, nimg - i0);
+        const int st = conv3x3_impl(
+            (const char*)x1 + (size_t)i0 * hw * C1 * 2, C1, x2 ? (const char*)x2 + (size_t)i0 * hw * C2 * 2 : nullptr,
+            C2, ni, H, W, stride, upsample, pad0, Wt, Cout, bias, row_bias ? row_bias + (size_t)i0 * ldrb : nullptr,
+            row_bias_div, ld_row_bias, R ? (const char*)R + (size_t)i0 * ohw * ldr * 2 : nullptr, ldr,
+            (char*)out + (size_t)i0 * ohw * ldc * 2, ldc, tile, splits, workspace, ws_bytes, stream);
+        if (st != VST_OK) return st;
+      }
+      return VST_OK;
+    }
+  }
   a.pad0 = pad0;
   a.A1 = (const bf16_t*)x1; a.A2 = (const bf16_t*)x2; a.C1 = C1; a.C2 = x2 ? C2 : 0;
   a.H = H; a.W = W; a.stride = stride; a.up = upsample;
