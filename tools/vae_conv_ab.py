@@ -12,6 +12,11 @@ SHAPES = [  # nimg, H, W, Cin, Cout (the SDXL VAE encoder at 512^2, 4-frame chun
     (4, 512, 512, 128, 128), (4, 256, 256, 256, 256), (4, 128, 128, 256, 256), (4, 64, 64, 512, 512),
     (4, 512, 512, 256, 128),
 ]
+if os.environ.get("VST_CONV_AB") == "unet":  # the denoise step's UNet convs (CFG pair x 16 frames = 32 images)
+    SHAPES = [(32, 64, 64, 320, 320), (32, 32, 32, 640, 640), (32, 16, 16, 1280, 1280), (32, 32, 32, 320, 640)]
+TILES = (("auto", 0), ("ring256x128", 4), ("ring256x256", 3), ("auto", 0))
+if os.environ.get("VST_CONV_AB") == "unet":
+    TILES = (("auto", 0), ("ring256x160", 6), ("ring256x256", 3), ("ring256x128", 4), ("auto", 0))
 
 
 def main():
@@ -23,7 +28,7 @@ def main():
         b = torch.randn(co, device=dev, generator=g) * 0.1
         res = {}
         outs = {}
-        for name, tile in (("auto", 0), ("ring256x128", 4), ("ring256x256", 3), ("auto", 0)):
+        for name, tile in TILES:
             K.GEMM_POLICY.update(tile=tile, splits=1 if tile else 0)
             try:
                 for _ in range(2):
