@@ -763,29 +763,40 @@ def test_ceiling_probes(cuda, K):
     assert 1000.0 < gbs < 9000.0, gbs
 
 
-def test_gemm_rows_past_2gb(cuda, K):
+@pytest.mark.parametrize("row_bias", [False, True])
+def test_gemm_rows_past_2gb(cuda, K, row_bias):
     """An A operand of 2.3 GB (the 64^2 ff.net.2 of an 8-clip CFG batch reads 2.7 GB): the kernels' buffer descriptors
-    take 32-bit byte offsets, so vst_gemm_ex runs such a call as row chunks (gemm.hip row_chunk).  The rows past
-    2 GiB are checked against fp32 torch and bitwise against a launch over those rows alone."""
-    M, Kd, N = 900_000, 1280, 320
+    take 32-bit byte offsets, so vst_gemm_ex runs such a call as row chunks (gemm.hip row_chunk; with a row bias the
+    chunks start on its row groups, here 4096-row frames).  The rows past 2 GiB are checked against fp32 torch and
+    bitwise against a launch over those rows alone."""
+    div = 4096
+    M, Kd, N = 220 * div, 1280, 320
     g = torch.Generator(device=cuda).manual_seed(5)
     x = torch.randn(M, Kd, generator=g, device=cuda).to(torch.bfloat16)
     w = (torch.randn(N, Kd, generator=g, device=cuda) * Kd ** -0.5).to(torch.bfloat16)
     b = torch.randn(N, generator=g, device=cuda) * 0.1
     r = torch.randn(M, N, generator=g, device=cuda).to(torch.bfloat16)
+    rb = torch.randn(M // div, N, generator=g, device=cuda) if row_bias else None
+    kw = dict(row_bias=rb, row_bias_div=div) if row_bias else {}
     assert (M - 1) * Kd * 2 > 2 ** 31
-    out = K.linear(x, w, b, residual=r)
-    tail = slice(M - 65536, M)
-    alone = K.linear(x[tail].contiguous(), w, b, residual=r[tail].contiguous())
+    out = K.linear(x, w, b, residual=r, **kw)
+    tail = slice(M - 16 * div, M)
+    kt = dict(row_bias=rb[-16:].contiguous(), row_bias_div=div) if row_bias else {}
+    alone = K.linear(x[tail].contiguous(), w, b, residual=r[tail].contiguous(), **kt)
     torch.cuda.synchronize()
     assert torch.equal(out[tail], alone)
-    ref = x[tail].float() @ w.float().t() + b + r[tail].float()
-    check(out[tail], ref, name="gemm rows past 2 GiB")
-    head = slice(0, 4096)
-    check(out[head], x[head].float() @ w.float().t() + b + r[head].float(), name="gemm first rows")
+
+    def ref(rows):
+        y = x[rows].float() @ w.float().t() + b + r[rows].float()
+        if row_bias:
+            y = y + rb.repeat_interleave(div, 0)[rows]
+        return y
+    check(out[tail], ref(tail), name="gemm rows past 2 GiB")
+    check(out[0:4096], ref(slice(0, 4096)), name="gemm first rows")
 
 
-def test_conv3x3_images_past_2gb(cuda, K):
+@pytest.mark.parametrize("row_bias", [False, True])
+def test_conv3x3_images_past_2gb(cuda, K, row_bias):
     """A conv input of 2.2 GB: vst_conv3x3_ex runs it as chunks of whole images; the last images (past 2 GiB) equal a
     conv of those 8 images alone (both on the 8-phase kernel), and fp32 torch on the last one."""
     n, Ci, Co, H, W = 42, 1024, 64, 160, 160
@@ -795,9 +806,13 @@ def test_conv3x3_images_past_2gb(cuda, K):
     b = torch.randn(Co, generator=g, device=cuda) * 0.1
     assert x.numel() * 2 > 2 ** 31
     wf = wflat(w.cpu()).to(cuda)
-    out = K.conv3x3(x, n, H, W, wf, b)
-    alone = K.conv3x3(x[(n - 8) * H * W:].contiguous(), 8, H, W, wf, b)
+    rb = torch.randn(n, Co, generator=g, device=cuda) if row_bias else None  # per image (the resnets' temb)
+    kw = dict(row_bias=rb, row_bias_div=H * W) if row_bias else {}
+    out = K.conv3x3(x, n, H, W, wf, b, **kw)
+    kt = dict(row_bias=rb[n - 8:].contiguous(), row_bias_div=H * W) if row_bias else {}
+    alone = K.conv3x3(x[(n - 8) * H * W:].contiguous(), 8, H, W, wf, b, **kt)
     torch.cuda.synchronize()
     assert torch.equal(out[(n - 8) * H * W:], alone)
     xi = x[(n - 1) * H * W:].float().view(1, H, W, Ci).permute(0, 3, 1, 2)
-    check(out[(n - 1) * H * W:], to_nhwc(conv_ref(xi, w.float(), b)), name="conv image past 2 GiB")
+    ref = to_nhwc(conv_ref(xi, w.float(), b)) + (rb[n - 1] if row_bias else 0)
+    check(out[(n - 1) * H * W:], ref, name="conv image past 2 GiB")
