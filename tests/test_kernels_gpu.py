@@ -816,3 +816,18 @@ def test_conv3x3_images_past_2gb(cuda, K, row_bias):
     xi = x[(n - 1) * H * W:].float().view(1, H, W, Ci).permute(0, 3, 1, 2)
     ref = to_nhwc(conv_ref(xi, w.float(), b)) + (rb[n - 1] if row_bias else 0)
     check(out[(n - 1) * H * W:], ref, name="conv image past 2 GiB")
+
+
+def test_unchunked_entry_points_refuse_past_2gb(cuda, K):
+    """Entry points that do not chunk (attention here) refuse operands past the kernels' 32-bit buffer offsets with
+    VST_ERR_ARG instead of computing on the zeros those offsets would read (vst_common.h Fit31)."""
+    from video_style_transfer_amd._lib import VstError
+    heads, Nq, Nk = 10, 4096, 77
+    nb = 420  # q: 1.72M rows x 640 bf16 = 2.2 GB
+    q = torch.empty(nb * Nq, heads * 64, dtype=torch.bfloat16, device=cuda)
+    kv = torch.zeros(nb * Nk, heads * 64, dtype=torch.bfloat16, device=cuda)
+    o = torch.empty(1, heads * 64, dtype=torch.bfloat16, device=cuda).expand(nb * Nq, heads * 64)
+    assert (nb * Nq - 1) * heads * 64 * 2 > 2 ** 31
+    with pytest.raises(VstError, match="status 1"):
+        K.spatial_attention(q, kv, kv, nb, heads, Nq, Nk, out=o)
+    torch.cuda.synchronize()

@@ -1130,7 +1130,6 @@ __global__ __launch_bounds__(256, 2) void sa_bwd_dkv_kernel(
   }
 }
 
-static inline uint32_t clampb(size_t b) { return b > 0x7fffffffULL ? 0x7fffffffu : (uint32_t)b; }
 
 template <int NT, int D>
 static int launch_temporal(const bf16_t* Q, const bf16_t* K, const bf16_t* V, int ld, bf16_t* O, int ldo,
@@ -1166,14 +1165,16 @@ extern "C" int vst_sa_self(int on) {
 extern "C" int vst_spatial_attention(const void* q, int ldq, const void* k, const void* v, int ldkv, void* o,
                                      int ldo, int nbatch, int heads, int Nq, int Nk, int kv_div, int head_dim,
                                      float scale, float* lse, void* stream) {
+  Fit31 fit;
   if (head_dim != 64 || !q || !k || !v || !o || nbatch <= 0 || heads <= 0 || Nq <= 0 || Nk <= 0 || kv_div <= 0)
     return VST_ERR_ARG;
   if ((ldq & 7) || (ldkv & 7) || (ldo & 7) || nbatch % kv_div) return VST_ERR_ARG;
   const int nqb = (Nq + 127) / 128;
   const int nkv = nbatch / kv_div;
-  const uint32_t qb = clampb(((size_t)(nbatch * Nq - 1) * ldq + heads * 64) * 2);
+  const uint32_t qb = fit(((size_t)(nbatch * Nq - 1) * ldq + heads * 64) * 2);
   // K and V may be column views of one fused buffer; each rsrc is sized from its own base
-  const uint32_t kvb_v = clampb(((size_t)(nkv * Nk - 1) * ldkv + heads * 64) * 2);
+  const uint32_t kvb_v = fit(((size_t)(nkv * Nk - 1) * ldkv + heads * 64) * 2);
+  if (fit.over) return VST_ERR_ARG;  // past the 32-bit buffer offsets: refuse, never read zeros
   const int nt = (Nk + SA_KT - 1) / SA_KT;
   static int pre_env = -1;  // VST_SA_PRELOAD=0 disables the whole-K/V preload (A/B diagnostics)
   if (pre_env < 0) {
@@ -1215,11 +1216,13 @@ extern "C" int vst_spatial_attention(const void* q, int ldq, const void* k, cons
 // transformers' CLIPTextTransformer): query i attends to keys 0..i.  Same kernel as vst_spatial_attention.
 extern "C" int vst_causal_attention(const void* q, int ldq, const void* k, const void* v, int ldkv, void* o, int ldo,
                                     int nbatch, int heads, int N, int head_dim, float scale, void* stream) {
+  Fit31 fit;
   if (head_dim != 64 || !q || !k || !v || !o || nbatch <= 0 || heads <= 0 || N <= 0) return VST_ERR_ARG;
   if ((ldq & 7) || (ldkv & 7) || (ldo & 7)) return VST_ERR_ARG;
   const int nqb = (N + 127) / 128;
-  const uint32_t qb = clampb(((size_t)(nbatch * N - 1) * ldq + heads * 64) * 2);
-  const uint32_t kvb = clampb(((size_t)(nbatch * N - 1) * ldkv + heads * 64) * 2);
+  const uint32_t qb = fit(((size_t)(nbatch * N - 1) * ldq + heads * 64) * 2);
+  const uint32_t kvb = fit(((size_t)(nbatch * N - 1) * ldkv + heads * 64) * 2);
+  if (fit.over) return VST_ERR_ARG;  // past the 32-bit buffer offsets: refuse, never read zeros
   const dim3 grid(nqb * heads * nbatch);
   hipLaunchKernelGGL(spatial_attn_kernel<0>, grid, dim3(256), SA_LDS, (hipStream_t)stream, (const bf16_t*)q, ldq,
                      (const bf16_t*)k, (const bf16_t*)v, ldkv, (bf16_t*)o, ldo, nbatch, heads, N, N, 1,
@@ -1229,9 +1232,11 @@ extern "C" int vst_causal_attention(const void* q, int ldq, const void* k, const
 
 extern "C" int vst_temporal_attention(const void* q, const void* k, const void* v, int ldqkv, void* o, int ldo,
                                       int nclip, int F, int HW, int heads, int head_dim, float scale, void* stream) {
+  Fit31 fit;
   if (!q || !k || !v || !o || nclip <= 0 || F <= 0 || F > 32 || HW <= 0 || heads <= 0) return VST_ERR_ARG;
   if ((ldqkv & 7) || (ldo & 7) || (head_dim & 7)) return VST_ERR_ARG;
-  const uint32_t bytes = clampb(((size_t)(nclip * F * HW - 1) * ldqkv + heads * head_dim) * 2);
+  const uint32_t bytes = fit(((size_t)(nclip * F * HW - 1) * ldqkv + heads * head_dim) * 2);
+  if (fit.over) return VST_ERR_ARG;  // past the 32-bit buffer offsets: refuse, never read zeros
   const float sl2 = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
   const bf16_t *Q = (const bf16_t*)q, *K = (const bf16_t*)k, *V = (const bf16_t*)v;
@@ -1257,13 +1262,15 @@ extern "C" int vst_temporal_attention(const void* q, const void* k, const void* 
 extern "C" int vst_temporal_attention_bwd(const void* q, const void* k, const void* v, int ldqkv, const void* dout,
                                           int lddo, void* dq, void* dk, void* dv, int lddqkv, int nclip, int F, int HW,
                                           int heads, int head_dim, float scale, void* stream) {
+  Fit31 fit;
   if (!q || !k || !v || !dout || !dq || !dk || !dv || nclip <= 0 || F <= 0 || F > 32 || HW <= 0 || heads <= 0)
     return VST_ERR_ARG;
   if ((ldqkv & 7) || (lddo & 7) || (lddqkv & 3) || (head_dim & 7)) return VST_ERR_ARG;
   const size_t units = (size_t)nclip * HW * heads;
   if (units > 0x7fffffffULL) return VST_ERR_ARG;
-  const uint32_t qkvb = clampb(((size_t)(nclip * F * HW - 1) * ldqkv + heads * head_dim) * 2);
-  const uint32_t dob = clampb(((size_t)(nclip * F * HW - 1) * lddo + heads * head_dim) * 2);
+  const uint32_t qkvb = fit(((size_t)(nclip * F * HW - 1) * ldqkv + heads * head_dim) * 2);
+  const uint32_t dob = fit(((size_t)(nclip * F * HW - 1) * lddo + heads * head_dim) * 2);
+  if (fit.over) return VST_ERR_ARG;  // past the 32-bit buffer offsets: refuse, never read zeros
   const float sl2 = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
   const bf16_t *Q = (const bf16_t*)q, *K = (const bf16_t*)k, *V = (const bf16_t*)v, *G = (const bf16_t*)dout;
@@ -1303,6 +1310,7 @@ extern "C" int vst_spatial_attention_bwd(const void* q, int ldq, const void* k, 
                                          int ldo, const void* dout, int lddo, const float* lse, void* dq, int lddq,
                                          void* dk, void* dv, int lddkv, int nbatch, int heads, int Nq, int Nk,
                                          int kv_div, int head_dim, float scale, void* workspace, void* stream) {
+  Fit31 fit;
   if (head_dim != 64 || !q || !k || !v || !o || !dout || !lse || !dq || !workspace || nbatch <= 0 || heads <= 0 ||
       Nq <= 0 || Nk <= 0 || kv_div <= 0 || nbatch % kv_div || (!dk) != (!dv))
     return VST_ERR_ARG;
@@ -1311,10 +1319,11 @@ extern "C" int vst_spatial_attention_bwd(const void* q, int ldq, const void* k, 
   float* dvec = (float*)workspace;
   const int nkv = nbatch / kv_div;
   const float sl2 = scale * 1.4426950408889634f;
-  const uint32_t qb = clampb(((size_t)(nbatch * Nq - 1) * ldq + heads * 64) * 2);
-  const uint32_t ob = clampb(((size_t)(nbatch * Nq - 1) * ldo + heads * 64) * 2);
-  const uint32_t dob = clampb(((size_t)(nbatch * Nq - 1) * lddo + heads * 64) * 2);
-  const uint32_t kvb = clampb(((size_t)(nkv * Nk - 1) * ldkv + heads * 64) * 2);
+  const uint32_t qb = fit(((size_t)(nbatch * Nq - 1) * ldq + heads * 64) * 2);
+  const uint32_t ob = fit(((size_t)(nbatch * Nq - 1) * ldo + heads * 64) * 2);
+  const uint32_t dob = fit(((size_t)(nbatch * Nq - 1) * lddo + heads * 64) * 2);
+  const uint32_t kvb = fit(((size_t)(nkv * Nk - 1) * ldkv + heads * 64) * 2);
+  if (fit.over) return VST_ERR_ARG;  // past the 32-bit buffer offsets: refuse, never read zeros
   const int nqb = (Nq + 127) / 128, nkb = (Nk + 127) / 128;
   hipLaunchKernelGGL(sa_bwd_dq_kernel, dim3(nqb * heads * nbatch), dim3(256), 6 * SB_TILE, s, (const bf16_t*)q, ldq,
                      (const bf16_t*)k, (const bf16_t*)v, ldkv, (const bf16_t*)o, ldo, (const bf16_t*)dout, lddo, lse,

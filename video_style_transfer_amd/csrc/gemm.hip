@@ -565,7 +565,6 @@ static int launch_one(const GemmArgs& a, hipStream_t s, int splits) {
   return hipGetLastError() == hipSuccess ? VST_OK : VST_ERR_LAUNCH;
 }
 
-static inline uint32_t clamp_bytes(size_t b) { return b > 0x7fffffffULL ? 0x7fffffffu : (uint32_t)b; }
 
 constexpr int kCUs = 256;
 
@@ -897,6 +896,7 @@ extern "C" int vst_gemm_lora_supported(int M, int N, int K, int P, int group_n, 
 extern "C" int vst_gemm_lora(const void* x, int ldx, const void* Acat, int ld_acat, int P, int group_n, int group_r,
                              const void* W, int ldw, int M, int N, int K, const float* bias, const void* R, int ldr,
                              void* C, int ldc, void* stream) {
+  Fit31 fit;
   if (!x || !Acat || !W || !C || M <= 0 || N <= 0 || K <= 0) return VST_ERR_ARG;
   if ((ldx & 7) || (ld_acat & 7) || (ldw & 7) || (ldc & 7) || ldx < K || ld_acat < K || ldw < K + P) return VST_ERR_ARG;
   if (R && ((ldr & 7) || ldr < N)) return VST_ERR_ARG;
@@ -906,12 +906,13 @@ extern "C" int vst_gemm_lora(const void* x, int ldx, const void* Acat, int ld_ac
   a.A1 = (const bf16_t*)x; a.A2 = nullptr; a.lda1 = ldx; a.lda2 = 0; a.K1 = K;
   a.Wt = (const bf16_t*)W; a.ldw = ldw; a.M = M; a.N = N; a.K = K;
   a.bias = bias; a.R = (const bf16_t*)R; a.ldr = ldr; a.C = (bf16_t*)C; a.ldc = ldc;
-  a.a1_bytes = clamp_bytes(((size_t)(M - 1) * ldx + K) * 2);
-  a.w_bytes = clamp_bytes(((size_t)(N - 1) * ldw + K) * 2);
-  a.wtail_bytes = clamp_bytes(((size_t)(N - 1) * ldw + K + P) * 2);
-  a.r_bytes = R ? clamp_bytes(((size_t)(M - 1) * ldr + N) * 2) : 0;
+  a.a1_bytes = fit(((size_t)(M - 1) * ldx + K) * 2);
+  a.w_bytes = fit(((size_t)(N - 1) * ldw + K) * 2);
+  a.wtail_bytes = fit(((size_t)(N - 1) * ldw + K + P) * 2);
+  a.r_bytes = R ? fit(((size_t)(M - 1) * ldr + N) * 2) : 0;
   a.la = (const bf16_t*)Acat; a.lda_la = ld_acat; a.la_p = P; a.la_gn = group_n; a.la_gr = group_r;
-  a.la_bytes = clamp_bytes((size_t)P * ld_acat * 2);
+  a.la_bytes = fit((size_t)P * ld_acat * 2);
+  if (fit.over) return VST_ERR_ARG;  // past the 32-bit buffer offsets (not chunked here): refuse
   a.stride = 1; a.splits = 1;
   a.p8_bn = bn;
   a.ablate = gemm_ablate_env();  // (reaches the kernel in the diagnostics build only, -DVST_P8_TRACE)
@@ -946,6 +947,7 @@ extern "C" int vst_gemm_cross_attention(const void* x, int ldx, const void* Acat
                                         int group_r, const void* W, int ldw, const float* bias, int M, int N, int K,
                                         const void* Kt, const void* Vt, int ldkv, int nkv_rows, int Nq, int Nk,
                                         int kv_div, float scale, void* O, int ldo, void* stream) {
+  Fit31 fit;
   if (!x || !W || !Kt || !Vt || !O || M <= 0 || N <= 0 || K <= 0 || kv_div <= 0 || nkv_rows <= 0) return VST_ERR_ARG;
   if ((ldx & 7) || (ldw & 7) || (ldo & 7) || (ldkv & 7) || ldx < K || ldo < N || ldkv < N) return VST_ERR_ARG;
   if (Acat && ((ld_acat & 7) || ld_acat < K || ldw < K + P)) return VST_ERR_ARG;
@@ -956,16 +958,17 @@ extern "C" int vst_gemm_cross_attention(const void* x, int ldx, const void* Acat
   a.A1 = (const bf16_t*)x; a.lda1 = ldx; a.K1 = K;
   a.Wt = (const bf16_t*)W; a.ldw = ldw; a.M = M; a.N = N; a.K = K;
   a.bias = bias; a.C = (bf16_t*)O; a.ldc = ldo;
-  a.a1_bytes = clamp_bytes(((size_t)(M - 1) * ldx + K) * 2);
-  a.w_bytes = clamp_bytes(((size_t)(N - 1) * ldw + K) * 2);
+  a.a1_bytes = fit(((size_t)(M - 1) * ldx + K) * 2);
+  a.w_bytes = fit(((size_t)(N - 1) * ldw + K) * 2);
   if (Acat) {
-    a.wtail_bytes = clamp_bytes(((size_t)(N - 1) * ldw + K + P) * 2);
+    a.wtail_bytes = fit(((size_t)(N - 1) * ldw + K + P) * 2);
     a.la = (const bf16_t*)Acat; a.lda_la = ld_acat; a.la_p = P; a.la_gn = group_n; a.la_gr = group_r;
-    a.la_bytes = clamp_bytes((size_t)P * ld_acat * 2);
+    a.la_bytes = fit((size_t)P * ld_acat * 2);
   }
   a.xa_k = (const bf16_t*)Kt; a.xa_v = (const bf16_t*)Vt; a.xa_ldkv = ldkv; a.xa_nk = Nk; a.xa_nq = Nq;
   a.xa_kvdiv = kv_div; a.xa_scale_log2 = scale * 1.4426950408889634f;
-  a.xa_kv_bytes = clamp_bytes(((size_t)(nkv_rows - 1) * ldkv + N) * 2);
+  a.xa_kv_bytes = fit(((size_t)(nkv_rows - 1) * ldkv + N) * 2);
+  if (fit.over) return VST_ERR_ARG;  // past the 32-bit buffer offsets (not chunked here): refuse
   a.stride = 1; a.splits = 1; a.p8_bn = 192;
   a.ablate = gemm_ablate_env();  // (diagnostics build only)
   return launch_gemm_p8_xattn(a, (hipStream_t)stream);
@@ -990,6 +993,7 @@ extern "C" int vst_gemm_temporal_attention_supported(int M, int K, int nclip, in
 extern "C" int vst_gemm_temporal_attention(const void* x, int ldx, const void* Wt, int ldw, const float* bias, int M,
                                            int K, int nclip, int F, int HW, int heads, int head_dim, float scale,
                                            void* O, int ldo, void* stream) {
+  Fit31 fit;
   if (!x || !Wt || !O || M <= 0 || K <= 0) return VST_ERR_ARG;
   if ((ldx & 7) || (ldw & 7) || (ldo & 7) || ldx < K || ldw < K || ldo < heads * head_dim) return VST_ERR_ARG;
   if (!tattn_ok(M, K, nclip, F, HW, heads, head_dim)) return VST_ERR_UNSUPPORTED;
@@ -998,8 +1002,9 @@ extern "C" int vst_gemm_temporal_attention(const void* x, int ldx, const void* W
   a.A1 = (const bf16_t*)x; a.lda1 = ldx; a.K1 = K;
   a.Wt = (const bf16_t*)Wt; a.ldw = ldw; a.M = M; a.N = N; a.K = K;
   a.bias = bias; a.C = (bf16_t*)O; a.ldc = ldo;
-  a.a1_bytes = clamp_bytes(((size_t)(M - 1) * ldx + K) * 2);
-  a.w_bytes = clamp_bytes(((size_t)(N - 1) * ldw + K) * 2);
+  a.a1_bytes = fit(((size_t)(M - 1) * ldx + K) * 2);
+  a.w_bytes = fit(((size_t)(N - 1) * ldw + K) * 2);
+  if (fit.over) return VST_ERR_ARG;  // past the 32-bit buffer offsets (not chunked here): refuse
   a.ta_hw = HW; a.ta_heads = heads; a.ta_d = head_dim; a.ta_scale_log2 = scale * 1.4426950408889634f;
   a.stride = 1; a.splits = 1; a.p8_bn = 256;
   return launch_gemm_p8_tattn(a, (hipStream_t)stream);
@@ -1051,7 +1056,7 @@ extern "C" const char* vst_gemm_kernel_name(int M, int N, int K, int kind, int t
   return names[tile - 1][kind == 2 ? 2 : kind];
 }
 
-// The kernels address A, A2 and the residual through buffer descriptors with 32-bit byte offsets (clamp_bytes): an
+// The kernels address A, A2 and the residual through buffer descriptors with 32-bit byte offsets (Fit31): an
 // operand whose byte extent passes 2^31 - 1 would read zeros past that point.  Such a call (e.g. the motion modules'
 // ff.net.2 at the 64^2 level of an 8-clip CFG batch, A = 1M x 1280 bf16 = 2.7 GB) runs as equal row chunks with
 // offset pointers instead.  The kernels' per-row k order does not depend on M, and chunks this large take the same
@@ -1071,6 +1076,7 @@ extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int
                            int N, int K, const float* bias, const float* row_bias, int row_bias_div, int ld_row_bias,
                            const void* R, int ldr, void* C, int ldc, int epilogue, int tile, int splits,
                            void* workspace, size_t ws_bytes, void* stream) {
+  Fit31 fit;
   if (!A || !W || !C || M <= 0 || N <= 0 || K <= 0) return VST_ERR_ARG;
   if ((K & 7) || (lda & 7) || (ldw & 7) || (ldc & 7)) return VST_ERR_ARG;
   if (A2) {
@@ -1117,10 +1123,11 @@ extern "C" int vst_gemm_ex(const void* A, int lda, const void* A2, int lda2, int
   a.bias = bias; a.rbias = row_bias; a.rbias_div = row_bias_div; a.ldrb = ld_row_bias;
   a.R = (const bf16_t*)R; a.ldr = ldr; a.C = (bf16_t*)C; a.ldc = ldc;
   a.ws = (float*)workspace;
-  a.a1_bytes = clamp_bytes(((size_t)(M - 1) * lda + K1) * 2);
-  a.a2_bytes = A2 ? clamp_bytes(((size_t)(M - 1) * lda2 + (K - K1)) * 2) : 0;
-  a.w_bytes = clamp_bytes(((size_t)(N - 1) * ldw + K) * 2);
-  a.r_bytes = R ? clamp_bytes(((size_t)(M - 1) * ldr + N) * 2) : 0;
+  a.a1_bytes = fit(((size_t)(M - 1) * lda + K1) * 2);
+  a.a2_bytes = A2 ? fit(((size_t)(M - 1) * lda2 + (K - K1)) * 2) : 0;
+  a.w_bytes = fit(((size_t)(N - 1) * ldw + K) * 2);
+  a.r_bytes = R ? fit(((size_t)(M - 1) * ldr + N) * 2) : 0;
+  if (fit.over) return VST_ERR_ARG;  // (A / R / C are chunked above; a weight past 2^31 - 1 bytes is refused)
   a.C1 = 0; a.C2 = 0; a.stride = 1; a.up = 0;
   a.act = epilogue == 2 ? 1 : 0;
   if (epilogue == 2) epilogue = 0;
@@ -1155,6 +1162,7 @@ static int conv3x3_impl(const void* x1, int C1, const void* x2, int C2, int nimg
                         int upsample, int pad0, const void* Wt, int Cout, const float* bias, const float* row_bias,
                         int row_bias_div, int ld_row_bias, const void* R, int ldr, void* out, int ldc, int tile,
                         int splits, void* workspace, size_t ws_bytes, void* stream, float* colstat = nullptr) {
+  Fit31 fit;
   if (!x1 || !Wt || !out || nimg <= 0 || H <= 0 || W <= 0 || Cout <= 0) return VST_ERR_ARG;
   if (pad0 && (stride != 2 || H < 2 || W < 2)) return VST_ERR_ARG;
   if (stride != 1 && stride != 2) return VST_ERR_ARG;
@@ -1200,10 +1208,11 @@ static int conv3x3_impl(const void* x1, int C1, const void* x2, int C2, int nimg
   a.bias = bias; a.rbias = row_bias; a.rbias_div = row_bias_div; a.ldrb = ld_row_bias ? ld_row_bias : Cout;
   a.R = (const bf16_t*)R; a.ldr = ldr; a.C = (bf16_t*)out; a.ldc = ldc;
   a.ws = (float*)workspace;
-  a.a1_bytes = clamp_bytes((size_t)nimg * H * W * C1 * 2);
-  a.a2_bytes = x2 ? clamp_bytes((size_t)nimg * H * W * C2 * 2) : 0;
-  a.w_bytes = clamp_bytes((size_t)Cout * a.K * 2);
-  a.r_bytes = R ? clamp_bytes(((size_t)(a.M - 1) * ldr + Cout) * 2) : 0;
+  a.a1_bytes = fit((size_t)nimg * H * W * C1 * 2);
+  a.a2_bytes = x2 ? fit((size_t)nimg * H * W * C2 * 2) : 0;
+  a.w_bytes = fit((size_t)Cout * a.K * 2);
+  a.r_bytes = R ? fit(((size_t)(a.M - 1) * ldr + Cout) * 2) : 0;
+  if (fit.over) return VST_ERR_ARG;  // (A / R / C are chunked above; a weight past 2^31 - 1 bytes is refused)
   if ((ldc & 7) && Cout >= 8) return VST_ERR_ARG;
   if (!vec) { tile = 2; splits = 1; }
   // 3x3 convs with both sources a multiple of 64 channels run on the 8-phase kernel (implicit im2col; 128x320 tiles
@@ -1265,14 +1274,16 @@ extern "C" int vst_conv3x3_down_pad0(const void* x, int C, int nimg, int H, int 
 // head_dim 512, fp32 in the reference: inference_animatediff.py:164-169).
 extern "C" int vst_gemm_f32out(const void* A, int lda, const void* W, int ldw, int M, int N, int K, float* C,
                                void* stream) {
+  Fit31 fit;
   if (!A || !W || !C || M <= 0 || N <= 0 || K <= 0) return VST_ERR_ARG;
   if ((K & 7) || (lda & 7) || (ldw & 7) || (N & 3)) return VST_ERR_ARG;
   GemmArgs a{};
   a.A1 = (const bf16_t*)A; a.lda1 = lda; a.lda2 = lda; a.K1 = K;
   a.Wt = (const bf16_t*)W; a.ldw = ldw; a.M = M; a.N = N; a.K = K;
   a.C = nullptr; a.ldc = N; a.ws = C; a.splits = 1; a.stride = 1;
-  a.a1_bytes = clamp_bytes(((size_t)(M - 1) * lda + K) * 2);
-  a.w_bytes = clamp_bytes(((size_t)(N - 1) * ldw + K) * 2);
+  a.a1_bytes = fit(((size_t)(M - 1) * lda + K) * 2);
+  a.w_bytes = fit(((size_t)(N - 1) * ldw + K) * 2);
+  if (fit.over) return VST_ERR_ARG;  // past the 32-bit buffer offsets (not chunked here): refuse
   int tile = 0, splits = 1;
   choose(M, N, K, 0, 0, 0, tile, splits);
   if (tile == 8) tile = 3;

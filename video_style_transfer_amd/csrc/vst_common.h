@@ -19,6 +19,20 @@ typedef uint16_t bf16_t;  // storage type of a bf16 in global memory
 // Offset that is always outside every buffer resource: buffer loads return 0.
 constexpr int kOOB = 0x7ffffff0;
 
+// Host side: the byte size of a buffer descriptor, with a flag for extents past 2^31 - 1 (the kernels' 32-bit
+// offsets would read zeros there).  An entry point that is not chunked refuses such a call (VST_ERR_ARG) instead of
+// computing on zeros.
+struct Fit31 {
+  bool over = false;
+  uint32_t operator()(size_t bytes) {
+    if (bytes > 0x7fffffffULL) {
+      over = true;
+      return 0x7fffffffu;
+    }
+    return (uint32_t)bytes;
+  }
+};
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
