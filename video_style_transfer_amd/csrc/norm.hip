@@ -1077,6 +1077,7 @@ extern "C" int vst_layernorm_lora(const void* x, int ldx, int C, int rows, const
                                   float eps, const void* A, int R, void* y, int ldy, void* u, int ldu, void* stream) {
   if (!x || !y || !u || !A || !gamma || !beta || rows <= 0 || C <= 0 || (C & 31) || C > 1280) return VST_ERR_ARG;
   if (R <= 0 || R > 64 || (R & 15) || (ldx & 7) || (ldy & 7) || (ldu & 3) || ldu < R) return VST_ERR_ARG;
+  if (((size_t)(rows - 1) * ldx + C) * 2 > 0x7fffffffULL) return VST_ERR_ARG;  // x through a 32-bit buffer offset
   const dim3 grid((rows + 16 * VST_LNL_MI - 1) / (16 * VST_LNL_MI)), blk(512);
   hipStream_t s = (hipStream_t)stream;
 #define VST_LNL(NJ, MT)                                                                                         \
