@@ -300,6 +300,14 @@ int vst_colsum(const void* x, int ldx, int M, int N, float* y, void* workspace, 
  * stride-2 conv without padding.  Output [nimg, (H-2)/2+1, (W-2)/2+1, Cout], row stride ldc. */
 int vst_conv3x3_down_pad0(const void* x, int C, int nimg, int H, int W, const void* Wt, int Cout, const float* bias,
                           void* out, int ldc, void* workspace, size_t ws_bytes, void* stream);
+/* C[N][K] (bf16, row stride ldc) = A^T B with A [M][N] and B [M][K] row-major over M tokens: the training step's
+ * weight gradients (dW = g^T x, dA = s v^T x, dB = s g^T u; autograd.py, the backward of train_animatediff.py:265-319)
+ * without transposed copies of either operand.  fp32 accumulation; the token range splits over workgroups and the
+ * fp32 partials (workspace of vst_gemm_tn_workspace_bytes, may be 0) are summed in a fixed order.  N, K, lda, ldb
+ * multiples of 8. */
+size_t vst_gemm_tn_workspace_bytes(int M, int N, int K);
+int vst_gemm_tn(const void* A, int lda, const void* B, int ldb, int M, int N, int K, void* C, int ldc,
+                void* workspace, size_t ws_bytes, void* stream);
 /* vst_gemm_f32out: C[M][N] = A[M][K] . W[N][K]^T left in fp32 (row stride N).  The mid-block attention's scores
  * (one head of dim 512 over the latent's h*w tokens) feed vst_softmax_rows unrounded, as the fp32 reference's do. */
 int vst_gemm_f32out(const void* A, int lda, const void* W, int ldw, int M, int N, int K, float* C, void* stream);

@@ -831,3 +831,19 @@ def test_unchunked_entry_points_refuse_past_2gb(cuda, K):
     with pytest.raises(VstError, match="status 1"):
         K.spatial_attention(q, kv, kv, nb, heads, Nq, Nk, out=o)
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("M,N,Kc", [(262144, 320, 320), (65536, 640, 640), (20000, 1280, 1280), (4096, 2560, 320),
+                                    (1000, 32, 640), (300, 1280, 32), (16384, 1280, 5120), (77, 64, 8)])
+def test_gemm_tn_vs_torch(cuda, K, M, N, Kc):
+    """vst_gemm_tn (the training step's weight gradients, C = a^T b over M tokens) against fp32 torch: token tails
+    (M not a multiple of 64), N / K not multiples of 128, the split-token fp32 partials and the direct bf16 path."""
+    g = torch.Generator(device=cuda).manual_seed(M + N)
+    a = torch.randn(M, N, generator=g, device=cuda).to(torch.bfloat16)
+    b = (torch.randn(M, Kc, generator=g, device=cuda) * M ** -0.5).to(torch.bfloat16)
+    out = K.linear_tn(a, b)
+    ref = a.float().t() @ b.float()
+    check(out, ref, name=f"gemm_tn {M}x{N}x{Kc}")
+    again = K.linear_tn(a, b)
+    torch.cuda.synchronize()
+    assert torch.equal(out, again)  # deterministic (fixed-order split sum)

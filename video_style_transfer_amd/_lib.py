@@ -83,6 +83,8 @@ SIGNATURES = {
     "vst_temporal_attention_bwd": (_I, [_P, _P, _P, _I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P]),
     "vst_conv3x3_down_pad0": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P, _S, _P]),
     "vst_gemm_f32out": (_I, [_P, _I, _P, _I, _I, _I, _I, _P, _P]),
+    "vst_gemm_tn": (_I, [_P, _I, _P, _I, _I, _I, _I, _P, _I, _P, _S, _P]),
+    "vst_gemm_tn_workspace_bytes": (_S, [_I, _I, _I]),
     "vst_softmax_rows": (_I, [_P, _I, _I, _I, _F, _P, _I, _P]),
     "vst_nchw_to_nhwc": (_I, [_P, _I, _I, _I, _F, _P, _I, _P]),
     "vst_nhwc_to_nchw": (_I, [_P, _I, _I, _I, _I, _P, _P]),

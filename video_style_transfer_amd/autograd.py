@@ -7,8 +7,10 @@ proj_in/out unfrozen).  With g = dL/dy (bf16, tokens x out):
     forward   u = x A^T (skinny GEMM)            y = [x | u] . [W | s B]^T + b      (one fused GEMM)
     backward  v = g B                            dX = [g | v] . [W^T | s A^T]^T     (one fused GEMM)
               dA = s v^T x,  dB = s g^T u,  db = g^T 1 (a ones row appended to u^T),  dW = g^T x
-The weight-side products contract over the token axis, so g, x, u, v are transposed once (vst_transpose) into
-[features, tokens] operands for the ring GEMM; W^T is cached per weight version when W is frozen.
+The weight-side products contract over the token axis: vst_gemm_tn reads g, x, u, v as they lie ([tokens,
+features]) and reads both MFMA operands transposed from the LDS (`_tdot`); only the largest gradient outputs keep the
+older form (both operands transposed by vst_transpose into [features, tokens], then the split-K ring GEMM), which is
+faster there (tools/tn_bench.py).  W^T is cached per weight version when W is frozen.
 Gradients come out of bf16 MFMA GEMMs with fp32 accumulation (as under the reference's bf16 autocast) and are
 cast to the parameters' dtypes.
 """
@@ -35,6 +37,25 @@ def _wt(W: torch.Tensor) -> torch.Tensor:
         c = (key, K.transpose(W.detach().to(BF16).contiguous()))
         W.__dict__["_vst_wt"] = c
     return c[1]
+
+
+# a^T b over the token axis (weight gradients): vst_gemm_tn up to this many output elements; past it the transposed
+# operands' split-K GEMM measured faster (16384 x 10240 x 1280: 504 vs 594 us; every smaller training shape 1.1-2.9x
+# slower than vst_gemm_tn, profiles/r6_gemm_tn.txt).  VST_GEMM_TN=0: always the transposed form (A/B).
+_TN_MAX_OUT = 8 << 20
+_TN_ON = None
+
+
+def _tdot(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """bf16 [a.shape[1], b.shape[1]] = a^T b for token-major a [M, N], b [M, K]."""
+    global _TN_ON
+    if _TN_ON is None:
+        import os
+        _TN_ON = os.environ.get("VST_GEMM_TN", "1") != "0"
+    if _TN_ON and a.shape[1] * b.shape[1] <= _TN_MAX_OUT:
+        return K.linear_tn(a, b)
+    Mp = (a.shape[0] + 7) // 8 * 8  # the ring GEMM's K granule: zero-padded token columns
+    return K.linear(_transpose_padded(a, Mp), _transpose_padded(b, Mp))
 
 
 def _transpose_padded(t: torch.Tensor, Mp: int) -> torch.Tensor:
@@ -106,31 +127,20 @@ class LoRALinearFn(torch.autograd.Function):
         aug = ctx.aug
         s = ctx.s
         g = g.to(BF16).contiguous()
-        M, N = g.shape
         r = A.shape[0]
-        dev = g.device
         v = K.linear(g, aug.BT, kind="gemm_lora_down", alg_n=r)                # [M, P] = g B
         need_x, need_w, need_b, need_a, need_bb = ctx.needs_input_grad[:5]
         dX = dW = db = dA = dB = None
         if need_x:
             dX = K.linear(g, aug.WT_aug, x2=v, alg_k2=r)                         # [M, in]
-        if need_w or need_b or need_a or need_bb:
-            # the weight-side GEMMs contract over the token axis: pad it to the GEMM's K granule (8) with zeros
-            Mp = (M + 7) // 8 * 8
-            if need_w or need_a:
-                xT = _transpose_padded(x2d, Mp)                                  # [in, Mp]
-            if need_w or need_bb:
-                gT = _transpose_padded(g, Mp)                                    # [N, Mp]
-            if need_w:
-                dW = K.linear(gT, xT).to(W.dtype)                                # [N, in] = g^T x
-            if need_a:
-                vT = _transpose_padded(v, Mp)                                    # [P, Mp]
-                dA = (K.linear(vT, xT)[:r].float() * s).to(A.dtype)             # [r, in] = s v^T x
-            if need_bb:
-                uT = _transpose_padded(u, Mp)                                    # [P, Mp]
-                dB = (K.linear(gT, uT)[:, :r].float() * s).to(B.dtype)          # [N, r] = s g^T u
-            if need_b:
-                db = K.colsum(g).to(ctx.b_dtype)                                 # [N] = g^T 1
+        if need_w:
+            dW = _tdot(g, x2d).to(W.dtype)                                       # [N, in] = g^T x
+        if need_a:
+            dA = (_tdot(v, x2d)[:r].float() * s).to(A.dtype)                    # [r, in] = s v^T x
+        if need_bb:
+            dB = (_tdot(g, u)[:, :r].float() * s).to(B.dtype)                   # [N, r] = s g^T u
+        if need_b:
+            db = K.colsum(g).to(ctx.b_dtype)                                     # [N] = g^T 1
         return dX, dW, db, dA, dB, None, None
 
 
@@ -151,14 +161,12 @@ class PlainLinearFn(torch.autograd.Function):
     def backward(ctx, g):
         x2d, W = ctx.saved_tensors
         g = g.to(BF16).contiguous()
-        M = g.shape[0]
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
         dX = dW = db = None
         if need_x:
             dX = K.linear(g, _wt(W))
         if need_w:
-            Mp = (M + 7) // 8 * 8
-            dW = K.linear(_transpose_padded(g, Mp), _transpose_padded(x2d, Mp)).to(W.dtype)
+            dW = _tdot(g, x2d).to(W.dtype)
         if need_b:
             db = K.colsum(g).to(ctx.b_dtype)
         return dX, dW, db
@@ -287,7 +295,6 @@ class GEGLUFn(torch.autograd.Function):
     def backward(ctx, g):
         (x2d,) = ctx.saved_tensors
         Wi, bi = ctx.geglu.geglu_ops()
-        M = x2d.shape[0]
         p = K.linear(x2d, Wi, bi)                                              # [M, 2Nh] pre-activation
         dp = K.geglu_bwd(p, g.to(BF16).contiguous())
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
@@ -295,8 +302,7 @@ class GEGLUFn(torch.autograd.Function):
         if need_x:
             dX = K.linear(dp, _geglu_wt(ctx.geglu))                            # [M, C] = dp W
         if need_w:
-            Mp = (M + 7) // 8 * 8
-            dW = _deinterleave32(K.linear(_transpose_padded(dp, Mp), _transpose_padded(x2d, Mp))).to(ctx.w_dtype)
+            dW = _deinterleave32(_tdot(dp, x2d)).to(ctx.w_dtype)
         if need_b:
             db = _deinterleave32(K.colsum(dp)).to(ctx.b_dtype)
         return dX, dW, db, None

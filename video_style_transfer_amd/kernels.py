@@ -213,6 +213,27 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
     return out
 
 
+def linear_tn(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """out[N, K] (bf16) = a^T b with a [M, N] and b [M, K] row-major over the M tokens (vst_gemm_tn): the weight
+    gradients of the training backward (dW = g^T x, dA = s v^T x, dB = s g^T u) without transposed copies."""
+    _dev(a, BF16, "a")
+    _dev(b, BF16, "b")
+    M, N = a.shape
+    if b.shape[0] != M:
+        raise _lib.VstError(f"linear_tn: a {tuple(a.shape)} and b {tuple(b.shape)} differ in tokens")
+    K = b.shape[1]
+    if out is None:
+        out = torch.empty((N, K), dtype=BF16, device=a.device)
+    _dev(out, BF16, "out")
+    if out.shape != (N, K):
+        raise _lib.VstError(f"linear_tn: out shape {tuple(out.shape)} != {(N, K)}")
+    wsb = int(_lib.load().vst_gemm_tn_workspace_bytes(M, N, K))
+    ws = torch.empty(max(wsb // 4, 1), dtype=F32, device=a.device) if wsb else None
+    with _Rec("gemm_tn", 2.0 * M * N * K, 2.0 * (M * N + M * K + N * K), lambda: "gemm_tn", (N, K, M)):
+        _lib.call("vst_gemm_tn", _p(a), _ld(a), _p(b), _ld(b), M, N, K, _p(out), _ld(out), _p(ws), wsb, _stream())
+    return out
+
+
 _LORA_BN = {}
 
 
