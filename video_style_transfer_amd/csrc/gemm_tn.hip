@@ -10,7 +10,9 @@
 // ds_read_b64_tr_b16 (the O^T = V^T P^T read of spatial attention), so no transposed copy is ever written.
 //
 // Workgroup: 4 waves (2 x 2) over a 128 (n) x 128 (k) output tile, wave tile 64 x 64 = 4 x 4 accumulators of
-// 16 x 16; the token range splits over `splits` workgroups per tile so the grid fills the chip (the weight grids are
+// 16 x 16; one 32-KiB LDS stage (the next stage waits in registers), so three workgroups share a CU (3-10 % faster
+// per shape than two double-buffered ones, profiles/r6_gemm_tn.txt); the token range splits over `splits`
+// workgroups per tile so the grid fills the chip (the weight grids are
 // 3 x 3 .. 80 x 10 tiles against 20k-260k tokens).  splits == 1 writes bf16 directly; otherwise each split writes
 // its fp32 partial tile and gemm_tn_reduce_kernel sums the splits in index order (deterministic bits).
 #include "attn_common.h"
@@ -20,9 +22,9 @@ namespace vst {
 constexpr int TN_T = 64;                 // tokens per stage
 constexpr int TN_SUB = TN_T * 64 * 2;    // one [64 tokens][64 columns] bf16 sub-tile: 8 KiB
 constexpr int TN_STAGE = 4 * TN_SUB;     // A: columns n0 .. n0+127 (2 sub-tiles), B: k0 .. k0+127 (2)
-constexpr int TN_LDS = 2 * TN_STAGE;     // double-buffered: 64 KiB (two workgroups per CU)
+constexpr int TN_LDS = TN_STAGE;         // one stage (the next one waits in registers): 32 KiB, three workgroups per CU
 
-__global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const bf16_t* __restrict__ A, int lda,
+__global__ __launch_bounds__(256, 3) void gemm_tn_kernel(const bf16_t* __restrict__ A, int lda,
                                                          const bf16_t* __restrict__ B, int ldb, int M, int N, int K,
                                                          int tokens_per_split, uint32_t a_bytes, uint32_t b_bytes,
                                                          bf16_t* __restrict__ C, int ldc, float* __restrict__ ws) {
@@ -84,7 +86,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const bf16_t* __restric
   }
   __syncthreads();
   for (int t = 0; t < nstage; ++t) {
-    const int cur = t & 1;
+    const int cur = 0;
     if (t + 1 < nstage) load(t + 1);
     const char* As = smem + cur * TN_STAGE + wn * TN_SUB;
     const char* Bs = smem + cur * TN_STAGE + (2 + wk) * TN_SUB;
@@ -104,8 +106,11 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const bf16_t* __restric
         for (int nb = 0; nb < 4; ++nb)
           acc[kb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[kb], fa[nb], acc[kb][nb], 0, 0, 0);
     }
-    if (t + 1 < nstage) store(cur ^ 1);
-    __syncthreads();
+    __syncthreads();  // every wave's reads of the stage done
+    if (t + 1 < nstage) {
+      store(0);
+      __syncthreads();
+    }
   }
 
 #pragma unroll
@@ -141,8 +146,8 @@ __global__ __launch_bounds__(256) void gemm_tn_reduce_kernel(const float* __rest
 
 static int tn_splits(int M, int N, int K) {
   const int tiles = ((N + 127) / 128) * ((K + 127) / 128);
-  const int want = (512 + tiles - 1) / tiles;             // about two workgroups per CU
-  const int most = max(1, (M + 255) / 256);               // at least 256 tokens per split
+  const int want = (768 + tiles - 1) / tiles;             // about three workgroups per CU
+  const int most = max(1, (M + 2047) / 2048);             // at least 2048 tokens per split
   return max(1, min(want, most));
 }
 
