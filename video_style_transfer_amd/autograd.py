@@ -40,7 +40,7 @@ def _wt(W: torch.Tensor) -> torch.Tensor:
 
 
 # a^T b over the token axis (weight gradients): vst_gemm_tn up to this many output elements; past it the transposed
-# operands' split-K GEMM measured faster (16384 x 10240 x 1280: 504 vs 594 us; every smaller training shape 1.1-2.9x
+# operands' split-K GEMM measured faster (16384 x 10240 x 1280: 509 vs 671 us; every smaller training shape 1.2-3.4x
 # slower than vst_gemm_tn, profiles/r6_gemm_tn.txt).  VST_GEMM_TN=0: always the transposed form (A/B).
 _TN_MAX_OUT = 8 << 20
 _TN_ON = None
